@@ -1,0 +1,176 @@
+/*
+ * se3icp.h — C-ABI of the MI355X-native SE(3)-ICP engine (libse3icp.so).
+ *
+ * Drop-in boundary for the reference's engine class
+ *   class IterativeSE3Registration   include/iterative_SE3_registration.hpp:27-99
+ * (kenahm/se3-icp).  Plain pointers and sizes only; no C++/torch types.
+ *
+ * Two surfaces:
+ *   1. The object surface mirrors the reference class member for member
+ *      (constructor, setSourceCloud/setTargetCloud, public config fields,
+ *      run_icp / run_se3_icp / run_se3_icp_with_cf / run_se3_pure, and the
+ *      result fields current_estimated_T_, num_iterations_,
+ *      num_pure_se3_iterations_).  A binding for the reference would map each
+ *      call 1:1.
+ *   2. The batch surface registers many independent scan pairs in lockstep on
+ *      one GPU (the loop the reference's benchmark drivers run serially,
+ *      examples/benchmark_kitti.cpp:120-197), from host or device (HBM) buffers.
+ *
+ * Errors: functions return 0 on success and a negative se3icp_status otherwise;
+ * se3icp_status_string() describes a code.  Point arrays are AoS xyz float64
+ * (n*3 doubles), the layout of open3d::geometry::PointCloud::points_.
+ * Matrices are 4x4 row-major float64.
+ */
+#ifndef SE3ICP_H
+#define SE3ICP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SE3ICP_ABI_VERSION 1
+
+typedef enum se3icp_status {
+    SE3ICP_OK = 0,
+    SE3ICP_ERR_INVALID_ARG = -1,
+    SE3ICP_ERR_INVALID_METHOD = -2,   /* name not in the reference's whitelist */
+    SE3ICP_ERR_EMPTY_CLOUD = -3,
+    SE3ICP_ERR_K_TOO_LARGE = -4,      /* number_of_nn_for_LRF above SE3ICP_MAX_KNN */
+    SE3ICP_ERR_NO_DEVICE = -5,        /* no HIP device / kernels not loadable: never a CPU fallback */
+    SE3ICP_ERR_HIP = -6,              /* HIP runtime error */
+    SE3ICP_ERR_NONFINITE = -7,        /* NaN/Inf in the resulting pose */
+    SE3ICP_ERR_OUT_OF_MEMORY = -8
+} se3icp_status;
+
+#define SE3ICP_MAX_KNN 128
+
+/* Registration methods.  Names match examples/run_registration_method.cpp:19-24
+ * ("pt2pt","pt2pl","gicp","se3_pt2pt","se3_pt2pl","se3_gicp") plus the two run
+ * methods the CLI does not expose (run_se3_icp_with_cf, run_se3_pure). */
+typedef enum se3icp_method {
+    SE3ICP_PT2PT = 0,            /* run_icp("pt2pt")       ISR.cpp:473-552 */
+    SE3ICP_PT2PL = 1,            /* run_icp("pt2pl")                        */
+    SE3ICP_GICP = 2,             /* run_icp("gicp")                         */
+    SE3ICP_SE3_PT2PT = 3,        /* run_se3_icp("pt2pt")   ISR.cpp:555-739 */
+    SE3ICP_SE3_PT2PL = 4,        /* run_se3_icp("pt2pl")                    */
+    SE3ICP_SE3_GICP = 5,         /* run_se3_icp("gicp")                     */
+    SE3ICP_SE3_GICP_WITH_CF = 6, /* run_se3_icp_with_cf()  ISR.cpp:742-959 */
+    SE3ICP_SE3_PURE_PT2PT = 7,   /* run_se3_pure("pt2pt")  ISR.cpp:962-1127 */
+    SE3ICP_SE3_PURE_PT2PL = 8,
+    SE3ICP_SE3_PURE_GICP = 9,
+    SE3ICP_NUM_METHODS = 10
+} se3icp_method;
+
+/* Public config fields of IterativeSE3Registration (ISR.hpp:80-95); defaults are
+ * the constructor's (ISR.cpp:334-348). */
+typedef struct se3icp_params {
+    int32_t max_num_iterations;     /* 150   max_num_iterations_       */
+    int32_t max_num_se3_iterations; /* 20    max_num_se3_iterations_   */
+    int32_t number_of_nn_for_LRF;   /* 30    number_of_nn_for_LRF_     */
+    int32_t _reserved;
+    double mse;                     /* 1e-5  mse_                      */
+    double mse_switch_error;        /* 1e-3  mse_switch_error_         */
+    double estimated_overlap;       /* 1.0   estimated_overlap_        */
+    double alpha_rot;               /* 3.0   alpha_rot                 */
+    double beta_transl;             /* 1.0   beta_transl               */
+    double scale_preprocessing;     /* 3.0   scale_preprocessing       */
+} se3icp_params;
+
+/* Result of one registration (the reference's result members, ISR.hpp:85-98). */
+typedef struct se3icp_result {
+    double T[16];                     /* current_estimated_T_ (row-major)       */
+    int32_t num_iterations;           /* num_iterations_                        */
+    int32_t num_pure_se3_iterations;  /* num_pure_se3_iterations_ (-1 for run_icp, as the ctor) */
+    int32_t status;                   /* se3icp_status of this pair             */
+    int32_t num_rechecked;            /* NN queries re-resolved in f64 (diagnostic) */
+    double scaling_factor;            /* 3 / max radius (1 for run_icp)         */
+    double time_setup_ms;             /* normalization + TOLDI + normals (batch wall time) */
+    double time_loop_ms;              /* ICP loop (batch wall time)             */
+    double time_se3_correspondence_search_ms; /* time_se3_correspondence_search_ */
+} se3icp_result;
+
+/* ------------------------------------------------------------- misc */
+int se3icp_abi_version(void);
+const char* se3icp_status_string(int status);
+/* "se3_pt2pl" -> SE3ICP_SE3_PT2PL ...; also "se3_gicp_with_cf", "se3_pure_pt2pt" ...
+ * Returns SE3ICP_ERR_INVALID_METHOD for any other string. */
+int se3icp_method_from_name(const char* name);
+const char* se3icp_method_name(int method);
+void se3icp_default_params(se3icp_params* p);
+/* Number of visible HIP devices (0 if none). */
+int se3icp_device_count(void);
+
+/* ------------------------------------------------------------- object surface
+ * Mirrors IterativeSE3Registration (ISR.hpp:27-99). One object = one pair,
+ * single use, like the reference (its run_* normalize member clouds in place). */
+typedef struct se3icp_registration se3icp_registration;
+
+se3icp_registration* se3icp_registration_new(void);           /* IterativeSE3Registration()   ISR.cpp:334 */
+void se3icp_registration_free(se3icp_registration* r);
+/* setSourceCloud(const PointCloud&) ISR.cpp:358-366 — APPENDS like the reference */
+int se3icp_set_source_cloud(se3icp_registration* r, const double* xyz, int64_t n);
+/* setTargetCloud(const PointCloud&) ISR.cpp:372-376 — appends */
+int se3icp_set_target_cloud(se3icp_registration* r, const double* xyz, int64_t n);
+/* the public config fields */
+se3icp_params* se3icp_params_of(se3icp_registration* r);
+/* run_icp(variant)  ISR.cpp:473 ;  variant in {"pt2pt","pt2pl","gicp"} */
+int se3icp_run_icp(se3icp_registration* r, const char* variant);
+/* run_se3_icp(variant)  ISR.cpp:555 */
+int se3icp_run_se3_icp(se3icp_registration* r, const char* variant);
+/* run_se3_icp_with_cf()  ISR.cpp:742 */
+int se3icp_run_se3_icp_with_cf(se3icp_registration* r);
+/* run_se3_pure(variant)  ISR.cpp:962 */
+int se3icp_run_se3_pure(se3icp_registration* r, const char* variant);
+/* result members */
+int se3icp_get_result(const se3icp_registration* r, se3icp_result* out);
+
+/* ------------------------------------------------------------- batch surface
+ * Register n_pairs independent (source, target) pairs with one method and one
+ * parameter set, on device `device` (HIP ordinal).  Host buffers. */
+int se3icp_register_batch(int device, int32_t n_pairs, const double* const* src_xyz, const int64_t* n_src,
+                          const double* const* tgt_xyz, const int64_t* n_tgt, int method,
+                          const se3icp_params* params, se3icp_result* results);
+
+/* Same, with all clouds already resident in HBM: d_src_xyz / d_tgt_xyz are
+ * device pointers to the concatenation of every pair's AoS xyz; the host arrays
+ * src_off/tgt_off (n_pairs+1 entries) give each pair's point range.
+ * `hip_stream` is a hipStream_t (NULL = the engine's own stream). */
+int se3icp_register_batch_device(int device, int32_t n_pairs, const double* d_src_xyz, const int64_t* src_off,
+                                 const double* d_tgt_xyz, const int64_t* tgt_off, int method,
+                                 const se3icp_params* params, se3icp_result* results, void* hip_stream);
+
+/* Single pair convenience (host buffers). */
+int se3icp_register(int device, const double* src_xyz, int64_t n_src, const double* tgt_xyz, int64_t n_tgt,
+                    int method, const se3icp_params* params, se3icp_result* result);
+
+/* ------------------------------------------------------------- stage surface
+ * One entry point per reference member/free function on the hot path, operating
+ * on host buffers.  They let a caller (and the parity tests) check each stage in
+ * isolation.  All run on device `device`. */
+
+/* computeAllTOLDISE3FramesOMP (ISR.cpp:318-331 -> 241-316): frames [n*16] row-major 4x4. */
+int se3icp_toldi_frames(int device, const double* xyz, int64_t n, int k, double* frames);
+/* KDTreeFlann::SearchKNN of every point against its own cloud: idx [n*k], sorted by (d2, idx). */
+int se3icp_knn_self(int device, const double* xyz, int64_t n, int k, int32_t* idx);
+/* PointCloud::EstimateNormals(KNN k) (ISR.cpp:643, :43): normals [n*3]. */
+int se3icp_estimate_normals(int device, const double* xyz, int64_t n, int k, double* normals);
+/* update_correspondences_raw_flann_SE3 (ISR.cpp:444-470) / update_correspondences_kd_tree_XYZ
+ * (ISR.cpp:402-416): exact 1-NN of nq queries among nd points in `dim` (12 or 3)
+ * dimensions (AoS rows), tie -> lowest index.  idx [nq]; d2 [nq] (may be NULL). */
+int se3icp_nn(int device, const double* query, int64_t nq, const double* data, int64_t nd, int dim,
+              int32_t* idx, double* d2, int32_t* num_rechecked);
+
+/* ------------------------------------------------------------- diagnostics
+ * Not part of the reference boundary: per-kernel GPU times (HIP events) of the
+ * last batch on `device`, used by bench.py for the roofline figures.
+ * out[10] = {sweep_se3_ms, sweep_r3_ms, finalize_ms, recheck_ms, trim_ms, reduce_ms,
+ *            setup_ms, sweep_se3_launches, se3_pairs_evaluated, r3_pairs_evaluated} */
+int se3icp_set_profiling(int device, int on);
+int se3icp_last_kernel_times(int device, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SE3ICP_H */

@@ -1,0 +1,67 @@
+// common.hpp — data layout shared by the HIP kernels and the host engine.
+//
+// HBM layout (one batch = P independent pairs = 2P clouds, all concatenated):
+//   cloud c occupies global point indices [CloudDev.off, CloudDev.off + n).
+//   Every per-point array is SoA with row stride `ld` (= total points, padded):
+//     xyz64[3][ld]   normalized coordinates (source_/target_ after ISR.cpp:576-582)
+//     xyz32[3][ld]   f32 copy for the R3 sweep (centered, see k_setup.hip)
+//     fr64 [12][ld]  alpha/beta-weighted TOLDI SE(3) element as a 12-vector in the
+//                    reference's packing [R00 R10 R20 R01 R11 R21 R02 R12 R22 t0 t1 t2]
+//                    (ISR.cpp:450-453, 613-624)
+//     fr32 [12][ld]  f32 copy of target frames for the SE(3) sweep
+//     nrm64[3][ld], cov64[6][ld] (xx xy xz yy yz zz), conf64[ld]
+// Source clouds are never rewritten inside the loop: the current pose T of a pair
+// is applied on the fly (query = T * M0), see DESIGN.md "Pose on the fly".
+#pragma once
+#include <stdint.h>
+
+namespace se3icp {
+
+constexpr int kMaxKnn = 128;      // SE3ICP_MAX_KNN
+constexpr int kBlock = 256;       // threads per block of the streaming/sweep kernels
+constexpr int kRedVals = 28;      // 21 JTJ upper + 6 JTr + 1 mse-sum (pt2pt reuses the slots)
+
+enum Phase : int32_t { PHASE_IDLE = 0, PHASE_SE3 = 1, PHASE_R3 = 2 };
+enum Estimator : int32_t { EST_PT2PT = 0, EST_PT2PL = 1, EST_GICP = 2 };
+
+struct CloudDev {
+    int32_t off;        // first global point index
+    int32_t n;          // points
+    // uniform grid for the kNN search (k_setup.hip)
+    double org[3];
+    double h, inv_h;
+    int32_t dims[3];
+    int32_t cell_off;   // first cell in the concatenated cell arrays
+    int32_t ncells;
+    int32_t _pad;
+};
+
+// Rewritten by the host every iteration (tiny H2D copy).
+struct PairDev {
+    double T[12];          // accumulated pose, rows 0..2 of the 4x4 (row-major 3x4)
+    double f32_center[3];  // center subtracted from the f32 copies of this pair (R3 sweep)
+    int32_t src, tgt;      // cloud ids
+    int32_t phase;         // Phase
+    int32_t est;           // Estimator
+    int32_t cf;            // run_se3_icp_with_cf weighting / mse
+    int32_t trim;          // 1 if ratio < 1 (threshold key valid)
+    int32_t nkeep;         // floor(float(ratio) * float(ns))
+    int32_t _pad;
+    float tgt_norm12;      // max |target 12-vector| (f32 sweep error bound)
+    float tgt_norm3;       // max |centered target xyz| (f32 R3 error bound)
+};
+
+// Static work table: one entry per 256-query block of every pair.
+struct BlockWork {
+    int32_t pair;
+    int32_t q0;            // first local query index of the block
+};
+
+// NN split candidate (sweep -> finalize)
+struct Cand {
+    float d1;
+    int32_t i1;
+    float d2;
+};
+
+}  // namespace se3icp

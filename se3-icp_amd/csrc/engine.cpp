@@ -1,0 +1,782 @@
+// engine.cpp — host driver (see engine.hpp).
+#include "engine.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+
+namespace se3icp {
+
+namespace {
+
+#define HIPCHK(x)                                                                                   \
+    do {                                                                                            \
+        hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess) {                                                                     \
+            std::fprintf(stderr, "se3icp: HIP error %s at %s:%d (%s)\n", hipGetErrorString(e_), __FILE__, \
+                         __LINE__, #x);                                                             \
+            return SE3ICP_ERR_HIP;                                                                  \
+        }                                                                                           \
+    } while (0)
+
+double wall_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+enum Kind { KIND_ICP, KIND_SE3, KIND_CF, KIND_PURE };
+
+struct MethodInfo {
+    Kind kind;
+    int est;
+};
+
+bool decode_method(int method, MethodInfo* mi) {
+    switch (method) {
+        case SE3ICP_PT2PT: *mi = {KIND_ICP, EST_PT2PT}; return true;
+        case SE3ICP_PT2PL: *mi = {KIND_ICP, EST_PT2PL}; return true;
+        case SE3ICP_GICP: *mi = {KIND_ICP, EST_GICP}; return true;
+        case SE3ICP_SE3_PT2PT: *mi = {KIND_SE3, EST_PT2PT}; return true;
+        case SE3ICP_SE3_PT2PL: *mi = {KIND_SE3, EST_PT2PL}; return true;
+        case SE3ICP_SE3_GICP: *mi = {KIND_SE3, EST_GICP}; return true;
+        case SE3ICP_SE3_GICP_WITH_CF: *mi = {KIND_CF, EST_GICP}; return true;
+        case SE3ICP_SE3_PURE_PT2PT: *mi = {KIND_PURE, EST_PT2PT}; return true;
+        case SE3ICP_SE3_PURE_PT2PL: *mi = {KIND_PURE, EST_PT2PL}; return true;
+        case SE3ICP_SE3_PURE_GICP: *mi = {KIND_PURE, EST_GICP}; return true;
+        default: return false;
+    }
+}
+
+template <class T>
+int pinned(T*& p, size_t& cap, size_t count) {
+    if (cap >= count && p) return 0;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    size_t want = std::max<size_t>(count, 16);
+    if (hipHostMalloc((void**)&p, want * sizeof(T), hipHostMallocDefault) != hipSuccess) {
+        cap = 0;
+        return SE3ICP_ERR_OUT_OF_MEMORY;
+    }
+    cap = want;
+    return 0;
+}
+
+}  // namespace
+
+Engine::Engine(int device) : dev_(device) {
+    for (auto& e : ev_) e = nullptr;
+    ok_ = init() == 0;
+}
+
+int Engine::init() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || dev_ < 0 || dev_ >= n) return SE3ICP_ERR_NO_DEVICE;
+    HIPCHK(hipSetDevice(dev_));
+    HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    for (auto& e : ev_) HIPCHK(hipEventCreate(&e));
+    return 0;
+}
+
+Engine::~Engine() {
+    if (!ok_) return;
+    (void)hipSetDevice(dev_);
+    DevBuf* all[] = {&d_clouds_, &d_setup_, &d_pairs_, &d_cloud_of_, &d_inptr_, &d_in_, &d_xyz64_, &d_xyz32_,
+                     &d_fr64_, &d_fr32_, &d_nrm64_, &d_cov64_, &d_conf64_, &d_knn_, &d_cell_cnt_, &d_cell_start_,
+                     &d_slot_, &d_sidx_, &d_sxyz_, &d_norm12_, &d_norm3_, &d_corr_idx_, &d_corr_dist_, &d_cand_,
+                     &d_flag_list_, &d_flag_count_, &d_trim_key_, &d_red_partial_, &d_red_out_, &d_work_, &d_wb_,
+                     &d_wn_, &d_chunks_, &d_partial_, &d_centers_, &d_scan_tmp_, &d_rechecked_};
+    for (DevBuf* b : all)
+        if (b->p) (void)hipFree(b->p);
+    if (h_pairs_) (void)hipHostFree(h_pairs_);
+    if (h_red_) (void)hipHostFree(h_red_);
+    if (h_partial_) (void)hipHostFree(h_partial_);
+    if (h_rechecked_) (void)hipHostFree(h_rechecked_);
+    for (auto& e : ev_)
+        if (e) (void)hipEventDestroy(e);
+    if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+template <class T>
+T* Engine::ensure(DevBuf& b, size_t count) {
+    const size_t want = std::max<size_t>(count, 1) * sizeof(T);
+    if (b.bytes >= want) return static_cast<T*>(b.p);
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+    const size_t alloc = want + want / 4;
+    if (hipMalloc(&b.p, alloc) != hipSuccess) {
+        b.p = nullptr;
+        return nullptr;
+    }
+    b.bytes = alloc;
+    return static_cast<T*>(b.p);
+}
+
+int Engine::alloc_points(int64_t ntot, int kmax, int nsplit) {
+    if (ntot >= (int64_t)1 << 30) return SE3ICP_ERR_INVALID_ARG;
+    ntot_ = ntot;
+    ld_ = (int)((std::max<int64_t>(ntot, 1) + 63) / 64 * 64);
+    kmax_ = std::max(kmax, 1);
+    nsplit_ = std::max(nsplit, 1);
+    const size_t L = (size_t)ld_;
+    bool ok = ensure<int32_t>(d_cloud_of_, L) && ensure<double>(d_in_, 3 * L) && ensure<double>(d_xyz64_, 3 * L) &&
+              ensure<float>(d_xyz32_, 3 * L) && ensure<double>(d_fr64_, 12 * L) && ensure<float>(d_fr32_, 12 * L) &&
+              ensure<double>(d_nrm64_, 3 * L) && ensure<double>(d_cov64_, 6 * L) && ensure<double>(d_conf64_, L) &&
+              ensure<int32_t>(d_knn_, L * kmax_) && ensure<int32_t>(d_slot_, L) && ensure<int32_t>(d_sidx_, L) &&
+              ensure<double>(d_sxyz_, 3 * L) && ensure<int32_t>(d_corr_idx_, L) && ensure<float>(d_corr_dist_, L) &&
+              ensure<Cand>(d_cand_, L * nsplit_) && ensure<int32_t>(d_flag_list_, L) && ensure<int32_t>(d_flag_count_, 4);
+    return ok ? 0 : SE3ICP_ERR_OUT_OF_MEMORY;
+}
+
+View Engine::view() const {
+    View v{};
+    v.ld = ld_;
+    v.npts = (int32_t)ntot_;
+    v.nclouds = nclouds_;
+    v.npairs = npairs_;
+    v.kmax = kmax_;
+    v.clouds = (CloudDev*)d_clouds_.p;
+    v.setup = (CloudSetup*)d_setup_.p;
+    v.pairs = (PairDev*)d_pairs_.p;
+    v.cloud_of = (int32_t*)d_cloud_of_.p;
+    v.in_ptr = (const double* const*)d_inptr_.p;
+    v.xyz64 = (double*)d_xyz64_.p;
+    v.xyz32 = (float*)d_xyz32_.p;
+    v.fr64 = (double*)d_fr64_.p;
+    v.fr32 = (float*)d_fr32_.p;
+    v.nrm64 = (double*)d_nrm64_.p;
+    v.cov64 = (double*)d_cov64_.p;
+    v.conf64 = (double*)d_conf64_.p;
+    v.knn = (int32_t*)d_knn_.p;
+    v.cell_cnt = (int32_t*)d_cell_cnt_.p;
+    v.cell_start = (int32_t*)d_cell_start_.p;
+    v.slot = (int32_t*)d_slot_.p;
+    v.sidx = (int32_t*)d_sidx_.p;
+    v.sxyz = (double*)d_sxyz_.p;
+    v.norm12_bits = (uint32_t*)d_norm12_.p;
+    v.norm3_bits = (uint32_t*)d_norm3_.p;
+    v.corr_idx = (int32_t*)d_corr_idx_.p;
+    v.corr_dist = (float*)d_corr_dist_.p;
+    v.cand = (Cand*)d_cand_.p;
+    v.nsplit = nsplit_;
+    v.flag_list = (int32_t*)d_flag_list_.p;
+    v.flag_count = (int32_t*)d_flag_count_.p;
+    v.trim_key = (uint64_t*)d_trim_key_.p;
+    v.red_partial = (double*)d_red_partial_.p;
+    v.red_out = (double*)d_red_out_.p;
+    v.work = (const BlockWork*)d_work_.p;
+    v.nwork = nwork_;
+    v.pair_rechecked = (int32_t*)d_rechecked_.p;
+    return v;
+}
+
+// ----------------------------------------------------------------------------- setup
+int Engine::setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool normalize_pairs, double scale_pre,
+                         std::vector<double>* centers_out, std::vector<double>* scales_out, hipStream_t s) {
+    nclouds_ = (int)clouds.size();
+    h_clouds_.assign(nclouds_, CloudDev{});
+    h_setup_.resize(nclouds_);
+    h_chunks_.clear();
+    h_inptr_.assign(nclouds_, nullptr);
+    int64_t off = 0;
+    for (int c = 0; c < nclouds_; ++c) {
+        h_clouds_[c].off = (int32_t)off;
+        h_clouds_[c].n = (int32_t)clouds[c].n;
+        h_setup_[c] = clouds[c].st;
+        for (int64_t p0 = 0; p0 < clouds[c].n; p0 += kChunk) h_chunks_.push_back(ChunkWork{c, (int32_t)p0});
+        off += clouds[c].n;
+    }
+    // inputs
+    double* d_in = (double*)d_in_.p;
+    for (int c = 0; c < nclouds_; ++c) {
+        if (on_device) {
+            h_inptr_[c] = clouds[c].in;
+        } else {
+            double* dst = d_in + 3 * (size_t)h_clouds_[c].off;
+            HIPCHK(hipMemcpyAsync(dst, clouds[c].in, sizeof(double) * 3 * clouds[c].n, hipMemcpyHostToDevice, s));
+            h_inptr_[c] = dst;
+        }
+    }
+    const int nch = (int)h_chunks_.size();
+    if (!ensure<CloudDev>(d_clouds_, nclouds_) || !ensure<CloudSetup>(d_setup_, nclouds_) ||
+        !ensure<ChunkWork>(d_chunks_, nch) || !ensure<const double*>(d_inptr_, nclouds_) ||
+        !ensure<double>(d_partial_, (size_t)nch * 9) || !ensure<double>(d_centers_, 3 * (size_t)nclouds_) ||
+        !ensure<uint32_t>(d_norm12_, nclouds_) || !ensure<uint32_t>(d_norm3_, nclouds_))
+        return SE3ICP_ERR_OUT_OF_MEMORY;
+    if (pinned(h_partial_, h_partial_cap_, (size_t)nch * 9 + 8)) return SE3ICP_ERR_OUT_OF_MEMORY;
+    HIPCHK(hipMemcpyAsync(d_clouds_.p, h_clouds_.data(), sizeof(CloudDev) * nclouds_, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_setup_.p, h_setup_.data(), sizeof(CloudSetup) * nclouds_, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_chunks_.p, h_chunks_.data(), sizeof(ChunkWork) * nch, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_inptr_.p, h_inptr_.data(), sizeof(double*) * nclouds_, hipMemcpyHostToDevice, s));
+    View v = view();
+
+    // 1) ingest: SoA copy + sums + bbox
+    launch_ingest(v, (const ChunkWork*)d_chunks_.p, nch, (double*)d_partial_.p, s);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(h_partial_, d_partial_.p, sizeof(double) * 9 * nch, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::vector<double> cen(3 * nclouds_, 0.0);
+    {
+        std::vector<double> sum(3 * nclouds_, 0.0);
+        for (int k = 0; k < nch; ++k) {
+            const int c = h_chunks_[k].cloud;
+            for (int a = 0; a < 3; ++a) sum[3 * c + a] += h_partial_[9 * k + a];
+        }
+        for (int c = 0; c < nclouds_; ++c)
+            for (int a = 0; a < 3; ++a) cen[3 * c + a] = clouds[c].n > 0 ? sum[3 * c + a] / (double)clouds[c].n : 0.0;
+    }
+    if (centers_out) *centers_out = cen;
+
+    // 2) normalization parameters (ISR.cpp:568-574)
+    if (normalize_pairs) {
+        HIPCHK(hipMemcpyAsync(d_centers_.p, cen.data(), sizeof(double) * 3 * nclouds_, hipMemcpyHostToDevice, s));
+        launch_radius(v, (const ChunkWork*)d_chunks_.p, nch, (const double*)d_centers_.p, (double*)d_partial_.p, s);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(h_partial_, d_partial_.p, sizeof(double) * nch, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        std::vector<double> rad(nclouds_, -1.0);
+        for (int k = 0; k < nch; ++k) rad[h_chunks_[k].cloud] = std::max(rad[h_chunks_[k].cloud], h_partial_[k]);
+        if (scales_out) scales_out->assign(nclouds_ / 2, 1.0);
+        for (int p = 0; p < nclouds_ / 2; ++p) {
+            const double rmax = std::max(rad[2 * p], rad[2 * p + 1]);
+            const double sf = scale_pre * (1.0 / rmax);
+            for (int c = 2 * p; c <= 2 * p + 1; ++c) {
+                for (int a = 0; a < 3; ++a) {
+                    h_setup_[c].norm_center[a] = cen[3 * c + a];
+                    h_setup_[c].f32_center[a] = 0.0;
+                }
+                h_setup_[c].norm_scale = sf;
+            }
+            if (scales_out) (*scales_out)[p] = sf;
+        }
+    } else {
+        for (int c = 0; c < nclouds_; ++c) {
+            // raw coordinates; f32 copies centered on the target (pairs) / own centroid (single clouds)
+            const int cc = (nclouds_ % 2 == 0 && npairs_ > 0) ? (c | 1) : c;
+            for (int a = 0; a < 3; ++a) {
+                h_setup_[c].norm_center[a] = 0.0;
+                h_setup_[c].f32_center[a] = cen[3 * cc + a];
+            }
+            h_setup_[c].norm_scale = 1.0;
+        }
+    }
+    HIPCHK(hipMemcpyAsync(d_setup_.p, h_setup_.data(), sizeof(CloudSetup) * nclouds_, hipMemcpyHostToDevice, s));
+
+    // 3) normalize in place + f32 copy + bbox
+    launch_normalize(v, (const ChunkWork*)d_chunks_.p, nch, (double*)d_partial_.p, s);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(h_partial_, d_partial_.p, sizeof(double) * 7 * nch, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::vector<double> bb(6 * nclouds_);
+    for (int c = 0; c < nclouds_; ++c)
+        for (int a = 0; a < 3; ++a) { bb[6 * c + a] = 1e300; bb[6 * c + 3 + a] = -1e300; }
+    for (int k = 0; k < nch; ++k) {
+        const int c = h_chunks_[k].cloud;
+        for (int a = 0; a < 3; ++a) {
+            bb[6 * c + a] = std::min(bb[6 * c + a], h_partial_[7 * k + a]);
+            bb[6 * c + 3 + a] = std::max(bb[6 * c + 3 + a], h_partial_[7 * k + 3 + a]);
+        }
+    }
+
+    // 4) uniform grid for the clouds that need a kNN list
+    int64_t cells = 0;
+    for (int c = 0; c < nclouds_; ++c) {
+        CloudDev& cl = h_clouds_[c];
+        cl.cell_off = (int32_t)cells;
+        cl.ncells = 0;
+        const int K = h_setup_[c].k_knn;
+        if (K <= 0 || cl.n <= 0) continue;
+        double ext[3], diag2 = 0;
+        for (int a = 0; a < 3; ++a) {
+            ext[a] = std::max(bb[6 * c + 3 + a] - bb[6 * c + a], 0.0);
+            diag2 += ext[a] * ext[a];
+        }
+        const double diag = std::sqrt(diag2);
+        // cell edge ~ the expected k-NN radius of a surface sampled with n points
+        double h = 0.6 * diag * std::sqrt((double)std::min(K, cl.n) / (double)cl.n);
+        if (!(h > 0) || !std::isfinite(h)) h = std::max(diag, 1.0);
+        int64_t d[3];
+        for (int it = 0; it < 200; ++it) {
+            for (int a = 0; a < 3; ++a) d[a] = (int64_t)std::floor(ext[a] / h) + 1;
+            if (d[0] * d[1] * d[2] <= 4 * (int64_t)cl.n + 64) break;
+            h *= 1.26;
+        }
+        for (int a = 0; a < 3; ++a) {
+            cl.org[a] = bb[6 * c + a];
+            cl.dims[a] = (int32_t)d[a];
+        }
+        cl.h = h;
+        cl.inv_h = 1.0 / h;
+        cl.ncells = (int32_t)(d[0] * d[1] * d[2]);
+        cells += cl.ncells;
+    }
+    ncells_ = cells;
+    if (!ensure<int32_t>(d_cell_cnt_, cells + 1) || !ensure<int32_t>(d_cell_start_, cells + 1))
+        return SE3ICP_ERR_OUT_OF_MEMORY;
+    v = view();
+    HIPCHK(hipMemcpyAsync(d_clouds_.p, h_clouds_.data(), sizeof(CloudDev) * nclouds_, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(d_norm12_.p, 0, sizeof(uint32_t) * nclouds_, s));
+    HIPCHK(hipMemsetAsync(d_norm3_.p, 0, sizeof(uint32_t) * nclouds_, s));
+    if (cells > 0) {
+        HIPCHK(hipMemsetAsync(d_cell_cnt_.p, 0, sizeof(int32_t) * (cells + 1), s));
+        launch_grid_count(v, s);
+        size_t tmp = 0;
+        if (launch_grid_scan(v, (int32_t)cells, nullptr, &tmp, s) != 0) return SE3ICP_ERR_HIP;
+        if (!ensure<char>(d_scan_tmp_, tmp)) return SE3ICP_ERR_OUT_OF_MEMORY;
+        tmp = d_scan_tmp_.bytes;
+        if (launch_grid_scan(v, (int32_t)cells, d_scan_tmp_.p, &tmp, s) != 0) return SE3ICP_ERR_HIP;
+        launch_grid_scatter(v, s);
+        launch_knn(v, s);
+        HIPCHK(hipGetLastError());
+    }
+    launch_frames(v, s);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+// ----------------------------------------------------------------------------- batch registration
+int Engine::register_batch(int npairs, const double* const* src, const int64_t* ns, const double* const* tgt,
+                           const int64_t* nt, bool on_device, int method, const se3icp_params& prm,
+                           se3icp_result* out, hipStream_t user_stream) {
+    if (!ok_) return SE3ICP_ERR_NO_DEVICE;
+    if (npairs <= 0 || !src || !tgt || !ns || !nt || !out) return SE3ICP_ERR_INVALID_ARG;
+    MethodInfo mi;
+    if (!decode_method(method, &mi)) return SE3ICP_ERR_INVALID_METHOD;
+    for (int p = 0; p < npairs; ++p) {
+        if (ns[p] <= 0 || nt[p] <= 0) return SE3ICP_ERR_EMPTY_CLOUD;
+        if (!src[p] || !tgt[p]) return SE3ICP_ERR_INVALID_ARG;
+    }
+    const bool se3 = mi.kind != KIND_ICP;
+    const int k_lrf = se3 ? prm.number_of_nn_for_LRF : 0;
+    if (se3 && k_lrf <= 0) return SE3ICP_ERR_INVALID_ARG;
+    int k_nrm_s = 0, k_nrm_t = 0;
+    if (mi.est == EST_PT2PL) k_nrm_t = 30;                    // target_.EstimateNormals() default KNN(30)
+    if (mi.est == EST_GICP) { k_nrm_s = 20; k_nrm_t = 20; }   // InitializePointCloudForGeneralizedICP KNN(20)
+    const int kmax = std::max({k_lrf, k_nrm_s, k_nrm_t, 1});
+    if (kmax > kMaxKnn) return SE3ICP_ERR_K_TOO_LARGE;
+    HIPCHK(hipSetDevice(dev_));
+    hipStream_t s = user_stream ? user_stream : stream_;
+    const double t_begin = wall_ms();
+    ktimes_ = KernelTimes{};
+
+    npairs_ = npairs;
+    int64_t ntot = 0, max_nt = 0;
+    for (int p = 0; p < npairs; ++p) { ntot += ns[p] + nt[p]; max_nt = std::max<int64_t>(max_nt, nt[p]); }
+    // work table: one entry per 256-query block of every pair's source cloud
+    h_work_.clear();
+    h_wb_.assign(npairs, 0);
+    h_wn_.assign(npairs, 0);
+    for (int p = 0; p < npairs; ++p) {
+        h_wb_[p] = (int32_t)h_work_.size();
+        for (int64_t q0 = 0; q0 < ns[p]; q0 += kBlock) h_work_.push_back(BlockWork{p, (int32_t)q0});
+        h_wn_[p] = (int32_t)h_work_.size() - h_wb_[p];
+    }
+    nwork_ = (int)h_work_.size();
+    // target splits: enough blocks to fill 256 CUs several times over
+    int nsplit = (int)std::min<int64_t>(16, std::max<int64_t>(1, (4096 + nwork_ - 1) / nwork_));
+    nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(nsplit, (max_nt + 2047) / 2048));
+    int rc = alloc_points(ntot, kmax, nsplit);
+    if (rc) return rc;
+    if (!ensure<PairDev>(d_pairs_, npairs) || !ensure<BlockWork>(d_work_, nwork_) || !ensure<int32_t>(d_wb_, npairs) ||
+        !ensure<int32_t>(d_wn_, npairs) || !ensure<uint64_t>(d_trim_key_, npairs) ||
+        !ensure<double>(d_red_partial_, (size_t)nwork_ * kRedVals) || !ensure<double>(d_red_out_, (size_t)npairs * kRedVals) ||
+        !ensure<int32_t>(d_rechecked_, npairs))
+        return SE3ICP_ERR_OUT_OF_MEMORY;
+    if (pinned(h_pairs_, h_pairs_cap_, npairs) || pinned(h_red_, h_red_cap_, (size_t)npairs * kRedVals) ||
+        pinned(h_rechecked_, h_rechecked_cap_, npairs))
+        return SE3ICP_ERR_OUT_OF_MEMORY;
+    HIPCHK(hipMemcpyAsync(d_work_.p, h_work_.data(), sizeof(BlockWork) * nwork_, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_wb_.p, h_wb_.data(), sizeof(int32_t) * npairs, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_wn_.p, h_wn_.data(), sizeof(int32_t) * npairs, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(d_rechecked_.p, 0, sizeof(int32_t) * npairs, s));
+
+    // ---- setup (ISR.cpp:568-648)
+    std::vector<CloudReq> clouds(2 * npairs);
+    for (int p = 0; p < npairs; ++p) {
+        for (int side = 0; side < 2; ++side) {
+            CloudReq& r = clouds[2 * p + side];
+            r.in = side == 0 ? src[p] : tgt[p];
+            r.n = side == 0 ? ns[p] : nt[p];
+            CloudSetup& st = r.st;
+            st = CloudSetup{};
+            st.k_lrf = k_lrf;
+            st.k_nrm = side == 0 ? k_nrm_s : k_nrm_t;
+            st.k_knn = std::max(st.k_lrf, st.k_nrm);
+            st.want_cov = mi.est == EST_GICP;
+            st.want_conf = mi.kind == KIND_CF;
+            st.is_target = side == 1;
+            st.cf_target = (mi.kind == KIND_CF && side == 1);
+            st.alpha = prm.alpha_rot;
+            st.beta = prm.beta_transl;
+            st.norm_scale = 1.0;
+        }
+    }
+    std::vector<double> centers, scales;
+    rc = setup_clouds(clouds, on_device, se3, prm.scale_preprocessing, &centers, &scales, s);
+    if (rc) return rc;
+    std::vector<uint32_t> n12(nclouds_), n3(nclouds_);
+    HIPCHK(hipMemcpyAsync(n12.data(), d_norm12_.p, sizeof(uint32_t) * nclouds_, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(n3.data(), d_norm3_.p, sizeof(uint32_t) * nclouds_, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const double t_setup = wall_ms();
+    ktimes_.setup_ms = t_setup - t_begin;
+
+    // ---- per-pair loop state (ISR.cpp:629-651)
+    struct St {
+        M4 T = M4::eye();
+        int iter = 0, pure = 0;
+        bool sw = false, done = false;
+        double mse_prev = 1e7, mse_cur = 1e7, rel = 1e7;
+        double sf = 1.0;
+        int nkeep = 0;
+        bool trim = false;
+    };
+    std::vector<St> st(npairs);
+    const float ratio = std::min(1.0f, std::max(0.0f, (float)prm.estimated_overlap));  // PCL setOverlapRatio(float)
+    for (int p = 0; p < npairs; ++p) {
+        st[p].sf = se3 ? scales[p] : 1.0;
+        const unsigned nv = (unsigned)std::floor(ratio * (float)ns[p]);
+        st[p].nkeep = (int)nv;
+        st[p].trim = (int64_t)nv < ns[p];
+        PairDev& P = h_pairs_[p];
+        std::memset(&P, 0, sizeof(P));
+        P.src = 2 * p;
+        P.tgt = 2 * p + 1;
+        P.est = mi.est;
+        P.cf = mi.kind == KIND_CF;
+        P.trim = st[p].trim;
+        P.nkeep = st[p].nkeep;
+        float f12, f3;
+        std::memcpy(&f12, &n12[2 * p + 1], 4);
+        std::memcpy(&f3, &n3[2 * p + 1], 4);
+        P.tgt_norm12 = f12;
+        P.tgt_norm3 = f3;
+        for (int a = 0; a < 3; ++a) P.f32_center[a] = h_setup_[2 * p].f32_center[a];
+    }
+    View v = view();
+    const int recheck_blocks = 512;
+    double nn_ms = 0;
+    int active = npairs;
+    while (active > 0) {
+        bool any_se3 = false, any_r3 = false, any_trim = false;
+        double se3_pairs = 0, r3_pairs = 0;
+        for (int p = 0; p < npairs; ++p) {
+            PairDev& P = h_pairs_[p];
+            St& S = st[p];
+            if (S.done) { P.phase = PHASE_IDLE; continue; }
+            S.iter++;                                                 // ISR.cpp:656
+            const bool se3_nn = (mi.kind == KIND_PURE) || (se3 && !S.sw);
+            if (se3_nn) S.pure++;                                     // ISR.cpp:660
+            P.phase = se3_nn ? PHASE_SE3 : PHASE_R3;
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 4; ++c) P.T[r * 4 + c] = S.T.m[r][c];
+            any_se3 |= se3_nn;
+            any_r3 |= !se3_nn;
+            any_trim |= S.trim;
+            (se3_nn ? se3_pairs : r3_pairs) += (double)ns[p] * (double)nt[p];
+        }
+        HIPCHK(hipMemcpyAsync(d_pairs_.p, h_pairs_, sizeof(PairDev) * npairs, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemsetAsync(d_flag_count_.p, 0, sizeof(int32_t), s));
+        HIPCHK(hipEventRecord(ev_[0], s));
+        if (any_se3) launch_sweep_se3(v, s);
+        HIPCHK(hipEventRecord(ev_[1], s));
+        if (any_r3) launch_sweep_r3(v, s);
+        HIPCHK(hipEventRecord(ev_[2], s));
+        launch_finalize(v, s);
+        HIPCHK(hipEventRecord(ev_[3], s));
+        launch_recheck(v, recheck_blocks, s);
+        HIPCHK(hipEventRecord(ev_[4], s));
+        if (any_trim) launch_trim(v, s);
+        HIPCHK(hipEventRecord(ev_[5], s));
+        launch_reduce(v, (const int32_t*)d_wb_.p, (const int32_t*)d_wn_.p, s);
+        HIPCHK(hipEventRecord(ev_[6], s));
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(h_red_, d_red_out_.p, sizeof(double) * kRedVals * npairs, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        {
+            float ms[6];
+            for (int k = 0; k < 6; ++k) HIPCHK(hipEventElapsedTime(&ms[k], ev_[k], ev_[k + 1]));
+            ktimes_.sweep_se3_ms += ms[0];
+            ktimes_.sweep_r3_ms += ms[1];
+            ktimes_.finalize_ms += ms[2];
+            ktimes_.recheck_ms += ms[3];
+            ktimes_.trim_ms += ms[4];
+            ktimes_.reduce_ms += ms[5];
+            nn_ms += ms[0] + ms[1] + ms[2] + ms[3];
+            if (any_se3) { ktimes_.sweep_se3_launches++; ktimes_.se3_pairs_evaluated += se3_pairs; }
+            if (any_r3) { ktimes_.sweep_r3_launches++; ktimes_.r3_pairs_evaluated += r3_pairs; }
+        }
+        for (int p = 0; p < npairs; ++p) {
+            St& S = st[p];
+            if (S.done) continue;
+            const double* acc = h_red_ + (size_t)p * kRedVals;
+            const double K = S.trim ? (double)S.nkeep : (double)ns[p];
+            // ISR.cpp:684-686 (mean of the kept distances; NaN when nothing is kept, as the reference)
+            S.mse_prev = S.mse_cur;
+            S.mse_cur = acc[27] / K;
+            S.rel = std::fabs(S.mse_cur - S.mse_prev);
+            // ISR.cpp:689-703 estimator
+            M4 Ti;
+            if (K <= 0) Ti = M4::eye();
+            else if (mi.est == EST_PT2PT) Ti = umeyama_from_moments(acc, acc[15]);
+            else Ti = solve_normal_equations(acc);
+            // ISR.cpp:706-716: the source cloud and its SE(3) elements follow T on the fly
+            const M4 Tprev = S.T;
+            S.T = mul4(Ti, S.T);
+            const double change = frob_diff4(Tprev, S.T);
+            if (mi.kind == KIND_ICP) {  // ISR.cpp:547-550
+                if (S.iter == prm.max_num_iterations || S.rel < prm.mse) S.done = true;
+            } else if (mi.kind == KIND_PURE) {  // ISR.cpp:1118-1119
+                if (S.iter == prm.max_num_se3_iterations || S.rel < S.sf * prm.mse) S.done = true;
+            } else if (!S.sw) {  // ISR.cpp:718-723
+                if (S.iter == prm.max_num_se3_iterations || change < prm.mse_switch_error) S.sw = true;
+            } else {  // ISR.cpp:724-729
+                if (S.iter == prm.max_num_iterations || S.rel < S.sf * prm.mse) S.done = true;
+            }
+            if (S.iter >= 100000) S.done = true;  // the reference would loop forever
+            if (S.done) --active;
+        }
+    }
+    HIPCHK(hipMemcpyAsync(h_rechecked_, d_rechecked_.p, sizeof(int32_t) * npairs, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    const double t_end = wall_ms();
+
+    int worst = 0;
+    for (int p = 0; p < npairs; ++p) {
+        St& S = st[p];
+        M4 T = S.T;
+        if (se3) {  // ISR.cpp:735-738 de-normalization
+            const double* cs = &centers[3 * (2 * p)];
+            const double* ct = &centers[3 * (2 * p + 1)];
+            for (int r = 0; r < 3; ++r) {
+                const double Rc = T.m[r][0] * cs[0] + T.m[r][1] * cs[1] + T.m[r][2] * cs[2];
+                T.m[r][3] = (1.0 / S.sf) * T.m[r][3] - Rc + ct[r];
+            }
+        }
+        se3icp_result& R = out[p];
+        std::memset(&R, 0, sizeof(R));
+        bool finite = true;
+        for (int i = 0; i < 4; ++i)
+            for (int j = 0; j < 4; ++j) {
+                R.T[i * 4 + j] = T.m[i][j];
+                finite &= std::isfinite(T.m[i][j]);
+            }
+        R.num_iterations = S.iter;
+        R.num_pure_se3_iterations = se3 ? S.pure : -1;
+        R.status = finite ? SE3ICP_OK : SE3ICP_ERR_NONFINITE;
+        R.num_rechecked = h_rechecked_[p];
+        R.scaling_factor = S.sf;
+        R.time_setup_ms = t_setup - t_begin;
+        R.time_loop_ms = t_end - t_setup;
+        R.time_se3_correspondence_search_ms = nn_ms;
+        if (R.status != SE3ICP_OK) worst = R.status;
+    }
+    return worst;
+}
+
+// ----------------------------------------------------------------------------- stage entry points
+int Engine::knn_self(const double* xyz, int64_t n, int k, int32_t* idx) {
+    if (!ok_) return SE3ICP_ERR_NO_DEVICE;
+    if (!xyz || !idx || n <= 0) return n <= 0 ? SE3ICP_ERR_EMPTY_CLOUD : SE3ICP_ERR_INVALID_ARG;
+    if (k <= 0) return SE3ICP_ERR_INVALID_ARG;
+    if (k > kMaxKnn) return SE3ICP_ERR_K_TOO_LARGE;
+    HIPCHK(hipSetDevice(dev_));
+    npairs_ = 0;
+    int rc = alloc_points(n, k, 1);
+    if (rc) return rc;
+    std::vector<CloudReq> cl(1);
+    cl[0].in = xyz;
+    cl[0].n = n;
+    cl[0].st.k_knn = k;
+    cl[0].st.norm_scale = 1.0;
+    rc = setup_clouds(cl, false, false, 1.0, nullptr, nullptr, stream_);
+    if (rc) return rc;
+    HIPCHK(hipMemcpy2DAsync(idx, sizeof(int32_t) * k, d_knn_.p, sizeof(int32_t) * kmax_, sizeof(int32_t) * k, n,
+                            hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    return 0;
+}
+
+int Engine::toldi_frames(const double* xyz, int64_t n, int k, double* frames) {
+    if (!ok_) return SE3ICP_ERR_NO_DEVICE;
+    if (!xyz || !frames || n <= 0) return n <= 0 ? SE3ICP_ERR_EMPTY_CLOUD : SE3ICP_ERR_INVALID_ARG;
+    if (k <= 0) return SE3ICP_ERR_INVALID_ARG;
+    if (k > kMaxKnn) return SE3ICP_ERR_K_TOO_LARGE;
+    HIPCHK(hipSetDevice(dev_));
+    npairs_ = 0;
+    int rc = alloc_points(n, k, 1);
+    if (rc) return rc;
+    std::vector<CloudReq> cl(1);
+    cl[0].in = xyz;
+    cl[0].n = n;
+    cl[0].st.k_knn = k;
+    cl[0].st.k_lrf = k;
+    cl[0].st.alpha = 1.0;
+    cl[0].st.beta = 1.0;
+    cl[0].st.norm_scale = 1.0;
+    rc = setup_clouds(cl, false, false, 1.0, nullptr, nullptr, stream_);
+    if (rc) return rc;
+    std::vector<double> fr(12 * (size_t)ld_);
+    HIPCHK(hipMemcpyAsync(fr.data(), d_fr64_.p, sizeof(double) * 12 * ld_, hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    for (int64_t i = 0; i < n; ++i) {
+        double* F = frames + 16 * i;
+        const double* v12[12];
+        for (int r = 0; r < 12; ++r) v12[r] = &fr[(size_t)r * ld_ + i];
+        // packing [R00 R10 R20 R01 R11 R21 R02 R12 R22 t0 t1 t2] -> row-major 4x4
+        for (int r = 0; r < 3; ++r) {
+            for (int c = 0; c < 3; ++c) F[r * 4 + c] = *v12[c * 3 + r];
+            F[r * 4 + 3] = *v12[9 + r];
+        }
+        F[12] = F[13] = F[14] = 0.0;
+        F[15] = 1.0;
+    }
+    return 0;
+}
+
+int Engine::estimate_normals(const double* xyz, int64_t n, int k, double* normals) {
+    if (!ok_) return SE3ICP_ERR_NO_DEVICE;
+    if (!xyz || !normals || n <= 0) return n <= 0 ? SE3ICP_ERR_EMPTY_CLOUD : SE3ICP_ERR_INVALID_ARG;
+    if (k <= 0) return SE3ICP_ERR_INVALID_ARG;
+    if (k > kMaxKnn) return SE3ICP_ERR_K_TOO_LARGE;
+    HIPCHK(hipSetDevice(dev_));
+    npairs_ = 0;
+    int rc = alloc_points(n, k, 1);
+    if (rc) return rc;
+    std::vector<CloudReq> cl(1);
+    cl[0].in = xyz;
+    cl[0].n = n;
+    cl[0].st.k_knn = k;
+    cl[0].st.k_nrm = k;
+    cl[0].st.norm_scale = 1.0;
+    rc = setup_clouds(cl, false, false, 1.0, nullptr, nullptr, stream_);
+    if (rc) return rc;
+    std::vector<double> nr(3 * (size_t)ld_);
+    HIPCHK(hipMemcpyAsync(nr.data(), d_nrm64_.p, sizeof(double) * 3 * ld_, hipMemcpyDeviceToHost, stream_));
+    HIPCHK(hipStreamSynchronize(stream_));
+    for (int64_t i = 0; i < n; ++i)
+        for (int a = 0; a < 3; ++a) normals[3 * i + a] = nr[(size_t)a * ld_ + i];
+    return 0;
+}
+
+int Engine::nn(const double* query, int64_t nq, const double* data, int64_t nd, int dim, int32_t* idx, double* d2,
+               int32_t* num_rechecked) {
+    if (!ok_) return SE3ICP_ERR_NO_DEVICE;
+    if (!query || !data || !idx || (dim != 3 && dim != 12)) return SE3ICP_ERR_INVALID_ARG;
+    if (nq <= 0 || nd <= 0) return SE3ICP_ERR_EMPTY_CLOUD;
+    HIPCHK(hipSetDevice(dev_));
+    hipStream_t s = stream_;
+    npairs_ = 1;
+    nclouds_ = 2;
+    const int64_t ntot = nq + nd;
+    h_work_.clear();
+    for (int64_t q0 = 0; q0 < nq; q0 += kBlock) h_work_.push_back(BlockWork{0, (int32_t)q0});
+    nwork_ = (int)h_work_.size();
+    int nsplit = (int)std::min<int64_t>(16, std::max<int64_t>(1, (4096 + nwork_ - 1) / nwork_));
+    nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(nsplit, (nd + 2047) / 2048));
+    int rc = alloc_points(ntot, 1, nsplit);
+    if (rc) return rc;
+    if (!ensure<PairDev>(d_pairs_, 1) || !ensure<BlockWork>(d_work_, nwork_) || !ensure<CloudDev>(d_clouds_, 2) ||
+        !ensure<int32_t>(d_rechecked_, 1))
+        return SE3ICP_ERR_OUT_OF_MEMORY;
+    h_clouds_.assign(2, CloudDev{});
+    h_clouds_[0].off = 0;
+    h_clouds_[0].n = (int32_t)nq;
+    h_clouds_[1].off = (int32_t)nq;
+    h_clouds_[1].n = (int32_t)nd;
+    // SoA f64 masters + f32 sweep copies, filled on the host (diagnostic entry point)
+    const size_t L = ld_;
+    std::vector<int32_t> cof(L, 0);
+    for (int64_t i = nq; i < ntot; ++i) cof[i] = 1;
+    double cen[3] = {0, 0, 0};
+    if (dim == 3) {
+        for (int64_t j = 0; j < nd; ++j)
+            for (int a = 0; a < 3; ++a) cen[a] += data[3 * j + a];
+        for (int a = 0; a < 3; ++a) cen[a] /= (double)nd;
+    }
+    std::vector<double> m64((size_t)dim * L, 0.0);
+    std::vector<float> m32((size_t)dim * L, 0.f);
+    double nb = 0;
+    for (int64_t i = 0; i < ntot; ++i) {
+        const double* row = i < nq ? query + dim * i : data + dim * (i - nq);
+        double n2 = 0;
+        for (int r = 0; r < dim; ++r) {
+            m64[(size_t)r * L + i] = row[r];
+            const double c = dim == 3 ? row[r] - cen[r] : row[r];
+            m32[(size_t)r * L + i] = (float)c;
+            n2 += c * c;
+        }
+        if (i >= nq) nb = std::max(nb, std::sqrt(n2));
+    }
+    double* dst64 = dim == 12 ? (double*)d_fr64_.p : (double*)d_xyz64_.p;
+    float* dst32 = dim == 12 ? (float*)d_fr32_.p : (float*)d_xyz32_.p;
+    HIPCHK(hipMemcpyAsync(dst64, m64.data(), sizeof(double) * m64.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(dst32, m32.data(), sizeof(float) * m32.size(), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_cloud_of_.p, cof.data(), sizeof(int32_t) * L, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_clouds_.p, h_clouds_.data(), sizeof(CloudDev) * 2, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_work_.p, h_work_.data(), sizeof(BlockWork) * nwork_, hipMemcpyHostToDevice, s));
+    PairDev P;
+    std::memset(&P, 0, sizeof(P));
+    P.T[0] = P.T[5] = P.T[10] = 1.0;
+    P.src = 0;
+    P.tgt = 1;
+    P.phase = dim == 12 ? PHASE_SE3 : PHASE_R3;
+    P.tgt_norm12 = (float)(nb * (1 + 1e-6));
+    P.tgt_norm3 = (float)(nb * (1 + 1e-6));
+    for (int a = 0; a < 3; ++a) P.f32_center[a] = cen[a];
+    HIPCHK(hipMemcpyAsync(d_pairs_.p, &P, sizeof(P), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(d_flag_count_.p, 0, sizeof(int32_t), s));
+    HIPCHK(hipMemsetAsync(d_rechecked_.p, 0, sizeof(int32_t), s));
+    View v = view();
+    if (dim == 12) {
+        // the finalize kernel also reads the translation rows of fr64 for the stored
+        // distance; they are the query/data vectors themselves here.
+        launch_sweep_se3(v, s);
+    } else {
+        launch_sweep_r3(v, s);
+    }
+    launch_finalize(v, s);
+    launch_recheck(v, 512, s);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(idx, d_corr_idx_.p, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, s));
+    int32_t rech = 0;
+    HIPCHK(hipMemcpyAsync(&rech, d_rechecked_.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (num_rechecked) *num_rechecked = rech;
+    if (d2) {
+        for (int64_t i = 0; i < nq; ++i) {
+            const double* a = query + dim * i;
+            const double* b = data + (size_t)dim * idx[i];
+            double r = 0;
+            if (dim == 12) {
+                for (int d = 0; d < 12; d += 4) {
+                    const double d0 = a[d] - b[d], d1 = a[d + 1] - b[d + 1], dd2 = a[d + 2] - b[d + 2], d3 = a[d + 3] - b[d + 3];
+                    r += d0 * d0 + d1 * d1 + dd2 * dd2 + d3 * d3;
+                }
+            } else {
+                const double d0 = a[0] - b[0], d1 = a[1] - b[1], dd2 = a[2] - b[2];
+                r = (d0 * d0 + d1 * d1) + dd2 * dd2;
+            }
+            d2[i] = r;
+        }
+    }
+    return 0;
+}
+
+// ----------------------------------------------------------------------------- engine registry
+Engine* engine_for(int device) {
+    static std::mutex reg_mu;
+    static std::map<int, std::unique_ptr<Engine>> reg;
+    std::lock_guard<std::mutex> lk(reg_mu);
+    auto it = reg.find(device);
+    if (it != reg.end()) return it->second.get();
+    auto e = std::make_unique<Engine>(device);
+    Engine* raw = e.get();
+    reg[device] = std::move(e);
+    return raw;
+}
+
+}  // namespace se3icp

@@ -1,0 +1,112 @@
+// engine.hpp — host driver of the MI355X SE(3)-ICP engine.
+//
+// One Engine per HIP device.  register_batch() runs every pair of a batch in
+// lockstep: each iteration launches one grid per stage covering all active pairs
+// (pairs in the SE(3) phase and pairs already switched to the R3 phase share the
+// iteration), then reads back 28 doubles per pair and does the f64 solve and the
+// reference's switch / convergence logic (ISR.cpp:654-732) on the host.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <stdint.h>
+#include <vector>
+
+#include "hostmath.hpp"
+#include "se3icp.h"
+#include "view.hpp"
+
+namespace se3icp {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+// Per-kernel GPU time of the last register_batch (HIP events, ms), for bench.py.
+struct KernelTimes {
+    double sweep_se3_ms = 0, sweep_r3_ms = 0, finalize_ms = 0, recheck_ms = 0, trim_ms = 0, reduce_ms = 0;
+    double setup_ms = 0;
+    int64_t sweep_se3_launches = 0, sweep_r3_launches = 0;
+    double se3_pairs_evaluated = 0;  // sum over launches of (active queries x targets)
+    double r3_pairs_evaluated = 0;
+};
+
+class Engine {
+  public:
+    explicit Engine(int device);
+    ~Engine();
+    Engine(const Engine&) = delete;
+    Engine& operator=(const Engine&) = delete;
+
+    int device() const { return dev_; }
+    std::mutex& mutex() { return mu_; }
+    void set_profiling(bool on) { profile_ = on; }
+    const KernelTimes& kernel_times() const { return ktimes_; }
+
+    int register_batch(int npairs, const double* const* src, const int64_t* ns, const double* const* tgt,
+                       const int64_t* nt, bool on_device, int method, const se3icp_params& prm,
+                       se3icp_result* out, hipStream_t user_stream);
+
+    // stage entry points (host buffers)
+    int knn_self(const double* xyz, int64_t n, int k, int32_t* idx);
+    int toldi_frames(const double* xyz, int64_t n, int k, double* frames);
+    int estimate_normals(const double* xyz, int64_t n, int k, double* normals);
+    int nn(const double* query, int64_t nq, const double* data, int64_t nd, int dim, int32_t* idx, double* d2,
+           int32_t* num_rechecked);
+
+  private:
+    struct CloudReq {
+        const double* in = nullptr;  // AoS input
+        int64_t n = 0;
+        CloudSetup st{};
+    };
+    int init();
+    template <class T>
+    T* ensure(DevBuf& b, size_t count);
+    int alloc_points(int64_t ntot, int kmax, int nsplit);
+    // ingest -> (normalize) -> grid -> kNN -> frames for a list of clouds.  When
+    // `normalize_pairs` is set, clouds (2p, 2p+1) are normalized together with the
+    // reference's preprocessing and scale[p] receives the factor.
+    int setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool normalize_pairs, double scale_pre,
+                     std::vector<double>* centers, std::vector<double>* scales, hipStream_t s);
+    int upload_tables(hipStream_t s);
+    View view() const;
+
+    int dev_;
+    bool ok_ = false;
+    bool profile_ = false;
+    std::mutex mu_;
+    hipStream_t stream_ = nullptr;
+    KernelTimes ktimes_;
+
+    // geometry of the current batch
+    int nclouds_ = 0, npairs_ = 0;
+    int64_t ntot_ = 0;
+    int ld_ = 0, kmax_ = 1, nsplit_ = 1, nwork_ = 0;
+    int64_t ncells_ = 0;
+    std::vector<CloudDev> h_clouds_;
+    std::vector<CloudSetup> h_setup_;
+    std::vector<BlockWork> h_work_;
+    std::vector<int32_t> h_wb_, h_wn_;
+    std::vector<ChunkWork> h_chunks_;
+    std::vector<const double*> h_inptr_;
+
+    // device buffers
+    DevBuf d_clouds_, d_setup_, d_pairs_, d_cloud_of_, d_inptr_, d_in_, d_xyz64_, d_xyz32_, d_fr64_, d_fr32_, d_nrm64_,
+        d_cov64_, d_conf64_, d_knn_, d_cell_cnt_, d_cell_start_, d_slot_, d_sidx_, d_sxyz_, d_norm12_, d_norm3_,
+        d_corr_idx_, d_corr_dist_, d_cand_, d_flag_list_, d_flag_count_, d_trim_key_, d_red_partial_, d_red_out_,
+        d_work_, d_wb_, d_wn_, d_chunks_, d_partial_, d_centers_, d_scan_tmp_, d_rechecked_;
+    // pinned host mirrors
+    PairDev* h_pairs_ = nullptr;
+    double* h_red_ = nullptr;
+    double* h_partial_ = nullptr;
+    int32_t* h_rechecked_ = nullptr;
+    size_t h_pairs_cap_ = 0, h_red_cap_ = 0, h_partial_cap_ = 0, h_rechecked_cap_ = 0;
+    hipEvent_t ev_[16];
+};
+
+// process-wide engine per device (lazily created)
+Engine* engine_for(int device);
+
+}  // namespace se3icp

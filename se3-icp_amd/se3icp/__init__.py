@@ -1,0 +1,17 @@
+"""se3icp — MI355X-native SE(3)-ICP registration (host side of libse3icp.so).
+
+Drop-in for kenahm/se3-icp's ``IterativeSE3Registration`` (see registration.py);
+the registration itself runs in hand-written HIP kernels for gfx950 (csrc/).
+"""
+from ._lib import (MAX_KNN, METHODS, Params, Result, Se3IcpError, default_params, device_count, load,  # noqa: F401
+                   method_id, status_string)
+from .io import read_ply_xyz, write_ply_xyz  # noqa: F401
+from .registration import (IterativeSE3Registration, PairResult, cli_params, estimate_normals,  # noqa: F401
+                           kitti_params, knn_self, last_kernel_times, lounge_params, nearest_neighbors,
+                           register_batch, register_batch_device, toldi_frames)
+
+__all__ = [
+    "IterativeSE3Registration", "register_batch", "register_batch_device", "toldi_frames", "knn_self",
+    "estimate_normals", "nearest_neighbors", "default_params", "cli_params", "kitti_params", "lounge_params",
+    "read_ply_xyz", "write_ply_xyz", "METHODS", "MAX_KNN", "Se3IcpError",
+]

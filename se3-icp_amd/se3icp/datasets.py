@@ -1,0 +1,240 @@
+"""Seeded synthetic inputs for the benchmark configurations.
+
+The reference's datasets (KITTI seq. 07 downsampled scans, the Stanford lounge
+RGB-D sequence) are not available offline, so the workloads are synthesized with
+the same shape:
+
+* ``kitti_like_sequence``  64-beam rotating LiDAR (HDL-64E-like elevation fan)
+  ray-cast against a street scene (ground plane, building boxes, parked cars,
+  poles), ~120k points per scan, consecutive scans ~1 m apart with small yaw —
+  the C4 workload (examples/benchmark_kitti.cpp: source = scan i+1, target = scan i).
+* ``rgbd_room_sequence``   pinhole depth camera inside a furnished room, depth
+  0.4-4 m with a Kinect-like noise model, smooth trajectory — the C3/C5 surrogate
+  for the lounge sequence (examples/benchmark_lounge.cpp).
+* ``bunny_pair``           the reference's synthetic bunny protocol
+  (examples/benchmark_synthetic.cpp:91-160: x50 scale, random rigid transform,
+  Gaussian noise of variance 0.005 on both clouds).
+
+Everything is numpy with an explicit ``numpy.random.Generator(PCG64(seed))``.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def rot_3d(roll: float, pitch: float, yaw: float) -> np.ndarray:
+    """cc::rot_3d (src/cc.cpp:22-30): Rz(yaw) @ Ry(pitch) @ Rx(roll)."""
+    cx, sx = np.cos(roll), np.sin(roll)
+    cy, sy = np.cos(pitch), np.sin(pitch)
+    cz, sz = np.cos(yaw), np.sin(yaw)
+    Rx = np.array([[1, 0, 0], [0, cx, -sx], [0, sx, cx]])
+    Ry = np.array([[cy, 0, sy], [0, 1, 0], [-sy, 0, cy]])
+    Rz = np.array([[cz, -sz, 0], [sz, cz, 0], [0, 0, 1]])
+    return Rz @ Ry @ Rx
+
+
+def make_T(R: np.ndarray, t) -> np.ndarray:
+    T = np.eye(4)
+    T[:3, :3] = R
+    T[:3, 3] = t
+    return T
+
+
+def transform(T: np.ndarray, pts: np.ndarray) -> np.ndarray:
+    return pts @ T[:3, :3].T + T[:3, 3]
+
+
+# ----------------------------------------------------------------------------- ray casting
+class _Scene:
+    def __init__(self, ground: bool = True):
+        self.ground = ground
+        self.boxes_lo: list = []
+        self.boxes_hi: list = []
+        self.cyl: list = []  # (cx, cy, r, z0, z1)
+        self.inside_boxes_lo: list = []  # rooms: rays start inside, hit the walls from within
+        self.inside_boxes_hi: list = []
+
+    def add_box(self, lo, hi):
+        self.boxes_lo.append(lo)
+        self.boxes_hi.append(hi)
+
+    def cast(self, origin: np.ndarray, dirs: np.ndarray, tmax: float) -> np.ndarray:
+        """Nearest positive hit distance along each unit ray (inf if none)."""
+        best = np.full(dirs.shape[0], np.inf)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            if self.ground:
+                t = -origin[2] / dirs[:, 2]
+                best = np.where((t > 1e-6) & (t < best), t, best)
+            inv = 1.0 / dirs
+            if self.boxes_lo:
+                lo = np.asarray(self.boxes_lo)[None]  # (1,B,3)
+                hi = np.asarray(self.boxes_hi)[None]
+                t1 = (lo - origin[None, None]) * inv[:, None, :]
+                t2 = (hi - origin[None, None]) * inv[:, None, :]
+                tn = np.nanmax(np.minimum(t1, t2), axis=2)
+                tf = np.nanmin(np.maximum(t1, t2), axis=2)
+                hit = (tf >= tn) & (tn > 1e-6)
+                th = np.where(hit, tn, np.inf).min(axis=1)
+                best = np.minimum(best, th)
+            if self.inside_boxes_lo:
+                lo = np.asarray(self.inside_boxes_lo)[None]
+                hi = np.asarray(self.inside_boxes_hi)[None]
+                t1 = (lo - origin[None, None]) * inv[:, None, :]
+                t2 = (hi - origin[None, None]) * inv[:, None, :]
+                tf = np.nanmin(np.maximum(t1, t2), axis=2)
+                th = np.where(tf > 1e-6, tf, np.inf).min(axis=1)
+                best = np.minimum(best, th)
+            for cx, cy, r, z0, z1 in self.cyl:
+                ox, oy = origin[0] - cx, origin[1] - cy
+                a = dirs[:, 0] ** 2 + dirs[:, 1] ** 2
+                b = 2 * (ox * dirs[:, 0] + oy * dirs[:, 1])
+                c = ox * ox + oy * oy - r * r
+                disc = b * b - 4 * a * c
+                t = (-b - np.sqrt(np.maximum(disc, 0))) / (2 * a)
+                z = origin[2] + t * dirs[:, 2]
+                ok = (disc >= 0) & (t > 1e-6) & (z >= z0) & (z <= z1)
+                best = np.where(ok & (t < best), t, best)
+        best[best > tmax] = np.inf
+        return best
+
+
+def _street_scene(rng, length: float) -> _Scene:
+    sc = _Scene(ground=True)
+    for side in (-1, 1):
+        x = -60.0
+        while x < length + 60:
+            w = rng.uniform(6, 22)
+            if rng.random() < 0.8:
+                y0 = rng.uniform(8, 13)
+                d = rng.uniform(6, 14)
+                h = rng.uniform(4, 16)
+                ylo, yhi = (y0, y0 + d) if side > 0 else (-y0 - d, -y0)
+                sc.add_box((x, ylo, 0.0), (x + w, yhi, h))
+            x += w + rng.uniform(1, 8)
+        x = -60.0
+        while x < length + 60:
+            if rng.random() < 0.5:  # parked car
+                y = side * rng.uniform(4.8, 5.6)
+                sc.add_box((x, y - 0.9, 0.0), (x + 4.2, y + 0.9, 1.5))
+            x += rng.uniform(6, 12)
+        x = -60.0
+        while x < length + 60:  # poles / trunks
+            sc.cyl.append((x + rng.uniform(-1, 1), side * rng.uniform(6.5, 7.5), rng.uniform(0.1, 0.35), 0.0,
+                           rng.uniform(3, 8)))
+            x += rng.uniform(8, 18)
+    return sc
+
+
+def kitti_like_sequence(n_scans: int, seed: int = 4, n_az: int = 1915, n_beams: int = 64, step: float = 1.0,
+                        max_yaw_deg: float = 2.0, range_noise: float = 0.02, max_range: float = 80.0):
+    """Return (scans, poses): scans[k] is an (N_k, 3) float64 cloud in the sensor frame of
+    scan k, poses[k] its 4x4 world pose.  ~120k points per scan at the defaults."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    sc = _street_scene(rng, step * n_scans)
+    elev = np.deg2rad(np.linspace(-24.8, 2.0, n_beams))
+    scans, poses = [], []
+    yaw = 0.0
+    pos = np.array([0.0, 0.0, 1.73])
+    for k in range(n_scans):
+        if k > 0:
+            yaw += np.deg2rad(rng.uniform(-max_yaw_deg, max_yaw_deg)) * 0.5
+            pos = pos + np.array([np.cos(yaw), np.sin(yaw), 0.0]) * step * rng.uniform(0.9, 1.1)
+            pos[1] = np.clip(pos[1], -2.5, 2.5)
+        Rw = rot_3d(0, 0, yaw)
+        az = np.linspace(0, 2 * np.pi, n_az, endpoint=False) + rng.uniform(0, 2 * np.pi / n_az)
+        E, A = np.meshgrid(elev + rng.normal(0, 0.0005, n_beams), az, indexing="ij")
+        d = np.stack([np.cos(E) * np.cos(A), np.cos(E) * np.sin(A), np.sin(E)], axis=-1).reshape(-1, 3)
+        dw = d @ Rw.T
+        ts = []
+        for c0 in range(0, d.shape[0], 16384):
+            ts.append(sc.cast(pos, dw[c0:c0 + 16384], max_range))
+        t = np.concatenate(ts)
+        ok = np.isfinite(t) & (t > 1.0)
+        t = t[ok] + rng.normal(0, range_noise, ok.sum())
+        pts = d[ok] * t[:, None]
+        scans.append(np.ascontiguousarray(pts))
+        poses.append(make_T(Rw, pos))
+    return scans, poses
+
+
+def kitti_like_pairs(n_pairs: int, seed: int = 4, **kw):
+    """Consecutive-scan pairs (source = scan i+1, target = scan i, examples/benchmark_kitti.cpp:130-131)
+    with ground truth T = pose[i]^-1 pose[i+1]."""
+    scans, poses = kitti_like_sequence(n_pairs + 1, seed=seed, **kw)
+    pairs, gts = [], []
+    for i in range(n_pairs):
+        pairs.append((scans[i + 1], scans[i]))
+        gts.append(np.linalg.inv(poses[i]) @ poses[i + 1])
+    return pairs, gts
+
+
+def rgbd_room_sequence(n_frames: int, seed: int = 3, stride: int = 4, max_step_deg: float = 4.0,
+                       max_step_m: float = 0.08):
+    """Depth-camera frames inside a furnished room; points in the camera frame
+    (x right, y down, z forward, depth = z in metres, 0.4-4 m)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    sc = _Scene(ground=False)
+    sc.inside_boxes_lo.append((-3.5, -3.0, 0.0))
+    sc.inside_boxes_hi.append((3.5, 3.0, 2.8))
+    for _ in range(9):  # furniture
+        c = rng.uniform([-2.8, -2.3, 0], [2.8, 2.3, 0])
+        s = rng.uniform([0.3, 0.3, 0.3], [1.4, 1.0, 1.2])
+        sc.add_box((c[0] - s[0] / 2, c[1] - s[1] / 2, 0.0), (c[0] + s[0] / 2, c[1] + s[1] / 2, s[2]))
+    fx = fy = 525.0
+    W, H = 640, 480
+    u, v = np.meshgrid(np.arange(0, W, stride) + 0.5 * stride, np.arange(0, H, stride) + 0.5 * stride)
+    dc = np.stack([(u - 319.5) / fx, (v - 239.5) / fy, np.ones_like(u)], axis=-1).reshape(-1, 3)
+    dc /= np.linalg.norm(dc, axis=1, keepdims=True)
+    # camera (x right, y down, z fwd) -> world (x fwd, y left, z up) at yaw 0
+    C2W = np.array([[0, 0, 1], [-1, 0, 0], [0, -1, 0]], dtype=float)
+    frames, poses = [], []
+    yaw, pitch = rng.uniform(0, 2 * np.pi), np.deg2rad(-10)
+    pos = np.array([0.0, 0.0, 1.4])
+    for k in range(n_frames):
+        if k > 0:
+            yaw += np.deg2rad(rng.uniform(0.3, 1.0) * max_step_deg)
+            pitch = np.clip(pitch + np.deg2rad(rng.normal(0, 0.5)), np.deg2rad(-25), np.deg2rad(5))
+            pos = pos + rng.normal(0, max_step_m / 2, 3) * np.array([1, 1, 0.3])
+            pos = np.clip(pos, [-1.5, -1.2, 1.0], [1.5, 1.2, 1.8])
+        Rw = rot_3d(0, -pitch, yaw) @ C2W
+        dw = dc @ Rw.T
+        t = sc.cast(pos, dw, 10.0)
+        depth = t * dc[:, 2]
+        ok = np.isfinite(t) & (depth > 0.4) & (depth < 4.0)
+        z = depth[ok]
+        z = z + rng.normal(0, 1.0, z.shape) * (0.0012 + 0.0019 * (z - 0.4) ** 2)
+        pts = dc[ok] / dc[ok, 2:3] * z[:, None]
+        frames.append(np.ascontiguousarray(pts))
+        poses.append(make_T(Rw, pos))
+    return frames, poses
+
+
+def rgbd_pairs(n_pairs: int, seed: int = 3, gap: int = 1, **kw):
+    frames, poses = rgbd_room_sequence(n_pairs + gap, seed=seed, **kw)
+    pairs, gts = [], []
+    for i in range(n_pairs):
+        pairs.append((frames[i + gap], frames[i]))
+        gts.append(np.linalg.inv(poses[i]) @ poses[i + gap])
+    return pairs, gts
+
+
+def bunny_pair(bunny_unique: np.ndarray, seed: int = 1, noise_var: float = 0.005, easy: bool = True,
+               subsample: float | None = None):
+    """examples/benchmark_synthetic.cpp:91-160 protocol on the unique bunny vertices x50.
+    Returns (src, tgt, T_gt) with tgt ~ T_gt @ src."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    base = np.asarray(bunny_unique, dtype=np.float64) * 50.0
+    tr, rr = (5.0, np.pi / 4) if easy else (10.0, np.pi / 2)
+    t = rng.uniform(-tr, tr, 3)
+    R = rot_3d(*rng.uniform(-rr, rr, 3))
+    T = make_T(R, t)
+    if subsample:
+        src = base[rng.random(base.shape[0]) < subsample]
+        tgt = transform(T, base)[rng.random(base.shape[0]) < subsample]
+    else:
+        src = base.copy()
+        tgt = transform(T, base)
+    sd = np.sqrt(noise_var)
+    src = src + rng.normal(0, sd, src.shape)
+    tgt = tgt + rng.normal(0, sd, tgt.shape)
+    return np.ascontiguousarray(src), np.ascontiguousarray(tgt), T

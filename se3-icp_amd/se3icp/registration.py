@@ -1,0 +1,283 @@
+"""Host-side mirror of the reference's engine interface.
+
+``IterativeSE3Registration`` reproduces the public surface of
+``class IterativeSE3Registration`` (include/iterative_SE3_registration.hpp:27-99):
+same member names, same constructor defaults (src/iterative_SE3_registration.cpp:334-348),
+``setSourceCloud`` / ``setTargetCloud`` (append semantics, ISR.cpp:358-376), the four
+``run_*`` methods and the result members ``current_estimated_T_``,
+``num_iterations_``, ``num_pure_se3_iterations_``.  Every run goes through the
+C-ABI of libse3icp.so to the HIP kernels; nothing here computes registration on
+the CPU.
+
+``register_batch`` / ``register_batch_device`` expose the batched path (many scan
+pairs in lockstep on one GPU), the MI355X replacement for the serial pair loops of
+examples/benchmark_kitti.cpp:120-197 and examples/benchmark_lounge.cpp:154-235.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from .io import read_ply_xyz
+
+_PARAM_FIELDS = {
+    # reference member            -> se3icp_params field
+    "max_num_iterations_": "max_num_iterations",
+    "max_num_se3_iterations_": "max_num_se3_iterations",
+    "number_of_nn_for_LRF_": "number_of_nn_for_LRF",
+    "mse_": "mse",
+    "mse_switch_error_": "mse_switch_error",
+    "estimated_overlap_": "estimated_overlap",
+    "alpha_rot": "alpha_rot",
+    "beta_transl": "beta_transl",
+    "scale_preprocessing": "scale_preprocessing",
+}
+
+
+def _as_xyz(cloud) -> np.ndarray:
+    a = np.ascontiguousarray(np.asarray(cloud, dtype=np.float64))
+    if a.ndim != 2 or a.shape[1] != 3:
+        raise ValueError(f"expected an (N, 3) point array, got shape {a.shape}")
+    return a
+
+
+class IterativeSE3Registration:
+    """GPU drop-in for the reference class (one object per pair, like the reference)."""
+
+    def __init__(self):
+        L = _lib.load()
+        object.__setattr__(self, "_L", L)
+        object.__setattr__(self, "_h", L.se3icp_registration_new())
+        if not self._h:
+            raise MemoryError("se3icp_registration_new failed")
+        object.__setattr__(self, "_params", L.se3icp_params_of(self._h).contents)
+        object.__setattr__(self, "_res", _lib.Result())
+        L.se3icp_get_result(self._h, C.byref(self._res))
+        # constructor state of the reference (ISR.cpp:334-348); lrf_radius_ is only used by
+        # the dead SHOT code path (ISR.cpp:593-594)
+        object.__setattr__(self, "lrf_radius_", 0.8)
+        object.__setattr__(self, "time_before_pure_icp_", 0.0)
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            self._L.se3icp_registration_free(h)
+            object.__setattr__(self, "_h", None)
+
+    # ---- public config fields (ISR.hpp:80-95)
+    def __getattr__(self, name):
+        if name in _PARAM_FIELDS:
+            return getattr(self._params, _PARAM_FIELDS[name])
+        raise AttributeError(name)
+
+    def __setattr__(self, name, value):
+        if name in _PARAM_FIELDS:
+            setattr(self._params, _PARAM_FIELDS[name], value)
+        else:
+            object.__setattr__(self, name, value)
+
+    # ---- clouds (ISR.cpp:350-376)
+    def setSourceCloud(self, cloud):
+        pts = read_ply_xyz(cloud) if isinstance(cloud, (str, bytes)) else _as_xyz(cloud)
+        _lib.check(self._L.se3icp_set_source_cloud(self._h, pts.ctypes.data_as(C.POINTER(C.c_double)), pts.shape[0]))
+
+    def setTargetCloud(self, cloud):
+        pts = read_ply_xyz(cloud) if isinstance(cloud, (str, bytes)) else _as_xyz(cloud)
+        _lib.check(self._L.se3icp_set_target_cloud(self._h, pts.ctypes.data_as(C.POINTER(C.c_double)), pts.shape[0]))
+
+    # ---- run methods (ISR.hpp:46-50)
+    def _finish(self, rc):
+        self._L.se3icp_get_result(self._h, C.byref(self._res))
+        if rc in (_lib.ERR_NO_DEVICE, _lib.ERR_HIP, _lib.ERR_OUT_OF_MEMORY, _lib.ERR_EMPTY_CLOUD,
+                  _lib.ERR_K_TOO_LARGE, _lib.ERR_INVALID_ARG):
+            raise _lib.Se3IcpError(rc)
+        return rc
+
+    def run_icp(self, variant_name: str):
+        """Vanilla pt2pt / pt2pl / gicp ICP (ISR.cpp:473-552)."""
+        return self._finish(self._L.se3icp_run_icp(self._h, variant_name.encode()))
+
+    def run_se3_icp(self, variant_name: str):
+        """Proposed SE(3)-ICP, variant in {pt2pt, pt2pl, gicp} (ISR.cpp:555-739)."""
+        return self._finish(self._L.se3icp_run_se3_icp(self._h, variant_name.encode()))
+
+    def run_se3_icp_with_cf(self):
+        """SE(3)-GICP with depth confidences (ISR.cpp:742-959)."""
+        rc = self._L.se3icp_run_se3_icp_with_cf(self._h)
+        self._L.se3icp_get_result(self._h, C.byref(self._res))
+        print(f"### scaling factor = {self._res.scaling_factor:g}")  # ISR.cpp:794
+        return self._finish(rc)
+
+    def run_se3_pure(self, variant_name: str):
+        """SE(3) correspondences only, never switching to R3 (ISR.cpp:962-1127)."""
+        rc = self._finish(self._L.se3icp_run_se3_pure(self._h, variant_name.encode()))
+        print("pure se3 finished")
+        return rc
+
+    # ---- results (ISR.hpp:92-98)
+    @property
+    def current_estimated_T_(self) -> np.ndarray:
+        return np.array(self._res.T).reshape(4, 4)
+
+    @property
+    def num_iterations_(self) -> int:
+        return int(self._res.num_iterations)
+
+    @property
+    def num_pure_se3_iterations_(self) -> int:
+        return int(self._res.num_pure_se3_iterations)
+
+    @property
+    def time_se3_correspondence_search_(self) -> float:
+        return float(self._res.time_se3_correspondence_search_ms)
+
+    @property
+    def num_rechecked(self) -> int:
+        return int(self._res.num_rechecked)
+
+    @property
+    def status(self) -> int:
+        return int(self._res.status)
+
+
+@dataclass
+class PairResult:
+    T: np.ndarray
+    num_iterations: int
+    num_pure_se3_iterations: int
+    status: int
+    num_rechecked: int
+    scaling_factor: float
+    time_setup_ms: float
+    time_loop_ms: float
+    time_nn_ms: float
+
+
+def _results(res, n) -> list[PairResult]:
+    out = []
+    for i in range(n):
+        r = res[i]
+        out.append(PairResult(np.array(r.T).reshape(4, 4), int(r.num_iterations), int(r.num_pure_se3_iterations),
+                              int(r.status), int(r.num_rechecked), float(r.scaling_factor), float(r.time_setup_ms),
+                              float(r.time_loop_ms), float(r.time_se3_correspondence_search_ms)))
+    return out
+
+
+def cli_params(**overrides) -> _lib.Params:
+    """Parameter overrides of examples/run_registration_method.cpp:38-42."""
+    p = _lib.default_params(estimated_overlap=1.0, max_num_se3_iterations=10, mse=1e-5, mse_switch_error=5e-5,
+                            number_of_nn_for_LRF=90)
+    for k, v in overrides.items():
+        setattr(p, k, v)
+    return p
+
+
+def kitti_params(**overrides) -> _lib.Params:
+    """SE(3) parameters of examples/benchmark_kitti.cpp:133-148."""
+    p = _lib.default_params(estimated_overlap=0.7, max_num_se3_iterations=10, mse=1e-7, mse_switch_error=5e-7,
+                            number_of_nn_for_LRF=90)
+    for k, v in overrides.items():
+        setattr(p, k, v)
+    return p
+
+
+def lounge_params(**overrides) -> _lib.Params:
+    """Parameters of examples/benchmark_lounge.cpp:183-189."""
+    p = _lib.default_params(estimated_overlap=0.75, max_num_se3_iterations=10, mse_switch_error=5e-5,
+                            number_of_nn_for_LRF=90)
+    for k, v in overrides.items():
+        setattr(p, k, v)
+    return p
+
+
+def register_batch(pairs, method: str, params: _lib.Params | None = None, device: int = 0) -> list[PairResult]:
+    """Register [(src (N,3), tgt (M,3)), ...] in lockstep on one GPU (host buffers)."""
+    L = _lib.load()
+    srcs = [_as_xyz(s) for s, _ in pairs]
+    tgts = [_as_xyz(t) for _, t in pairs]
+    n = len(pairs)
+    dp = C.POINTER(C.c_double)
+    sp = (dp * n)(*[a.ctypes.data_as(dp) for a in srcs])
+    tp = (dp * n)(*[a.ctypes.data_as(dp) for a in tgts])
+    ns = (C.c_int64 * n)(*[a.shape[0] for a in srcs])
+    nt = (C.c_int64 * n)(*[a.shape[0] for a in tgts])
+    res = (_lib.Result * n)()
+    rc = L.se3icp_register_batch(device, n, sp, ns, tp, nt, _lib.method_id(method),
+                                 C.byref(params or _lib.default_params()), res)
+    if rc not in (_lib.OK, _lib.ERR_NONFINITE):
+        raise _lib.Se3IcpError(rc, "register_batch")
+    return _results(res, n)
+
+
+def register_batch_device(src_ptr: int, src_off, tgt_ptr: int, tgt_off, method: str,
+                          params: _lib.Params | None = None, device: int = 0, stream: int = 0) -> list[PairResult]:
+    """Register pairs whose clouds are already in HBM.
+
+    src_ptr/tgt_ptr: device addresses of the concatenated AoS float64 xyz arrays
+    (e.g. ``torch_tensor.data_ptr()``); src_off/tgt_off: n_pairs+1 point offsets.
+    """
+    L = _lib.load()
+    n = len(src_off) - 1
+    so = (C.c_int64 * (n + 1))(*[int(x) for x in src_off])
+    to = (C.c_int64 * (n + 1))(*[int(x) for x in tgt_off])
+    res = (_lib.Result * n)()
+    rc = L.se3icp_register_batch_device(device, n, C.c_void_p(src_ptr), so, C.c_void_p(tgt_ptr), to,
+                                        _lib.method_id(method), C.byref(params or _lib.default_params()), res,
+                                        C.c_void_p(stream) if stream else None)
+    if rc not in (_lib.OK, _lib.ERR_NONFINITE):
+        raise _lib.Se3IcpError(rc, "register_batch_device")
+    return _results(res, n)
+
+
+# ---- stage entry points (one per reference function on the hot path)
+def toldi_frames(pts, k: int, device: int = 0) -> np.ndarray:
+    """computeAllTOLDISE3FramesOMP (ISR.cpp:318-331): (N, 4, 4) frames."""
+    pts = _as_xyz(pts)
+    out = np.zeros((pts.shape[0], 4, 4))
+    _lib.check(_lib.load().se3icp_toldi_frames(device, pts.ctypes.data_as(C.POINTER(C.c_double)), pts.shape[0], k,
+                                               out.ctypes.data_as(C.POINTER(C.c_double))), "toldi_frames")
+    return out
+
+
+def knn_self(pts, k: int, device: int = 0) -> np.ndarray:
+    """KDTreeFlann::SearchKNN of every point in its own cloud: (N, k) indices."""
+    pts = _as_xyz(pts)
+    out = np.zeros((pts.shape[0], k), np.int32)
+    _lib.check(_lib.load().se3icp_knn_self(device, pts.ctypes.data_as(C.POINTER(C.c_double)), pts.shape[0], k,
+                                           out.ctypes.data_as(C.POINTER(C.c_int32))), "knn_self")
+    return out
+
+
+def estimate_normals(pts, k: int = 30, device: int = 0) -> np.ndarray:
+    """PointCloud::EstimateNormals(KDTreeSearchParamKNN(k)) (ISR.cpp:643)."""
+    pts = _as_xyz(pts)
+    out = np.zeros_like(pts)
+    _lib.check(_lib.load().se3icp_estimate_normals(device, pts.ctypes.data_as(C.POINTER(C.c_double)), pts.shape[0],
+                                                   k, out.ctypes.data_as(C.POINTER(C.c_double))), "estimate_normals")
+    return out
+
+
+def nearest_neighbors(query, data, device: int = 0):
+    """Exact 1-NN in 3 or 12 dims (ISR.cpp:402-416 / 444-470); returns (idx, d2, n_rechecked)."""
+    q = np.ascontiguousarray(query, dtype=np.float64)
+    d = np.ascontiguousarray(data, dtype=np.float64)
+    dim = d.shape[1]
+    idx = np.zeros(q.shape[0], np.int32)
+    d2 = np.zeros(q.shape[0])
+    nr = C.c_int32(0)
+    dp = C.POINTER(C.c_double)
+    _lib.check(_lib.load().se3icp_nn(device, q.ctypes.data_as(dp), q.shape[0], d.ctypes.data_as(dp), d.shape[0], dim,
+                                     idx.ctypes.data_as(C.POINTER(C.c_int32)), d2.ctypes.data_as(dp), C.byref(nr)),
+               "nn")
+    return idx, d2, int(nr.value)
+
+
+def last_kernel_times(device: int = 0) -> dict:
+    out = (C.c_double * 10)()
+    _lib.check(_lib.load().se3icp_last_kernel_times(device, out))
+    keys = ["sweep_se3_ms", "sweep_r3_ms", "finalize_ms", "recheck_ms", "trim_ms", "reduce_ms", "setup_ms",
+            "sweep_se3_launches", "se3_pairs_evaluated", "r3_pairs_evaluated"]
+    return dict(zip(keys, list(out)))

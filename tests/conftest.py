@@ -1,0 +1,37 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "se3-icp_amd")
+for p in (PKG, ROOT):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
+
+
+@pytest.fixture(scope="session")
+def fixture_clouds():
+    from se3icp.io import read_ply_xyz
+    return (read_ply_xyz(os.path.join(GOLDEN, "fixture_source.ply")),
+            read_ply_xyz(os.path.join(GOLDEN, "fixture_target.ply")))
+
+
+@pytest.fixture(scope="session")
+def fixture_T_gt():
+    from se3icp import datasets
+    import numpy as np
+    # examples/create_and_save_reg_problem.cpp:31-37, cc::rot_3d(pi/9, pi/8, -pi/7), t = (1,2,3)
+    return datasets.make_T(datasets.rot_3d(np.pi / 9, np.pi / 8, -np.pi / 7), [1.0, 2.0, 3.0])
+
+
+@pytest.fixture(scope="session")
+def bunny_unique():
+    import numpy as np
+    return np.load(os.path.join(GOLDEN, "bunny_unique_f32.npy")).astype(np.float64)

@@ -1,0 +1,189 @@
+"""GPU parity tests: the HIP engine (through the C-ABI) against the CPU restatement.
+
+Bars (BASELINE.json north_star): identical integer arg-min correspondences (modulo
+exact f64 ties between equal target coordinates) and final poses within 1e-5
+Frobenius of the oracle.  Floating-point stage outputs (TOLDI frames, normals)
+are compared with the tolerances written in each test.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def se3icp_mod():
+    import se3icp
+    se3icp.load()
+    if se3icp.device_count() < 1:
+        pytest.fail("no HIP device visible: the GPU tests must run on an MI355X")
+    return se3icp
+
+
+@pytest.fixture(scope="module")
+def refcpu():
+    from oracle import refcpu as r
+    r.lib()
+    return r
+
+
+def _tie_ok(data, q, i_gpu, i_ref, d2_ref, dim):
+    """GPU and oracle NN agree, or both are exact minimisers (equal f64 distance)."""
+    if i_gpu == i_ref:
+        return True
+    a = q
+    b = data[i_gpu]
+    d = a - b
+    dg = float(np.dot(d, d))
+    return abs(dg - d2_ref) <= 1e-12 * max(1.0, d2_ref)
+
+
+# --------------------------------------------------------------------------- end to end
+@pytest.mark.parametrize("variant", ["pt2pt", "pt2pl", "gicp"])
+def test_fixture_se3_icp_matches_oracle_and_ground_truth(se3icp_mod, refcpu, fixture_clouds, fixture_T_gt, variant):
+    src, tgt = fixture_clouds
+    reg = se3icp_mod.IterativeSE3Registration()
+    reg.setSourceCloud(src)
+    reg.setTargetCloud(tgt)
+    reg.estimated_overlap_ = 1.0
+    reg.max_num_se3_iterations_ = 10
+    reg.mse_ = 0.00001
+    reg.mse_switch_error_ = 5 * reg.mse_
+    reg.number_of_nn_for_LRF_ = 90
+    assert reg.run_se3_icp(variant) == 0
+    ref = refcpu.register(src, tgt, refcpu.RUN_SE3_ICP, variant, refcpu.cli_params())
+    T = reg.current_estimated_T_
+    assert np.linalg.norm(T - ref["T"]) <= 1e-5
+    assert np.linalg.norm(T - fixture_T_gt) <= 1e-6
+    assert abs(reg.num_iterations_ - ref["num_iterations"]) <= 1
+    assert abs(reg.num_pure_se3_iterations_ - ref["num_pure_se3_iterations"]) <= 1
+
+
+@pytest.mark.parametrize("variant", ["pt2pt", "pt2pl", "gicp"])
+def test_fixture_vanilla_icp_matches_oracle(se3icp_mod, refcpu, fixture_clouds, variant):
+    src, tgt = fixture_clouds
+    params = se3icp_mod.cli_params()
+    got = se3icp_mod.register_batch([(src, tgt)], variant, params)[0]
+    ref = refcpu.register(src, tgt, refcpu.RUN_ICP, variant, refcpu.cli_params())
+    assert np.linalg.norm(got.T - ref["T"]) <= 1e-5
+    assert got.num_pure_se3_iterations == -1
+    assert abs(got.num_iterations - ref["num_iterations"]) <= 1
+
+
+def test_fixture_with_cf_matches_oracle(se3icp_mod, refcpu, fixture_clouds, fixture_T_gt):
+    src, tgt = fixture_clouds
+    got = se3icp_mod.register_batch([(src, tgt)], "se3_gicp_with_cf", se3icp_mod.cli_params())[0]
+    ref = refcpu.register(src, tgt, refcpu.RUN_SE3_ICP_CF, "gicp", refcpu.cli_params())
+    assert np.linalg.norm(got.T - ref["T"]) <= 1e-5
+    assert np.linalg.norm(got.T - fixture_T_gt) <= 1e-6
+
+
+# --------------------------------------------------------------------------- stages
+def test_knn_self_matches_oracle(se3icp_mod, refcpu, fixture_clouds):
+    src, _ = fixture_clouds
+    k = 90
+    g = se3icp_mod.knn_self(src, k)
+    ri, rd = refcpu.knn_self(src, k)
+    same = (g == ri)
+    if not same.all():
+        # allowed only where the two lists differ by exact-distance ties
+        bad = np.nonzero(~same.all(axis=1))[0]
+        for i in bad:
+            dg = np.sum((src[g[i]] - src[i]) ** 2, axis=1)
+            np.testing.assert_allclose(np.sort(dg), rd[i], rtol=0, atol=1e-12)
+    # sorted ascending
+    d = np.sum((src[g] - src[:, None, :]) ** 2, axis=2)
+    assert (np.diff(d, axis=1) >= -1e-15).all()
+
+
+def test_toldi_frames_match_oracle(se3icp_mod, refcpu, fixture_clouds):
+    src, _ = fixture_clouds
+    g = se3icp_mod.toldi_frames(src, 90)
+    r = refcpu.toldi_frames(src, 90)
+    diff = np.abs(g - r).reshape(len(src), -1).max(axis=1)
+    # frames are smooth functions of the neighbourhoods except where the covariance has a
+    # (near-)degenerate smallest eigenvalue; require 99.9 % agreement at 1e-8
+    assert np.mean(diff <= 1e-8) >= 0.999, np.sort(diff)[-10:]
+    R = g[:, :3, :3]
+    np.testing.assert_allclose(np.einsum("nij,nik->njk", R, R), np.broadcast_to(np.eye(3), R.shape), atol=1e-9)
+
+
+def test_estimate_normals_match_oracle(se3icp_mod, refcpu, fixture_clouds):
+    src, _ = fixture_clouds
+    g = se3icp_mod.estimate_normals(src, 30)
+    r = refcpu.estimate_normals(src, 30)
+    # sign included: FastEigen3x3 is deterministic given the covariance
+    diff = np.abs(g - r).max(axis=1)
+    assert np.mean(diff <= 1e-8) >= 0.999
+
+
+def _se3_vectors(frames, alpha=3.0, beta=1.0):
+    R = frames[:, :3, :3]
+    t = frames[:, :3, 3]
+    return np.concatenate([alpha * R.transpose(0, 2, 1).reshape(-1, 9), beta * t], axis=1)
+
+
+def test_se3_nn_matches_oracle(se3icp_mod, refcpu, fixture_clouds):
+    src, tgt = fixture_clouds
+    fs = refcpu.toldi_frames(src, 90)
+    ft = refcpu.toldi_frames(tgt, 90)
+    q = _se3_vectors(fs)
+    d = _se3_vectors(ft)
+    gi, gd2, nrech = se3icp_mod.nearest_neighbors(q, d)
+    ri, rd2 = refcpu.nn(q, d)
+    for i in np.nonzero(gi != ri)[0]:
+        assert _tie_ok(d, q[i], gi[i], ri[i], rd2[i], 12), (i, gi[i], ri[i])
+    np.testing.assert_allclose(gd2, rd2, rtol=0, atol=1e-12)
+
+
+def test_r3_nn_matches_oracle(se3icp_mod, refcpu, fixture_clouds):
+    src, tgt = fixture_clouds
+    rng = np.random.default_rng(0)
+    q = src + rng.normal(0, 0.05, src.shape)
+    gi, gd2, _ = se3icp_mod.nearest_neighbors(q, tgt)
+    ri, rd2 = refcpu.nn(q, tgt)
+    for i in np.nonzero(gi != ri)[0]:
+        assert _tie_ok(tgt, q[i], gi[i], ri[i], rd2[i], 3)
+    np.testing.assert_allclose(gd2, rd2, rtol=0, atol=1e-12)
+
+
+def test_nn_exact_ties_pick_lowest_index(se3icp_mod):
+    data = np.array([[1.0, 0, 0], [0, 1.0, 0], [1.0, 0, 0], [-1.0, 0, 0]])
+    q = np.zeros((1, 3))
+    gi, _, nrech = se3icp_mod.nearest_neighbors(q, data)
+    assert gi[0] == 0 and nrech >= 1
+
+
+# --------------------------------------------------------------------------- synthetic workloads
+def test_bunny_pair_se3_pt2pt(se3icp_mod, refcpu, bunny_unique):
+    from se3icp import datasets
+    src, tgt, T_gt = datasets.bunny_pair(bunny_unique, seed=1, subsample=0.12)
+    params = se3icp_mod.cli_params()
+    got = se3icp_mod.register_batch([(src, tgt)], "se3_pt2pt", params)[0]
+    ref = refcpu.register(src, tgt, refcpu.RUN_SE3_ICP, "pt2pt", refcpu.cli_params())
+    assert np.linalg.norm(got.T - ref["T"]) <= 1e-5
+    assert abs(got.num_iterations - ref["num_iterations"]) <= 1
+
+
+def test_kitti_like_batch_gicp_trimmed(se3icp_mod, refcpu):
+    from se3icp import datasets
+    pairs, gts = datasets.kitti_like_pairs(2, seed=11, n_az=300)
+    params = se3icp_mod.kitti_params()
+    got = se3icp_mod.register_batch(pairs, "se3_gicp", params)
+    rp = refcpu.default_params(estimated_overlap=0.7, max_num_se3_iterations=10, mse=1e-7, mse_switch_error=5e-7,
+                               number_of_nn_for_LRF=90)
+    for (s, t), g in zip(pairs, got):
+        ref = refcpu.register(s, t, refcpu.RUN_SE3_ICP, "gicp", rp)
+        assert np.linalg.norm(g.T - ref["T"]) <= 1e-5, (g.T, ref["T"])
+
+
+def test_rgbd_batch_with_cf(se3icp_mod, refcpu):
+    from se3icp import datasets
+    pairs, gts = datasets.rgbd_pairs(2, seed=3, stride=8)
+    params = se3icp_mod.lounge_params()
+    got = se3icp_mod.register_batch(pairs, "se3_gicp_with_cf", params)
+    rp = refcpu.default_params(estimated_overlap=0.75, max_num_se3_iterations=10, mse_switch_error=5e-5,
+                               number_of_nn_for_LRF=90)
+    for (s, t), g in zip(pairs, got):
+        ref = refcpu.register(s, t, refcpu.RUN_SE3_ICP_CF, "gicp", rp)
+        assert np.linalg.norm(g.T - ref["T"]) <= 1e-5, (g.T, ref["T"])
