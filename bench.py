@@ -1,0 +1,244 @@
+#!/usr/bin/env python3
+"""bench.py — ICP iterations/sec + pairs/sec on KITTI-scale LiDAR pairs (BASELINE.json).
+
+Workload (BASELINE.json configs[3]): se3_gicp with the KITTI driver's
+parameters (examples/benchmark_kitti.cpp:133-148: overlap 0.7, mse 1e-7, mse_switch 5e-7,
+max_se3 10, k = 90) on synthetic 64-beam LiDAR scans of ~120k points (the KITTI data are
+not available offline).  64 consecutive-scan pairs are sharded over the GPUs: 8 pairs per
+GPU (weak scaling), each rank registering its own 8 pairs in lockstep with no data-path
+collective; RCCL (torch.distributed "nccl") only gathers the per-pair results.
+
+A step = registering the rank's batch end to end (TOLDI/kNN/normals setup + the ICP loop),
+clouds already resident in HBM.  value = ICP iterations (all ranks) / step wall time.
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 under torch.distributed.run.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "se3-icp_amd"), ROOT]
+
+FP32_PEAK_TFLOPS = 157.3   # MI355X vector (= f32 MFMA) peak, /opt/skills/guides/MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0
+
+
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def rot_err_deg(A, B):
+    R = A[:3, :3].T @ B[:3, :3]
+    return float(np.degrees(np.arccos(np.clip((np.trace(R) - 1) / 2, -1, 1))))
+
+
+def pmc_traffic(kernel_substr: str):
+    """HBM bytes per launch of a kernel from the newest committed PMC summary (profiles/*pmc*.json),
+    written by tools/pmc_summary.py from separate rocprofv3 --pmc passes."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        for k, v in d.get("kernels", {}).items():
+            if kernel_substr in k and v.get("hbm_bytes_per_launch") is not None:
+                return float(v["hbm_bytes_per_launch"]), os.path.relpath(f, ROOT)
+    return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--pairs-per-gpu", type=int, default=8)
+    ap.add_argument("--method", default="se3_gicp")
+    ap.add_argument("--n-az", type=int, default=1975, help="azimuth steps per revolution (~120k pts at 1975)")
+    ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+
+    import torch
+    import se3icp
+    from se3icp import datasets
+
+    se3icp.load()
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    P = args.pairs_per_gpu
+    t0 = time.time()
+    pairs, gts = datasets.kitti_like_pairs(P, seed=4, first=rank * P, total_pairs=world * P, n_az=args.n_az)
+    npts = [p[0].shape[0] for p in pairs] + [p[1].shape[0] for p in pairs]
+    log(f"rank {rank}: generated {P} pairs in {time.time() - t0:.1f}s, points/cloud "
+        f"min {min(npts)} mean {np.mean(npts):.0f} max {max(npts)}")
+    src = np.concatenate([p[0] for p in pairs])
+    tgt = np.concatenate([p[1] for p in pairs])
+    src_off = np.concatenate([[0], np.cumsum([p[0].shape[0] for p in pairs])])
+    tgt_off = np.concatenate([[0], np.cumsum([p[1].shape[0] for p in pairs])])
+    dev = torch.device("cuda", local)
+    d_src = torch.from_numpy(src).to(dev)
+    d_tgt = torch.from_numpy(tgt).to(dev)
+    torch.cuda.synchronize()
+    params = se3icp.kitti_params()
+
+    def step():
+        return se3icp.register_batch_device(d_src.data_ptr(), src_off, d_tgt.data_ptr(), tgt_off, args.method,
+                                            params, device=local)
+
+    for w in range(args.warmup):
+        tw = time.time()
+        step()
+        log(f"rank {rank}: warmup {w} {time.time() - tw:.2f}s")
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    iters = 0
+    loop_ms = 0.0
+    ktot: dict = {}
+    last = None
+    for s in range(args.steps):
+        res = step()
+        kt = se3icp.last_kernel_times(local)
+        for k, v in kt.items():
+            ktot[k] = ktot.get(k, 0.0) + v
+        iters += sum(r.num_iterations for r in res)
+        loop_ms += res[0].time_loop_ms
+        last = res
+        log(f"rank {rank}: step {s} done ({sum(r.num_iterations for r in res)} iterations)")
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+
+    # ---- cross-rank: max time, summed work, RCCL gather of the per-pair results
+    stats = torch.tensor([elapsed, float(iters), loop_ms / 1000.0], dtype=torch.float64, device=dev)
+    poses = torch.tensor(np.stack([r.T for r in last]), dtype=torch.float64, device=dev)
+    if dist:
+        t_max = stats[[0, 2]].clone()
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        tot = stats[1:2].clone()
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        gathered = [torch.empty_like(poses) for _ in range(world)]
+        dist.all_gather(gathered, poses)
+        elapsed, loop_s, iters_all = float(t_max[0]), float(t_max[1]), float(tot[0])
+    else:
+        loop_s, iters_all = loop_ms / 1000.0, float(iters)
+        gathered = [poses]
+
+    if rank == 0:
+        total_pairs = world * P * args.steps
+        value = iters_all / elapsed
+        ms_per_step = 1000.0 * elapsed / args.steps
+        rot_errs = [rot_err_deg(r.T, g) for r, g in zip(last, gts)]
+        tr_errs = [float(np.linalg.norm(r.T[:3, 3] - g[:3, 3])) for r, g in zip(last, gts)]
+        # dominant kernel + roofline (HIP events around every launch, on the engine's stream)
+        kms = {k: ktot.get(k, 0.0) for k in ["nn_se3_ms", "nn_r3_ms", "recheck_ms", "trim_ms", "reduce_ms"]}
+        dom = max(["nn_se3_ms", "nn_r3_ms"], key=lambda k: kms[k])
+        if dom == "nn_se3_ms":
+            D, evals, boxes, nl, kname = 12, ktot["se3_dist_evals"], ktot["se3_box_tests"], ktot["nn_se3_launches"], \
+                "k_nn_group<12>"
+        else:
+            D, evals, boxes, nl, kname = 3, ktot["r3_dist_evals"], ktot["r3_box_tests"], ktot["nn_r3_launches"], \
+                "k_nn_group<3>"
+        t_ms = kms[dom]
+        # work actually done: lane x target distance evaluations (3D flop: D sub + D FMA) and
+        # lane x box tests (4D flop: 2D sub/max + D FMA), counted on the device
+        flop_dist, flop_box = 3 * D, 4 * D
+        flops = evals * flop_dist + boxes * flop_box
+        achieved = flops / (t_ms / 1000.0) / 1e12 if t_ms > 0 else 0.0
+        nl = max(1.0, nl)
+        traffic, traffic_src = pmc_traffic("k_nn_groupILi12" if D == 12 else "k_nn_groupILi3")
+        out = {
+            "metric": "ICP iterations/sec + pairs/sec, ~120k-pt KITTI clouds, 1/2/4/8 GPU",
+            "value": round(value, 3),
+            "unit": "ICP iterations/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32 sweep + f64 certify/solve",
+            "data": "synthetic (64-beam LiDAR ray-cast street scenes, seed 4; KITTI not available offline)",
+            "config": {
+                "workload": "C4: se3_gicp, KITTI driver params (overlap 0.7, mse 1e-7, switch 5e-7, max_se3 10, k=90)",
+                "pairs_per_gpu": P,
+                "global_batch_pairs": world * P,
+                "points_per_cloud_mean": int(np.mean(npts)),
+                "parallelism": f"pair-sharded dp{world} (RCCL result gather only)",
+            },
+            "pairs_per_sec": round(total_pairs / elapsed, 4),
+            "loop_iterations_per_sec": round(iters_all / loop_s, 3) if loop_s > 0 else None,
+            "iterations_per_pair_mean": round(iters_all / total_pairs, 2),
+            "accuracy_vs_gt": {"rot_deg_max": round(max(rot_errs), 4), "trans_m_max": round(max(tr_errs), 4)},
+            "kernel_ms_per_step": {k: round(v / args.steps, 3) for k, v in kms.items()},
+            "roofline": {
+                "kernel": kname,
+                "bound": "mfma",
+                "note": "f32 VALU kd-tree sweep (leaf distance sweeps + box tests); gfx950 f32 MFMA peak = f32 VALU peak",
+                "achieved": round(achieved, 3),
+                "peak": FP32_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+                "avg_launch_ms": round(t_ms / nl, 4),
+                "launches": int(nl),
+                "flop_per_unit": {"distance_eval": flop_dist, "box_test": flop_box},
+                "units_per_launch": {"distance_evals": round(evals / nl), "box_tests": round(boxes / nl)},
+                "traffic": traffic,
+                "traffic_source": traffic_src,
+            },
+            "cpu_baseline": None,
+        }
+        if world == 1 and args.cpu_baseline == "auto":
+            out["cpu_baseline"], out["parity_vs_cpu"] = cpu_baseline(pairs[0], last[0], args.cpu_threads)
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(pair, gpu_res, threads):
+    """The oracle (C++/OpenMP restatement of the reference, kd-tree NN) on one pair of the
+    same workload, timed end to end on the host cores."""
+    from oracle import refcpu
+    n = max(1, min(threads, os.cpu_count() or 1))
+    refcpu.set_num_threads(n)
+    p = refcpu.default_params(estimated_overlap=0.7, max_num_se3_iterations=10, mse=1e-7, mse_switch_error=5e-7,
+                              number_of_nn_for_LRF=90)
+    log(f"cpu baseline: oracle on 1 pair with {n} threads ...")
+    t0 = time.perf_counter()
+    r = refcpu.register(pair[0], pair[1], refcpu.RUN_SE3_ICP, "gicp", p)
+    dt = time.perf_counter() - t0
+    log(f"cpu baseline: {r['num_iterations']} iterations in {dt:.2f}s")
+    base = {"value": round(r["num_iterations"] / dt, 4), "unit": "ICP iterations/s", "cores": n,
+            "kind": "port",
+            "sample": f"1 pair (source {pair[0].shape[0]} / target {pair[1].shape[0]} pts), end to end incl. "
+                      f"setup: {r['num_iterations']} iterations in {dt:.2f} s; loop {r['time_loop_ms']:.0f} ms, "
+                      f"setup {r['time_setup_ms']:.0f} ms"}
+    parity = {"pose_frobenius": float(np.linalg.norm(gpu_res.T - r["T"])),
+              "iterations_gpu": gpu_res.num_iterations, "iterations_cpu": r["num_iterations"]}
+    return base, parity
+
+
+if __name__ == "__main__":
+    main()

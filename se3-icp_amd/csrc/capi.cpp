@@ -273,20 +273,22 @@ int se3icp_set_profiling(int device, int on) {
     return 0;
 }
 
-int se3icp_last_kernel_times(int device, double* out /* [10] */) {
+int se3icp_last_kernel_times(int device, double* out /* [12] */) {
     Engine* e = usable_engine(device);
     if (!e || !out) return SE3ICP_ERR_NO_DEVICE;
     const auto& k = e->kernel_times();
-    out[0] = k.sweep_se3_ms;
-    out[1] = k.sweep_r3_ms;
-    out[2] = k.finalize_ms;
-    out[3] = k.recheck_ms;
-    out[4] = k.trim_ms;
-    out[5] = k.reduce_ms;
-    out[6] = k.setup_ms;
-    out[7] = (double)k.sweep_se3_launches;
-    out[8] = k.se3_pairs_evaluated;
-    out[9] = k.r3_pairs_evaluated;
+    out[0] = k.nn_se3_ms;
+    out[1] = k.nn_r3_ms;
+    out[2] = k.recheck_ms;
+    out[3] = k.trim_ms;
+    out[4] = k.reduce_ms;
+    out[5] = k.setup_ms;
+    out[6] = (double)k.nn_se3_launches;
+    out[7] = (double)k.nn_r3_launches;
+    out[8] = k.se3_dist_evals;
+    out[9] = k.se3_box_tests;
+    out[10] = k.r3_dist_evals;
+    out[11] = k.r3_box_tests;
     return 0;
 }
 

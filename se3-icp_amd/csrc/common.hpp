@@ -27,13 +27,6 @@ enum Estimator : int32_t { EST_PT2PT = 0, EST_PT2PL = 1, EST_GICP = 2 };
 struct CloudDev {
     int32_t off;        // first global point index
     int32_t n;          // points
-    // uniform grid for the kNN search (k_setup.hip)
-    double org[3];
-    double h, inv_h;
-    int32_t dims[3];
-    int32_t cell_off;   // first cell in the concatenated cell arrays
-    int32_t ncells;
-    int32_t _pad;
 };
 
 // Rewritten by the host every iteration (tiny H2D copy).
@@ -55,13 +48,6 @@ struct PairDev {
 struct BlockWork {
     int32_t pair;
     int32_t q0;            // first local query index of the block
-};
-
-// NN split candidate (sweep -> finalize)
-struct Cand {
-    float d1;
-    int32_t i1;
-    float d2;
 };
 
 }  // namespace se3icp

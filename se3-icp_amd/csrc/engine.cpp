@@ -9,6 +9,8 @@
 #include <map>
 #include <memory>
 
+#include "tree.hpp"
+
 namespace se3icp {
 
 namespace {
@@ -64,6 +66,8 @@ int pinned(T*& p, size_t& cap, size_t count) {
     return 0;
 }
 
+constexpr int kStatSlots = 64;  // NN work counters: [64][4] u64
+
 }  // namespace
 
 Engine::Engine(int device) : dev_(device) {
@@ -84,10 +88,12 @@ Engine::~Engine() {
     if (!ok_) return;
     (void)hipSetDevice(dev_);
     DevBuf* all[] = {&d_clouds_, &d_setup_, &d_pairs_, &d_cloud_of_, &d_inptr_, &d_in_, &d_xyz64_, &d_xyz32_,
-                     &d_fr64_, &d_fr32_, &d_nrm64_, &d_cov64_, &d_conf64_, &d_knn_, &d_cell_cnt_, &d_cell_start_,
-                     &d_slot_, &d_sidx_, &d_sxyz_, &d_norm12_, &d_norm3_, &d_corr_idx_, &d_corr_dist_, &d_cand_,
-                     &d_flag_list_, &d_flag_count_, &d_trim_key_, &d_red_partial_, &d_red_out_, &d_work_, &d_wb_,
-                     &d_wn_, &d_chunks_, &d_partial_, &d_centers_, &d_scan_tmp_, &d_rechecked_};
+                     &d_fr64_, &d_fr32_, &d_nrm64_, &d_cov64_, &d_conf64_, &d_knn_, &d_norm12_, &d_norm3_,
+                     &d_corr_idx_, &d_corr_dist_, &d_flag_list_, &d_flag_count_, &d_trim_key_, &d_red_partial_,
+                     &d_red_out_, &d_work_, &d_gwork_, &d_wb_, &d_wn_, &d_chunks_, &d_partial_, &d_centers_,
+                     &d_rechecked_, &d_keys0_, &d_keys1_, &d_vals1_, &d_sort_tmp_, &d_stats_,
+                     &t3_.perm, &t3_.pos, &t3_.vec, &t3_.blo, &t3_.bhi, &t3_.lo, &t3_.hi,
+                     &t12_.perm, &t12_.pos, &t12_.vec, &t12_.blo, &t12_.bhi, &t12_.lo, &t12_.hi};
     for (DevBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     if (h_pairs_) (void)hipHostFree(h_pairs_);
@@ -115,19 +121,22 @@ T* Engine::ensure(DevBuf& b, size_t count) {
     return static_cast<T*>(b.p);
 }
 
-int Engine::alloc_points(int64_t ntot, int kmax, int nsplit) {
+int Engine::alloc_points(int64_t ntot, int kmax) {
     if (ntot >= (int64_t)1 << 30) return SE3ICP_ERR_INVALID_ARG;
     ntot_ = ntot;
     ld_ = (int)((std::max<int64_t>(ntot, 1) + 63) / 64 * 64);
     kmax_ = std::max(kmax, 1);
-    nsplit_ = std::max(nsplit, 1);
     const size_t L = (size_t)ld_;
     bool ok = ensure<int32_t>(d_cloud_of_, L) && ensure<double>(d_in_, 3 * L) && ensure<double>(d_xyz64_, 3 * L) &&
               ensure<float>(d_xyz32_, 3 * L) && ensure<double>(d_fr64_, 12 * L) && ensure<float>(d_fr32_, 12 * L) &&
               ensure<double>(d_nrm64_, 3 * L) && ensure<double>(d_cov64_, 6 * L) && ensure<double>(d_conf64_, L) &&
-              ensure<int32_t>(d_knn_, L * kmax_) && ensure<int32_t>(d_slot_, L) && ensure<int32_t>(d_sidx_, L) &&
-              ensure<double>(d_sxyz_, 3 * L) && ensure<int32_t>(d_corr_idx_, L) && ensure<float>(d_corr_dist_, L) &&
-              ensure<Cand>(d_cand_, L * nsplit_) && ensure<int32_t>(d_flag_list_, L) && ensure<int32_t>(d_flag_count_, 4);
+              ensure<int32_t>(d_knn_, L * kmax_) && ensure<int32_t>(d_corr_idx_, L) && ensure<float>(d_corr_dist_, L) &&
+              ensure<int32_t>(d_flag_list_, L) && ensure<int32_t>(d_flag_count_, 4) &&
+              ensure<unsigned long long>(d_keys0_, L) && ensure<unsigned long long>(d_keys1_, L) &&
+              ensure<int32_t>(d_vals1_, L) && ensure<unsigned long long>(d_stats_, 4 * kStatSlots);
+    for (TreeBufs* t : {&t3_, &t12_})
+        ok = ok && ensure<int32_t>(t->perm, L) && ensure<int32_t>(t->pos, L);
+    ok = ok && ensure<float>(t3_.vec, 3 * L) && ensure<float>(t12_.vec, 12 * L);
     return ok ? 0 : SE3ICP_ERR_OUT_OF_MEMORY;
 }
 
@@ -151,17 +160,11 @@ View Engine::view() const {
     v.cov64 = (double*)d_cov64_.p;
     v.conf64 = (double*)d_conf64_.p;
     v.knn = (int32_t*)d_knn_.p;
-    v.cell_cnt = (int32_t*)d_cell_cnt_.p;
-    v.cell_start = (int32_t*)d_cell_start_.p;
-    v.slot = (int32_t*)d_slot_.p;
-    v.sidx = (int32_t*)d_sidx_.p;
-    v.sxyz = (double*)d_sxyz_.p;
     v.norm12_bits = (uint32_t*)d_norm12_.p;
     v.norm3_bits = (uint32_t*)d_norm3_.p;
     v.corr_idx = (int32_t*)d_corr_idx_.p;
     v.corr_dist = (float*)d_corr_dist_.p;
-    v.cand = (Cand*)d_cand_.p;
-    v.nsplit = nsplit_;
+    v.stats = (unsigned long long*)d_stats_.p;
     v.flag_list = (int32_t*)d_flag_list_.p;
     v.flag_count = (int32_t*)d_flag_count_.p;
     v.trim_key = (uint64_t*)d_trim_key_.p;
@@ -170,25 +173,80 @@ View Engine::view() const {
     v.work = (const BlockWork*)d_work_.p;
     v.nwork = nwork_;
     v.pair_rechecked = (int32_t*)d_rechecked_.p;
+    const int nnodes = 2 << tree_L_;
+    auto ref = [&](const TreeBufs& t) {
+        TreeRef r{};
+        r.L = tree_L_;
+        r.nnodes = nnodes;
+        r.perm = (const int32_t*)t.perm.p;
+        r.pos = (const int32_t*)t.pos.p;
+        r.tvec = (const float*)t.vec.p;
+        r.lo = (const float*)t.lo.p;
+        r.hi = (const float*)t.hi.p;
+        return r;
+    };
+    v.t3 = ref(t3_);
+    v.t12 = ref(t12_);
+    v.gwork = (const GroupWork*)d_gwork_.p;
+    v.ngwork = ngwork_;
     return v;
+}
+
+// ----------------------------------------------------------------------------- kd-trees
+int Engine::build_tree(int D, const float* vec, hipStream_t s) {
+    TreeBufs& tb = (D == 12) ? t12_ : t3_;
+    const int nnodes = 2 << tree_L_;
+    const size_t nb = (size_t)nclouds_ * nnodes * D;
+    if (!ensure<uint32_t>(tb.blo, nb) || !ensure<uint32_t>(tb.bhi, nb) || !ensure<float>(tb.lo, nb) ||
+        !ensure<float>(tb.hi, nb))
+        return SE3ICP_ERR_OUT_OF_MEMORY;
+    int cbits = 0;
+    while ((1 << cbits) < nclouds_) ++cbits;
+    const size_t need = tree_sort_temp_bytes((int)ntot_, 32 + tree_L_ + cbits);
+    if (!ensure<char>(d_sort_tmp_, need)) return SE3ICP_ERR_OUT_OF_MEMORY;
+    TreeView t{};
+    t.D = D;
+    t.L = tree_L_;
+    t.nnodes = nnodes;
+    t.nclouds = nclouds_;
+    t.npts = (int32_t)ntot_;
+    t.ld = ld_;
+    t.clouds = (const CloudDev*)d_clouds_.p;
+    t.cloud_of = (const int32_t*)d_cloud_of_.p;
+    t.vec = vec;
+    t.perm = (int32_t*)tb.perm.p;
+    t.pos = (int32_t*)tb.pos.p;
+    t.tvec = (float*)tb.vec.p;
+    t.blo = (uint32_t*)tb.blo.p;
+    t.bhi = (uint32_t*)tb.bhi.p;
+    t.lo = (float*)tb.lo.p;
+    t.hi = (float*)tb.hi.p;
+    if (build_trees(t, d_sort_tmp_.p, d_sort_tmp_.bytes, (unsigned long long*)d_keys0_.p,
+                    (unsigned long long*)d_keys1_.p, (int32_t*)d_vals1_.p, s) != 0)
+        return SE3ICP_ERR_HIP;
+    return 0;
 }
 
 // ----------------------------------------------------------------------------- setup
 int Engine::setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool normalize_pairs, double scale_pre,
-                         std::vector<double>* centers_out, std::vector<double>* scales_out, hipStream_t s) {
+                         bool build12, std::vector<double>* centers_out, std::vector<double>* scales_out,
+                         hipStream_t s) {
     nclouds_ = (int)clouds.size();
     h_clouds_.assign(nclouds_, CloudDev{});
     h_setup_.resize(nclouds_);
     h_chunks_.clear();
     h_inptr_.assign(nclouds_, nullptr);
     int64_t off = 0;
+    int max_n = 1;
     for (int c = 0; c < nclouds_; ++c) {
         h_clouds_[c].off = (int32_t)off;
         h_clouds_[c].n = (int32_t)clouds[c].n;
         h_setup_[c] = clouds[c].st;
+        max_n = std::max<int>(max_n, (int)clouds[c].n);
         for (int64_t p0 = 0; p0 < clouds[c].n; p0 += kChunk) h_chunks_.push_back(ChunkWork{c, (int32_t)p0});
         off += clouds[c].n;
     }
+    tree_L_ = tree_depth_for(max_n);
     // inputs
     double* d_in = (double*)d_in_.p;
     for (int c = 0; c < nclouds_; ++c) {
@@ -265,75 +323,27 @@ int Engine::setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool nor
     }
     HIPCHK(hipMemcpyAsync(d_setup_.p, h_setup_.data(), sizeof(CloudSetup) * nclouds_, hipMemcpyHostToDevice, s));
 
-    // 3) normalize in place + f32 copy + bbox
+    // 3) normalize in place + f32 copy
     launch_normalize(v, (const ChunkWork*)d_chunks_.p, nch, (double*)d_partial_.p, s);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(h_partial_, d_partial_.p, sizeof(double) * 7 * nch, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    std::vector<double> bb(6 * nclouds_);
-    for (int c = 0; c < nclouds_; ++c)
-        for (int a = 0; a < 3; ++a) { bb[6 * c + a] = 1e300; bb[6 * c + 3 + a] = -1e300; }
-    for (int k = 0; k < nch; ++k) {
-        const int c = h_chunks_[k].cloud;
-        for (int a = 0; a < 3; ++a) {
-            bb[6 * c + a] = std::min(bb[6 * c + a], h_partial_[7 * k + a]);
-            bb[6 * c + 3 + a] = std::max(bb[6 * c + 3 + a], h_partial_[7 * k + 3 + a]);
-        }
-    }
 
-    // 4) uniform grid for the clouds that need a kNN list
-    int64_t cells = 0;
-    for (int c = 0; c < nclouds_; ++c) {
-        CloudDev& cl = h_clouds_[c];
-        cl.cell_off = (int32_t)cells;
-        cl.ncells = 0;
-        const int K = h_setup_[c].k_knn;
-        if (K <= 0 || cl.n <= 0) continue;
-        double ext[3], diag2 = 0;
-        for (int a = 0; a < 3; ++a) {
-            ext[a] = std::max(bb[6 * c + 3 + a] - bb[6 * c + a], 0.0);
-            diag2 += ext[a] * ext[a];
-        }
-        const double diag = std::sqrt(diag2);
-        // cell edge ~ the expected k-NN radius of a surface sampled with n points
-        double h = 0.6 * diag * std::sqrt((double)std::min(K, cl.n) / (double)cl.n);
-        if (!(h > 0) || !std::isfinite(h)) h = std::max(diag, 1.0);
-        int64_t d[3];
-        for (int it = 0; it < 200; ++it) {
-            for (int a = 0; a < 3; ++a) d[a] = (int64_t)std::floor(ext[a] / h) + 1;
-            if (d[0] * d[1] * d[2] <= 4 * (int64_t)cl.n + 64) break;
-            h *= 1.26;
-        }
-        for (int a = 0; a < 3; ++a) {
-            cl.org[a] = bb[6 * c + a];
-            cl.dims[a] = (int32_t)d[a];
-        }
-        cl.h = h;
-        cl.inv_h = 1.0 / h;
-        cl.ncells = (int32_t)(d[0] * d[1] * d[2]);
-        cells += cl.ncells;
-    }
-    ncells_ = cells;
-    if (!ensure<int32_t>(d_cell_cnt_, cells + 1) || !ensure<int32_t>(d_cell_start_, cells + 1))
-        return SE3ICP_ERR_OUT_OF_MEMORY;
+    // 4) 3-D kd-trees of every cloud (kNN for TOLDI / normals, and the R3 NN of the loop)
+    int rc = build_tree(3, (const float*)d_xyz32_.p, s);
+    if (rc) return rc;
     v = view();
-    HIPCHK(hipMemcpyAsync(d_clouds_.p, h_clouds_.data(), sizeof(CloudDev) * nclouds_, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemsetAsync(d_norm12_.p, 0, sizeof(uint32_t) * nclouds_, s));
     HIPCHK(hipMemsetAsync(d_norm3_.p, 0, sizeof(uint32_t) * nclouds_, s));
-    if (cells > 0) {
-        HIPCHK(hipMemsetAsync(d_cell_cnt_.p, 0, sizeof(int32_t) * (cells + 1), s));
-        launch_grid_count(v, s);
-        size_t tmp = 0;
-        if (launch_grid_scan(v, (int32_t)cells, nullptr, &tmp, s) != 0) return SE3ICP_ERR_HIP;
-        if (!ensure<char>(d_scan_tmp_, tmp)) return SE3ICP_ERR_OUT_OF_MEMORY;
-        tmp = d_scan_tmp_.bytes;
-        if (launch_grid_scan(v, (int32_t)cells, d_scan_tmp_.p, &tmp, s) != 0) return SE3ICP_ERR_HIP;
-        launch_grid_scatter(v, s);
-        launch_knn(v, s);
-        HIPCHK(hipGetLastError());
-    }
+    bool any_knn = false;
+    for (int c = 0; c < nclouds_; ++c) any_knn |= h_setup_[c].k_knn > 0;
+    if (any_knn) launch_knn(v, s);
     launch_frames(v, s);
     HIPCHK(hipGetLastError());
+    // 5) 12-D kd-trees over the alpha/beta-weighted SE(3) elements
+    have12_ = build12;
+    if (build12) {
+        rc = build_tree(12, (const float*)d_fr32_.p, s);
+        if (rc) return rc;
+    }
     return 0;
 }
 
@@ -363,9 +373,9 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     ktimes_ = KernelTimes{};
 
     npairs_ = npairs;
-    int64_t ntot = 0, max_nt = 0;
-    for (int p = 0; p < npairs; ++p) { ntot += ns[p] + nt[p]; max_nt = std::max<int64_t>(max_nt, nt[p]); }
-    // work table: one entry per 256-query block of every pair's source cloud
+    int64_t ntot = 0;
+    for (int p = 0; p < npairs; ++p) ntot += ns[p] + nt[p];
+    // work table of the per-correspondence kernels: one entry per 256 queries of every pair
     h_work_.clear();
     h_wb_.assign(npairs, 0);
     h_wn_.assign(npairs, 0);
@@ -375,10 +385,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         h_wn_[p] = (int32_t)h_work_.size() - h_wb_[p];
     }
     nwork_ = (int)h_work_.size();
-    // target splits: enough blocks to fill 256 CUs several times over
-    int nsplit = (int)std::min<int64_t>(16, std::max<int64_t>(1, (4096 + nwork_ - 1) / nwork_));
-    nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(nsplit, (max_nt + 2047) / 2048));
-    int rc = alloc_points(ntot, kmax, nsplit);
+    int rc = alloc_points(ntot, kmax);
     if (rc) return rc;
     if (!ensure<PairDev>(d_pairs_, npairs) || !ensure<BlockWork>(d_work_, nwork_) || !ensure<int32_t>(d_wb_, npairs) ||
         !ensure<int32_t>(d_wn_, npairs) || !ensure<uint64_t>(d_trim_key_, npairs) ||
@@ -415,8 +422,17 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         }
     }
     std::vector<double> centers, scales;
-    rc = setup_clouds(clouds, on_device, se3, prm.scale_preprocessing, &centers, &scales, s);
+    rc = setup_clouds(clouds, on_device, se3, prm.scale_preprocessing, se3, &centers, &scales, s);
     if (rc) return rc;
+    // loop NN work: one wavefront per leaf of every source tree
+    h_gwork_.clear();
+    for (int p = 0; p < npairs; ++p)
+        for (int l = 0; l < (1 << tree_L_); ++l) h_gwork_.push_back(GroupWork{p, l});
+    ngwork_ = (int)h_gwork_.size();
+    if (!ensure<GroupWork>(d_gwork_, ngwork_)) return SE3ICP_ERR_OUT_OF_MEMORY;
+    HIPCHK(hipMemcpyAsync(d_gwork_.p, h_gwork_.data(), sizeof(GroupWork) * ngwork_, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(d_corr_idx_.p, 0xff, sizeof(int32_t) * ld_, s));  // no previous match yet
+    HIPCHK(hipMemsetAsync(d_stats_.p, 0, sizeof(unsigned long long) * 4 * kStatSlots, s));
     std::vector<uint32_t> n12(nclouds_), n3(nclouds_);
     HIPCHK(hipMemcpyAsync(n12.data(), d_norm12_.p, sizeof(uint32_t) * nclouds_, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(n3.data(), d_norm3_.p, sizeof(uint32_t) * nclouds_, hipMemcpyDeviceToHost, s));
@@ -462,7 +478,6 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     int active = npairs;
     while (active > 0) {
         bool any_se3 = false, any_r3 = false, any_trim = false;
-        double se3_pairs = 0, r3_pairs = 0;
         for (int p = 0; p < npairs; ++p) {
             PairDev& P = h_pairs_[p];
             St& S = st[p];
@@ -476,38 +491,34 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
             any_se3 |= se3_nn;
             any_r3 |= !se3_nn;
             any_trim |= S.trim;
-            (se3_nn ? se3_pairs : r3_pairs) += (double)ns[p] * (double)nt[p];
         }
         HIPCHK(hipMemcpyAsync(d_pairs_.p, h_pairs_, sizeof(PairDev) * npairs, hipMemcpyHostToDevice, s));
         HIPCHK(hipMemsetAsync(d_flag_count_.p, 0, sizeof(int32_t), s));
         HIPCHK(hipEventRecord(ev_[0], s));
-        if (any_se3) launch_sweep_se3(v, s);
+        if (any_se3) launch_nn_se3(v, s);
         HIPCHK(hipEventRecord(ev_[1], s));
-        if (any_r3) launch_sweep_r3(v, s);
+        if (any_r3) launch_nn_r3(v, s);
         HIPCHK(hipEventRecord(ev_[2], s));
-        launch_finalize(v, s);
-        HIPCHK(hipEventRecord(ev_[3], s));
         launch_recheck(v, recheck_blocks, s);
-        HIPCHK(hipEventRecord(ev_[4], s));
+        HIPCHK(hipEventRecord(ev_[3], s));
         if (any_trim) launch_trim(v, s);
-        HIPCHK(hipEventRecord(ev_[5], s));
+        HIPCHK(hipEventRecord(ev_[4], s));
         launch_reduce(v, (const int32_t*)d_wb_.p, (const int32_t*)d_wn_.p, s);
-        HIPCHK(hipEventRecord(ev_[6], s));
+        HIPCHK(hipEventRecord(ev_[5], s));
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(h_red_, d_red_out_.p, sizeof(double) * kRedVals * npairs, hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         {
-            float ms[6];
-            for (int k = 0; k < 6; ++k) HIPCHK(hipEventElapsedTime(&ms[k], ev_[k], ev_[k + 1]));
-            ktimes_.sweep_se3_ms += ms[0];
-            ktimes_.sweep_r3_ms += ms[1];
-            ktimes_.finalize_ms += ms[2];
-            ktimes_.recheck_ms += ms[3];
-            ktimes_.trim_ms += ms[4];
-            ktimes_.reduce_ms += ms[5];
-            nn_ms += ms[0] + ms[1] + ms[2] + ms[3];
-            if (any_se3) { ktimes_.sweep_se3_launches++; ktimes_.se3_pairs_evaluated += se3_pairs; }
-            if (any_r3) { ktimes_.sweep_r3_launches++; ktimes_.r3_pairs_evaluated += r3_pairs; }
+            float ms[5];
+            for (int k = 0; k < 5; ++k) HIPCHK(hipEventElapsedTime(&ms[k], ev_[k], ev_[k + 1]));
+            ktimes_.nn_se3_ms += ms[0];
+            ktimes_.nn_r3_ms += ms[1];
+            ktimes_.recheck_ms += ms[2];
+            ktimes_.trim_ms += ms[3];
+            ktimes_.reduce_ms += ms[4];
+            nn_ms += ms[0] + ms[1] + ms[2];
+            if (any_se3) ktimes_.nn_se3_launches++;
+            if (any_r3) ktimes_.nn_r3_launches++;
         }
         for (int p = 0; p < npairs; ++p) {
             St& S = st[p];
@@ -541,7 +552,18 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         }
     }
     HIPCHK(hipMemcpyAsync(h_rechecked_, d_rechecked_.p, sizeof(int32_t) * npairs, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    {
+        unsigned long long stats[4 * kStatSlots];
+        HIPCHK(hipMemcpyAsync(stats, d_stats_.p, sizeof(stats), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        double sum[4] = {0, 0, 0, 0};
+        for (int i = 0; i < kStatSlots; ++i)
+            for (int k = 0; k < 4; ++k) sum[k] += (double)stats[4 * i + k];
+        ktimes_.se3_dist_evals = sum[0];
+        ktimes_.se3_box_tests = sum[1];
+        ktimes_.r3_dist_evals = sum[2];
+        ktimes_.r3_box_tests = sum[3];
+    }
     const double t_end = wall_ms();
 
     int worst = 0;
@@ -585,14 +607,14 @@ int Engine::knn_self(const double* xyz, int64_t n, int k, int32_t* idx) {
     if (k > kMaxKnn) return SE3ICP_ERR_K_TOO_LARGE;
     HIPCHK(hipSetDevice(dev_));
     npairs_ = 0;
-    int rc = alloc_points(n, k, 1);
+    int rc = alloc_points(n, k);
     if (rc) return rc;
     std::vector<CloudReq> cl(1);
     cl[0].in = xyz;
     cl[0].n = n;
     cl[0].st.k_knn = k;
     cl[0].st.norm_scale = 1.0;
-    rc = setup_clouds(cl, false, false, 1.0, nullptr, nullptr, stream_);
+    rc = setup_clouds(cl, false, false, 1.0, false, nullptr, nullptr, stream_);
     if (rc) return rc;
     HIPCHK(hipMemcpy2DAsync(idx, sizeof(int32_t) * k, d_knn_.p, sizeof(int32_t) * kmax_, sizeof(int32_t) * k, n,
                             hipMemcpyDeviceToHost, stream_));
@@ -607,7 +629,7 @@ int Engine::toldi_frames(const double* xyz, int64_t n, int k, double* frames) {
     if (k > kMaxKnn) return SE3ICP_ERR_K_TOO_LARGE;
     HIPCHK(hipSetDevice(dev_));
     npairs_ = 0;
-    int rc = alloc_points(n, k, 1);
+    int rc = alloc_points(n, k);
     if (rc) return rc;
     std::vector<CloudReq> cl(1);
     cl[0].in = xyz;
@@ -617,19 +639,17 @@ int Engine::toldi_frames(const double* xyz, int64_t n, int k, double* frames) {
     cl[0].st.alpha = 1.0;
     cl[0].st.beta = 1.0;
     cl[0].st.norm_scale = 1.0;
-    rc = setup_clouds(cl, false, false, 1.0, nullptr, nullptr, stream_);
+    rc = setup_clouds(cl, false, false, 1.0, false, nullptr, nullptr, stream_);
     if (rc) return rc;
     std::vector<double> fr(12 * (size_t)ld_);
     HIPCHK(hipMemcpyAsync(fr.data(), d_fr64_.p, sizeof(double) * 12 * ld_, hipMemcpyDeviceToHost, stream_));
     HIPCHK(hipStreamSynchronize(stream_));
     for (int64_t i = 0; i < n; ++i) {
         double* F = frames + 16 * i;
-        const double* v12[12];
-        for (int r = 0; r < 12; ++r) v12[r] = &fr[(size_t)r * ld_ + i];
         // packing [R00 R10 R20 R01 R11 R21 R02 R12 R22 t0 t1 t2] -> row-major 4x4
         for (int r = 0; r < 3; ++r) {
-            for (int c = 0; c < 3; ++c) F[r * 4 + c] = *v12[c * 3 + r];
-            F[r * 4 + 3] = *v12[9 + r];
+            for (int c = 0; c < 3; ++c) F[r * 4 + c] = fr[(size_t)(c * 3 + r) * ld_ + i];
+            F[r * 4 + 3] = fr[(size_t)(9 + r) * ld_ + i];
         }
         F[12] = F[13] = F[14] = 0.0;
         F[15] = 1.0;
@@ -644,7 +664,7 @@ int Engine::estimate_normals(const double* xyz, int64_t n, int k, double* normal
     if (k > kMaxKnn) return SE3ICP_ERR_K_TOO_LARGE;
     HIPCHK(hipSetDevice(dev_));
     npairs_ = 0;
-    int rc = alloc_points(n, k, 1);
+    int rc = alloc_points(n, k);
     if (rc) return rc;
     std::vector<CloudReq> cl(1);
     cl[0].in = xyz;
@@ -652,7 +672,7 @@ int Engine::estimate_normals(const double* xyz, int64_t n, int k, double* normal
     cl[0].st.k_knn = k;
     cl[0].st.k_nrm = k;
     cl[0].st.norm_scale = 1.0;
-    rc = setup_clouds(cl, false, false, 1.0, nullptr, nullptr, stream_);
+    rc = setup_clouds(cl, false, false, 1.0, false, nullptr, nullptr, stream_);
     if (rc) return rc;
     std::vector<double> nr(3 * (size_t)ld_);
     HIPCHK(hipMemcpyAsync(nr.data(), d_nrm64_.p, sizeof(double) * 3 * ld_, hipMemcpyDeviceToHost, stream_));
@@ -662,6 +682,9 @@ int Engine::estimate_normals(const double* xyz, int64_t n, int k, double* normal
     return 0;
 }
 
+// Exact 1-NN of arbitrary query vectors among data vectors (3 or 12 dims): the vectors
+// are placed in the source/target slots of a one-pair batch with the identity pose, the
+// kd-trees are built over them, and the loop's NN + recheck kernels run once.
 int Engine::nn(const double* query, int64_t nq, const double* data, int64_t nd, int dim, int32_t* idx, double* d2,
                int32_t* num_rechecked) {
     if (!ok_) return SE3ICP_ERR_NO_DEVICE;
@@ -672,22 +695,17 @@ int Engine::nn(const double* query, int64_t nq, const double* data, int64_t nd, 
     npairs_ = 1;
     nclouds_ = 2;
     const int64_t ntot = nq + nd;
-    h_work_.clear();
-    for (int64_t q0 = 0; q0 < nq; q0 += kBlock) h_work_.push_back(BlockWork{0, (int32_t)q0});
-    nwork_ = (int)h_work_.size();
-    int nsplit = (int)std::min<int64_t>(16, std::max<int64_t>(1, (4096 + nwork_ - 1) / nwork_));
-    nsplit = (int)std::max<int64_t>(1, std::min<int64_t>(nsplit, (nd + 2047) / 2048));
-    int rc = alloc_points(ntot, 1, nsplit);
+    int rc = alloc_points(ntot, 1);
     if (rc) return rc;
-    if (!ensure<PairDev>(d_pairs_, 1) || !ensure<BlockWork>(d_work_, nwork_) || !ensure<CloudDev>(d_clouds_, 2) ||
-        !ensure<int32_t>(d_rechecked_, 1))
+    if (!ensure<PairDev>(d_pairs_, 1) || !ensure<CloudDev>(d_clouds_, 2) || !ensure<int32_t>(d_rechecked_, 1))
         return SE3ICP_ERR_OUT_OF_MEMORY;
     h_clouds_.assign(2, CloudDev{});
     h_clouds_[0].off = 0;
     h_clouds_[0].n = (int32_t)nq;
     h_clouds_[1].off = (int32_t)nq;
     h_clouds_[1].n = (int32_t)nd;
-    // SoA f64 masters + f32 sweep copies, filled on the host (diagnostic entry point)
+    tree_L_ = tree_depth_for((int)std::max(nq, nd));
+    // SoA f64 masters + f32 copies, filled on the host (diagnostic entry point)
     const size_t L = ld_;
     std::vector<int32_t> cof(L, 0);
     for (int64_t i = nq; i < ntot; ++i) cof[i] = 1;
@@ -717,7 +735,13 @@ int Engine::nn(const double* query, int64_t nq, const double* data, int64_t nd, 
     HIPCHK(hipMemcpyAsync(dst32, m32.data(), sizeof(float) * m32.size(), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(d_cloud_of_.p, cof.data(), sizeof(int32_t) * L, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(d_clouds_.p, h_clouds_.data(), sizeof(CloudDev) * 2, hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemcpyAsync(d_work_.p, h_work_.data(), sizeof(BlockWork) * nwork_, hipMemcpyHostToDevice, s));
+    rc = build_tree(dim, dst32, s);
+    if (rc) return rc;
+    h_gwork_.clear();
+    for (int l = 0; l < (1 << tree_L_); ++l) h_gwork_.push_back(GroupWork{0, l});
+    ngwork_ = (int)h_gwork_.size();
+    if (!ensure<GroupWork>(d_gwork_, ngwork_)) return SE3ICP_ERR_OUT_OF_MEMORY;
+    HIPCHK(hipMemcpyAsync(d_gwork_.p, h_gwork_.data(), sizeof(GroupWork) * ngwork_, hipMemcpyHostToDevice, s));
     PairDev P;
     std::memset(&P, 0, sizeof(P));
     P.T[0] = P.T[5] = P.T[10] = 1.0;
@@ -730,15 +754,10 @@ int Engine::nn(const double* query, int64_t nq, const double* data, int64_t nd, 
     HIPCHK(hipMemcpyAsync(d_pairs_.p, &P, sizeof(P), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemsetAsync(d_flag_count_.p, 0, sizeof(int32_t), s));
     HIPCHK(hipMemsetAsync(d_rechecked_.p, 0, sizeof(int32_t), s));
+    HIPCHK(hipMemsetAsync(d_corr_idx_.p, 0xff, sizeof(int32_t) * L, s));
     View v = view();
-    if (dim == 12) {
-        // the finalize kernel also reads the translation rows of fr64 for the stored
-        // distance; they are the query/data vectors themselves here.
-        launch_sweep_se3(v, s);
-    } else {
-        launch_sweep_r3(v, s);
-    }
-    launch_finalize(v, s);
+    if (dim == 12) launch_nn_se3(v, s);
+    else launch_nn_r3(v, s);
     launch_recheck(v, 512, s);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(idx, d_corr_idx_.p, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, s));

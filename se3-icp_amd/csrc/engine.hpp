@@ -25,11 +25,12 @@ struct DevBuf {
 
 // Per-kernel GPU time of the last register_batch (HIP events, ms), for bench.py.
 struct KernelTimes {
-    double sweep_se3_ms = 0, sweep_r3_ms = 0, finalize_ms = 0, recheck_ms = 0, trim_ms = 0, reduce_ms = 0;
+    double nn_se3_ms = 0, nn_r3_ms = 0, recheck_ms = 0, trim_ms = 0, reduce_ms = 0;
     double setup_ms = 0;
-    int64_t sweep_se3_launches = 0, sweep_r3_launches = 0;
-    double se3_pairs_evaluated = 0;  // sum over launches of (active queries x targets)
-    double r3_pairs_evaluated = 0;
+    int64_t nn_se3_launches = 0, nn_r3_launches = 0;
+    // work actually done by the NN kernels (device counters): lane-distance evaluations
+    // in leaf sweeps and lane-box tests in the traversal
+    double se3_dist_evals = 0, se3_box_tests = 0, r3_dist_evals = 0, r3_box_tests = 0;
 };
 
 class Engine {
@@ -61,16 +62,20 @@ class Engine {
         int64_t n = 0;
         CloudSetup st{};
     };
+    struct TreeBufs {
+        DevBuf perm, pos, vec, blo, bhi, lo, hi;
+    };
     int init();
     template <class T>
     T* ensure(DevBuf& b, size_t count);
-    int alloc_points(int64_t ntot, int kmax, int nsplit);
-    // ingest -> (normalize) -> grid -> kNN -> frames for a list of clouds.  When
-    // `normalize_pairs` is set, clouds (2p, 2p+1) are normalized together with the
-    // reference's preprocessing and scale[p] receives the factor.
+    int alloc_points(int64_t ntot, int kmax);
+    // build the D-dimensional kd-trees of every cloud over `vec` ([D][ld] f32)
+    int build_tree(int D, const float* vec, hipStream_t s);
+    // ingest -> (normalize) -> 3-D kd-trees -> kNN -> frames (-> 12-D kd-trees) for a
+    // list of clouds.  When `normalize_pairs` is set, clouds (2p, 2p+1) are normalized
+    // together with the reference's preprocessing and scale[p] receives the factor.
     int setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool normalize_pairs, double scale_pre,
-                     std::vector<double>* centers, std::vector<double>* scales, hipStream_t s);
-    int upload_tables(hipStream_t s);
+                     bool build12, std::vector<double>* centers, std::vector<double>* scales, hipStream_t s);
     View view() const;
 
     int dev_;
@@ -83,20 +88,22 @@ class Engine {
     // geometry of the current batch
     int nclouds_ = 0, npairs_ = 0;
     int64_t ntot_ = 0;
-    int ld_ = 0, kmax_ = 1, nsplit_ = 1, nwork_ = 0;
-    int64_t ncells_ = 0;
+    int ld_ = 0, kmax_ = 1, nwork_ = 0, ngwork_ = 0, tree_L_ = 0;
+    bool have12_ = false;
     std::vector<CloudDev> h_clouds_;
     std::vector<CloudSetup> h_setup_;
     std::vector<BlockWork> h_work_;
+    std::vector<GroupWork> h_gwork_;
     std::vector<int32_t> h_wb_, h_wn_;
     std::vector<ChunkWork> h_chunks_;
     std::vector<const double*> h_inptr_;
 
     // device buffers
     DevBuf d_clouds_, d_setup_, d_pairs_, d_cloud_of_, d_inptr_, d_in_, d_xyz64_, d_xyz32_, d_fr64_, d_fr32_, d_nrm64_,
-        d_cov64_, d_conf64_, d_knn_, d_cell_cnt_, d_cell_start_, d_slot_, d_sidx_, d_sxyz_, d_norm12_, d_norm3_,
-        d_corr_idx_, d_corr_dist_, d_cand_, d_flag_list_, d_flag_count_, d_trim_key_, d_red_partial_, d_red_out_,
-        d_work_, d_wb_, d_wn_, d_chunks_, d_partial_, d_centers_, d_scan_tmp_, d_rechecked_;
+        d_cov64_, d_conf64_, d_knn_, d_norm12_, d_norm3_, d_corr_idx_, d_corr_dist_, d_flag_list_, d_flag_count_,
+        d_trim_key_, d_red_partial_, d_red_out_, d_work_, d_gwork_, d_wb_, d_wn_, d_chunks_, d_partial_, d_centers_,
+        d_rechecked_, d_keys0_, d_keys1_, d_vals1_, d_sort_tmp_, d_stats_;
+    TreeBufs t3_, t12_;
     // pinned host mirrors
     PairDev* h_pairs_ = nullptr;
     double* h_red_ = nullptr;

@@ -1,14 +1,8 @@
 // k_loop.hip — kernels of one ICP iteration (gfx950), batched over every active pair.
 //
-//   sweep_se3   brute-force 1-NN under the weighted SE(3) metric (12-D L2),
-//               update_correspondences_raw_flann_SE3 ISR.cpp:444-470.  f32, LDS-tiled
-//               targets (broadcast ds_read_b128), per query the best (d1,i1) and the
-//               second-best distance d2 for the certification below.
-//   sweep_r3    same in 3-D, update_correspondences_kd_tree_XYZ ISR.cpp:402-416.
-//   finalize    merges target splits, computes the stored R3 distance in f64
-//               (ISR.cpp:465-468, 411-413) and certifies the f32 arg-min: when the gap
-//               d2-d1 is below twice a rigorous f32 error bound the query is queued for
-//   recheck     an exact f64 sweep in nanoflann's arithmetic (ties -> lowest index).
+//   (the correspondence search itself is k_nn.hip)
+//   recheck     queries whose f32 arg-min k_nn.hip could not certify: an exact f64 sweep
+//               in nanoflann's arithmetic (ties -> lowest index).
 //   trim        PCL CorrespondenceRejectorTrimmed: the floor(ratio*N)-th smallest
 //               (float dist, query) key by MSB radix select (ISR.cpp:669-671).
 //   reduce      per-correspondence Jacobian terms of the estimator, summed per block:
@@ -22,238 +16,15 @@
 #include <climits>
 #include <cmath>
 
-#include "view.hpp"
+#include "loopdev.hpp"
 
 namespace se3icp {
 
 namespace {
 
-constexpr int kTile = 256;  // targets staged per LDS tile
-
-// query = T * M0 for the 12-vector packing [R(:,0) R(:,1) R(:,2) t] (ISR.cpp:713-716).
-__device__ __forceinline__ void pose_frame(const double* T, const double* m, double* q) {
-#pragma unroll
-    for (int c = 0; c < 3; ++c)
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-            q[c * 3 + r] = T[r * 4 + 0] * m[c * 3 + 0] + T[r * 4 + 1] * m[c * 3 + 1] + T[r * 4 + 2] * m[c * 3 + 2];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) q[9 + r] = T[r * 4 + 0] * m[9] + T[r * 4 + 1] * m[10] + T[r * 4 + 2] * m[11] + T[r * 4 + 3];
-}
-__device__ __forceinline__ void pose_point(const double* T, double x, double y, double z, double* q) {
-#pragma unroll
-    for (int r = 0; r < 3; ++r) q[r] = T[r * 4 + 0] * x + T[r * 4 + 1] * y + T[r * 4 + 2] * z + T[r * 4 + 3];
-}
-
-__device__ __forceinline__ void load_T(const PairDev* P, double* T) {
-#pragma unroll
-    for (int i = 0; i < 12; ++i) T[i] = P->T[i];
-}
-
-// f64 query vector of source point g of pair P in the current phase.
-template <int D>
-__device__ __forceinline__ void query_f64(const View& v, const double* T, int g, double* q) {
-    if constexpr (D == 12) {
-        double m[12];
-#pragma unroll
-        for (int r = 0; r < 12; ++r) m[r] = v.fr64[(size_t)r * v.ld + g];
-        pose_frame(T, m, q);
-    } else {
-        pose_point(T, v.xyz64[g], v.xyz64[v.ld + g], v.xyz64[2 * (size_t)v.ld + g], q);
-    }
-}
-
-// ------------------------------------------------------------------ sweeps
-template <int D>
-__global__ __launch_bounds__(256) void k_sweep(View v) {
-    constexpr int NV = (D + 3) / 4;  // float4 per target
-    __shared__ float4 tile[kTile * NV];
-    const BlockWork w = v.work[blockIdx.x];
-    const PairDev* P = v.pairs + w.pair;
-    if (P->phase != (D == 12 ? PHASE_SE3 : PHASE_R3)) return;
-    const CloudDev cs = v.clouds[P->src], ct = v.clouds[P->tgt];
-    const int split = blockIdx.y, S = gridDim.y;
-    const int tb = (int)((long long)ct.n * split / S), te = (int)((long long)ct.n * (split + 1) / S);
-    const int qi = w.q0 + threadIdx.x;
-    const bool valid = qi < cs.n;
-    float q[D];
-    {
-        double T[12], Q[D];
-        load_T(P, T);
-        query_f64<D>(v, T, cs.off + (valid ? qi : 0), Q);
-        if constexpr (D == 3) {
-            Q[0] -= P->f32_center[0]; Q[1] -= P->f32_center[1]; Q[2] -= P->f32_center[2];
-        }
-#pragma unroll
-        for (int r = 0; r < D; ++r) q[r] = (float)Q[r];
-    }
-    const float* src = (D == 12) ? v.fr32 : v.xyz32;
-    float d1 = INFINITY, d2 = INFINITY;
-    int i1 = -1;
-    for (int t0 = tb; t0 < te; t0 += kTile) {
-        {
-            const int t = t0 + (int)threadIdx.x;
-            float a[NV * 4];
-#pragma unroll
-            for (int r = 0; r < NV * 4; ++r) a[r] = 0.f;
-            if (t < te) {
-                const int gt = ct.off + t;
-#pragma unroll
-                for (int r = 0; r < D; ++r) a[r] = src[(size_t)r * v.ld + gt];
-            } else {
-#pragma unroll
-                for (int r = 0; r < D; ++r) a[r] = 1e18f;  // padding: never the nearest
-            }
-#pragma unroll
-            for (int k = 0; k < NV; ++k) tile[threadIdx.x * NV + k] = make_float4(a[4 * k], a[4 * k + 1], a[4 * k + 2], a[4 * k + 3]);
-        }
-        __syncthreads();
-#pragma unroll 4
-        for (int j = 0; j < kTile; ++j) {
-            float acc;
-            if constexpr (D == 12) {
-                const float4 A = tile[j * 3], B = tile[j * 3 + 1], C = tile[j * 3 + 2];
-                float e;
-                e = q[0] - A.x; acc = e * e;
-                e = q[1] - A.y; acc = fmaf(e, e, acc);
-                e = q[2] - A.z; acc = fmaf(e, e, acc);
-                e = q[3] - A.w; acc = fmaf(e, e, acc);
-                e = q[4] - B.x; acc = fmaf(e, e, acc);
-                e = q[5] - B.y; acc = fmaf(e, e, acc);
-                e = q[6] - B.z; acc = fmaf(e, e, acc);
-                e = q[7] - B.w; acc = fmaf(e, e, acc);
-                e = q[8] - C.x; acc = fmaf(e, e, acc);
-                e = q[9] - C.y; acc = fmaf(e, e, acc);
-                e = q[10] - C.z; acc = fmaf(e, e, acc);
-                e = q[11] - C.w; acc = fmaf(e, e, acc);
-            } else {
-                const float4 A = tile[j];
-                float e;
-                e = q[0] - A.x; acc = e * e;
-                e = q[1] - A.y; acc = fmaf(e, e, acc);
-                e = q[2] - A.z; acc = fmaf(e, e, acc);
-            }
-            const bool lt = acc < d1;
-            d2 = __builtin_amdgcn_fmed3f(d1, d2, acc);
-            d1 = lt ? acc : d1;
-            i1 = lt ? (t0 + j) : i1;
-        }
-        __syncthreads();
-    }
-    if (valid) v.cand[(size_t)split * v.ld + cs.off + qi] = Cand{d1, i1, d2};
-}
-
-// ------------------------------------------------------------------ finalize
-// Rigorous bound on |f32 distance - exact distance of the f64 vectors| (DESIGN.md
-// "Certified f32 arg-min"): inputs rounded to f32 (u = 2^-24), D differences and a
-// D-term FMA chain.  na, nb bound the norms of the query and target vectors.
-__device__ __forceinline__ float f32_err(float d, float na, float nb, int D) {
-    const float u = 5.9604645e-08f;
-    const float s = na + nb;
-    return 1.25f * (2.f * u * s * sqrtf(fmaxf(d, 0.f)) + (float)(D + 3) * u * d + 4.f * u * u * s * s) + 1e-30f;
-}
-
-__device__ __forceinline__ double l2_nanoflann12(const double* a, const double* b) {
-#pragma clang fp contract(off)
-    double result = 0.0;
-#pragma unroll
-    for (int d = 0; d < 12; d += 4) {
-        const double d0 = a[d] - b[d], d1 = a[d + 1] - b[d + 1], d2 = a[d + 2] - b[d + 2], d3 = a[d + 3] - b[d + 3];
-        result += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
-    }
-    return result;
-}
-__device__ __forceinline__ double l2_nanoflann3(const double* a, const double* b) {
-#pragma clang fp contract(off)
-    const double d0 = a[0] - b[0], d1 = a[1] - b[1], d2 = a[2] - b[2];
-    return (d0 * d0 + d1 * d1) + d2 * d2;
-}
-
-// target search vector j (12-D: alpha-weighted rotation rows + translation rows;
-// for run_se3_icp_with_cf the translation rows are the points, ISR.cpp:834-836)
-__device__ __forceinline__ void target12(const View& v, const CloudDev& ct, bool cf, int j, double* b) {
-    const int gt = ct.off + j;
-#pragma unroll
-    for (int r = 0; r < 9; ++r) b[r] = v.fr64[(size_t)r * v.ld + gt];
-    if (cf) {
-        b[9] = v.xyz64[gt]; b[10] = v.xyz64[v.ld + gt]; b[11] = v.xyz64[2 * (size_t)v.ld + gt];
-    } else {
-        b[9] = v.fr64[9 * (size_t)v.ld + gt]; b[10] = v.fr64[10 * (size_t)v.ld + gt]; b[11] = v.fr64[11 * (size_t)v.ld + gt];
-    }
-}
-
-// stored distance: R3 distance between the translation parts (ISR.cpp:465: uses the
-// beta-weighted target_se3_cloud_ translation even in the cf variant) or the 3-D NN distance
-__device__ __forceinline__ float stored_dist(const View& v, int phase, const CloudDev& ct, const double* Q, int j) {
-    const int gt = ct.off + j;
-    if (phase == PHASE_SE3) {
-        const double dx = Q[9] - v.fr64[9 * (size_t)v.ld + gt];
-        const double dy = Q[10] - v.fr64[10 * (size_t)v.ld + gt];
-        const double dz = Q[11] - v.fr64[11 * (size_t)v.ld + gt];
-        return (float)sqrt((dx * dx + dy * dy) + dz * dz);
-    }
-    const double b[3] = {v.xyz64[gt], v.xyz64[v.ld + gt], v.xyz64[2 * (size_t)v.ld + gt]};
-    return (float)sqrt(l2_nanoflann3(Q, b));
-}
-
-__global__ __launch_bounds__(256) void k_finalize(View v) {
-    const BlockWork w = v.work[blockIdx.x];
-    const PairDev* P = v.pairs + w.pair;
-    const int phase = P->phase;
-    if (phase == PHASE_IDLE) return;
-    const CloudDev cs = v.clouds[P->src], ct = v.clouds[P->tgt];
-    const int qi = w.q0 + threadIdx.x;
-    if (qi >= cs.n) return;
-    const int g = cs.off + qi;
-    Cand c = v.cand[g];
-    float d1 = c.d1, d2 = c.d2;
-    int i1 = c.i1;
-    for (int s = 1; s < v.nsplit; ++s) {
-        const Cand o = v.cand[(size_t)s * v.ld + g];
-        if (o.d1 < d1 || (o.d1 == d1 && o.i1 >= 0 && (i1 < 0 || o.i1 < i1))) {
-            d2 = fminf(d1, o.d2);
-            d1 = o.d1;
-            i1 = o.i1;
-        } else {
-            d2 = fminf(d2, o.d1);
-        }
-    }
-    double T[12], Q[12];
-    load_T(P, T);
-    float na;
-    int D;
-    float nb;
-    if (phase == PHASE_SE3) {
-        query_f64<12>(v, T, g, Q);
-        double n2 = 0;
-#pragma unroll
-        for (int r = 0; r < 12; ++r) n2 += Q[r] * Q[r];
-        na = (float)sqrt(n2) * 1.000001f;
-        nb = P->tgt_norm12;
-        D = 12;
-    } else {
-        query_f64<3>(v, T, g, Q);
-        const double fx = Q[0] - P->f32_center[0], fy = Q[1] - P->f32_center[1], fz = Q[2] - P->f32_center[2];
-        na = (float)sqrt(fx * fx + fy * fy + fz * fz) * 1.000001f;
-        nb = P->tgt_norm3;
-        D = 3;
-    }
-    const bool flag = (i1 < 0) || !(d2 - d1 > 2.f * f32_err(d2, na, nb, D));
-    if (flag && ct.n > 1) {
-        const int at = atomicAdd(v.flag_count, 1);
-        v.flag_list[at] = g;
-        atomicAdd(&v.pair_rechecked[w.pair], 1);
-    }
-    if (i1 < 0) i1 = 0;  // NaN query: the reference's zero-initialised result index
-    v.corr_idx[g] = i1;
-    v.corr_dist[g] = stored_dist(v, phase, ct, Q, i1);
-}
+using namespace loopdev;
 
 // ------------------------------------------------------------------ recheck (exact f64)
-__device__ __forceinline__ bool key_less(double da, int ia, double db, int ib) {
-    return da < db || (da == db && ia < ib);
-}
-
 __global__ __launch_bounds__(256) void k_recheck(View v) {
     __shared__ double s_d[4];
     __shared__ int s_i[4];
@@ -497,7 +268,9 @@ __global__ __launch_bounds__(256) void k_reduce(View v) {
                     wgt = wc * wc;
                 }
             }
-            for (int rr = 0; rr < nrows; ++rr) {
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr) {
+                if (rr >= nrows) break;
                 int k = 0;
 #pragma unroll
                 for (int a = 0; a < 6; ++a)
@@ -551,15 +324,6 @@ __global__ __launch_bounds__(256) void k_reduce_final(View v, const int32_t* pai
 
 }  // namespace
 
-void launch_sweep_se3(const View& v, hipStream_t s) {
-    hipLaunchKernelGGL(k_sweep<12>, dim3(v.nwork, v.nsplit), dim3(256), 0, s, v);
-}
-void launch_sweep_r3(const View& v, hipStream_t s) {
-    hipLaunchKernelGGL(k_sweep<3>, dim3(v.nwork, v.nsplit), dim3(256), 0, s, v);
-}
-void launch_finalize(const View& v, hipStream_t s) {
-    hipLaunchKernelGGL(k_finalize, dim3(v.nwork), dim3(256), 0, s, v);
-}
 void launch_recheck(const View& v, int nblocks, hipStream_t s) {
     hipLaunchKernelGGL(k_recheck, dim3(nblocks), dim3(256), 0, s, v);
 }

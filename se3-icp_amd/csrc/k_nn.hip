@@ -1,0 +1,208 @@
+// k_nn.hip — the correspondence search of one ICP iteration, batched over every active pair.
+//
+//   SE(3) phase: exact 1-NN of each source SE(3) element under the weighted SE(3) metric
+//                (12-D L2), update_correspondences_raw_flann_SE3 ISR.cpp:444-470;
+//   R3 phase:    exact 3-D 1-NN, update_correspondences_kd_tree_XYZ ISR.cpp:402-416.
+//
+// One wavefront = one leaf (<= 64 points) of the SOURCE kd-tree, i.e. 64 queries close
+// together in the search space (the pose acts on the 12-D/3-D vectors as an isometry, so
+// a leaf stays compact as the source moves).  The wave walks the TARGET kd-tree depth
+// first; a node is entered when some lane's f32 box bound is below that lane's pruning
+// threshold, and a leaf's <= 64 targets are staged through LDS and swept with broadcast
+// ds_read_b128 while each lane keeps (d1, i1, d2).  The previous iteration's match seeds
+// the threshold.  The f32 arg-min is then certified (k_loop.hip recheck handles the rest):
+//   thr = d1 + 3 err(d1)  => every unvisited target is > 2 err farther than the winner,
+//   and among the visited ones the gap d2 - d1 must exceed 2 err(d2).
+#include <hip/hip_runtime.h>
+
+#include "loopdev.hpp"
+#include "tree.hpp"
+
+namespace se3icp {
+
+namespace {
+
+using namespace loopdev;
+
+constexpr int kWaves = 4;
+constexpr int kStack = 64;
+
+template <int D>
+__device__ __forceinline__ float box_lb(const float* lo, const float* hi, const float* q) {
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const float e = fmaxf(fmaxf(lo[d] - q[d], q[d] - hi[d]), 0.f);
+        s = fmaf(e, e, s);
+    }
+    return s;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_nn_group(View v) {
+    constexpr int NV = (D + 3) / 4;
+    __shared__ float4 s_tile[kWaves][kLeafMax * NV];
+    __shared__ int s_stack[kWaves][kStack];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int gi = blockIdx.x * kWaves + wid;
+    if (gi >= v.ngwork) return;
+    const GroupWork w = v.gwork[gi];
+    const PairDev* P = v.pairs + w.pair;
+    const int phase = P->phase;
+    if (phase != (D == 12 ? PHASE_SE3 : PHASE_R3)) return;
+    const CloudDev cs = v.clouds[P->src], ct = v.clouds[P->tgt];
+    const TreeRef TR = (D == 12) ? v.t12 : v.t3;
+    const int a = tree_first(cs.n, TR.L, w.leaf), b = tree_first(cs.n, TR.L, w.leaf + 1);
+    if (b <= a) return;
+    const bool valid = lane < b - a;
+    const int g = cs.off + (valid ? TR.perm[cs.off + a + lane] : TR.perm[cs.off + a]);
+
+    // query: f64 pose applied to the source element, rounded to f32
+    double Tm[12], Q[D];
+    load_T(P, Tm);
+    query_f64<D>(v, Tm, g, Q);
+    float q[D];
+    float na;
+    {
+        double n2 = 0;
+#pragma unroll
+        for (int r = 0; r < D; ++r) {
+            const double c = (D == 3) ? Q[r] - P->f32_center[r] : Q[r];
+            q[r] = (float)c;
+            n2 += c * c;
+        }
+        na = (float)sqrt(n2) * 1.000001f;
+    }
+    const float nb = (D == 12) ? P->tgt_norm12 : P->tgt_norm3;
+    const float* tv = TR.tvec + ct.off;
+    const size_t ld = v.ld;
+
+    float d1 = INFINITY, d2 = INFINITY;
+    int i1 = -1;  // target tree position of the best candidate
+    float thr = valid ? INFINITY : -1.f;
+    if (valid) {  // seed the pruning threshold with the previous match
+        const int prev = v.corr_idx[g];
+        if (prev >= 0 && prev < ct.n) {
+            const int tp = TR.pos[ct.off + prev];
+            float s = 0.f;
+#pragma unroll
+            for (int r = 0; r < D; ++r) {
+                const float e = q[r] - tv[(size_t)r * ld + tp];
+                s = fmaf(e, e, s);
+            }
+            thr = s + 3.f * f32_err(s, na, nb, D);
+        }
+    }
+
+    const float* box_lo = TR.lo + (size_t)P->tgt * TR.nnodes * D;
+    const float* box_hi = TR.hi + (size_t)P->tgt * TR.nnodes * D;
+    const int first_leaf = (1 << TR.L) - 1;
+    float4* tile = s_tile[wid];
+    int* stk = s_stack[wid];
+    if (lane == 0) stk[0] = 0;
+    int sp = 1;
+    unsigned n_eval = 0, n_box = 0;  // wave-uniform work counters (roofline accounting)
+    while (sp > 0) {
+        __builtin_amdgcn_wave_barrier();
+        const int h = __builtin_amdgcn_readfirstlane(stk[sp - 1]);
+        --sp;
+        if (h >= first_leaf) {
+            const int li = h - first_leaf;
+            const int ta = tree_first(ct.n, TR.L, li), tb = tree_first(ct.n, TR.L, li + 1);
+            const int cnt = tb - ta;
+            if (cnt <= 0) continue;
+            __builtin_amdgcn_wave_barrier();
+            if (lane < cnt) {
+                float e[NV * 4];
+#pragma unroll
+                for (int r = 0; r < NV * 4; ++r) e[r] = (r < D) ? tv[(size_t)r * ld + ta + lane] : 0.f;
+#pragma unroll
+                for (int k = 0; k < NV; ++k) tile[lane * NV + k] = make_float4(e[4 * k], e[4 * k + 1], e[4 * k + 2], e[4 * k + 3]);
+            }
+            __builtin_amdgcn_wave_barrier();
+            for (int j = 0; j < cnt; ++j) {
+                float acc;
+                if constexpr (D == 12) {
+                    const float4 A = tile[j * 3], B = tile[j * 3 + 1], C = tile[j * 3 + 2];
+                    float e;
+                    e = q[0] - A.x; acc = e * e;
+                    e = q[1] - A.y; acc = fmaf(e, e, acc);
+                    e = q[2] - A.z; acc = fmaf(e, e, acc);
+                    e = q[3] - A.w; acc = fmaf(e, e, acc);
+                    e = q[4] - B.x; acc = fmaf(e, e, acc);
+                    e = q[5] - B.y; acc = fmaf(e, e, acc);
+                    e = q[6] - B.z; acc = fmaf(e, e, acc);
+                    e = q[7] - B.w; acc = fmaf(e, e, acc);
+                    e = q[8] - C.x; acc = fmaf(e, e, acc);
+                    e = q[9] - C.y; acc = fmaf(e, e, acc);
+                    e = q[10] - C.z; acc = fmaf(e, e, acc);
+                    e = q[11] - C.w; acc = fmaf(e, e, acc);
+                } else {
+                    const float4 A = tile[j];
+                    float e;
+                    e = q[0] - A.x; acc = e * e;
+                    e = q[1] - A.y; acc = fmaf(e, e, acc);
+                    e = q[2] - A.z; acc = fmaf(e, e, acc);
+                }
+                const bool lt = acc < d1;
+                d2 = __builtin_amdgcn_fmed3f(d1, d2, acc);
+                d1 = lt ? acc : d1;
+                i1 = lt ? (ta + j) : i1;  // target tree position
+            }
+            if (valid && d1 < INFINITY) thr = fminf(thr, d1 + 3.f * f32_err(d1, na, nb, D));
+            n_eval += cnt;
+            continue;
+        }
+        n_box += 2;
+        const int hl = 2 * h + 1, hr = 2 * h + 2;
+        const float ll = box_lb<D>(box_lo + (size_t)hl * D, box_hi + (size_t)hl * D, q);
+        const float lr = box_lb<D>(box_lo + (size_t)hr * D, box_hi + (size_t)hr * D, q);
+        // the f32 bound is within (D+2) ulps of the exact distance to the (inflated) box
+        const bool vl = __ballot(ll * (1.f - 2e-6f) < thr) != 0ull;
+        const bool vr = __ballot(lr * (1.f - 2e-6f) < thr) != 0ull;
+        const bool left_first = __builtin_amdgcn_readfirstlane(ll <= lr ? 1 : 0) != 0;
+        const int nearh = left_first ? hl : hr, farh = left_first ? hr : hl;
+        const bool vnear = left_first ? vl : vr, vfar = left_first ? vr : vl;
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {
+            if (vfar) stk[sp] = farh;
+            if (vnear) stk[sp + (vfar ? 1 : 0)] = nearh;
+        }
+        sp += (vfar ? 1 : 0) + (vnear ? 1 : 0);
+    }
+
+    if (lane == 0) {  // 64 lanes per evaluation; 64 counter slots against contention
+        unsigned long long* st = v.stats + 4 * (gi & 63) + (D == 12 ? 0 : 2);
+        atomicAdd(st, 64ull * n_eval);
+        atomicAdd(st + 1, 64ull * n_box);
+    }
+    if (!valid) return;
+    // certification (see the header) and the stored distance
+    const bool flag = (i1 < 0) || !(d2 - d1 > 2.f * f32_err(d2, na, nb, D));
+    if (flag && ct.n > 1) {
+        const int at = atomicAdd(v.flag_count, 1);
+        v.flag_list[at] = g;
+        atomicAdd(&v.pair_rechecked[w.pair], 1);
+    }
+    // tree position -> target index; a NaN query keeps the reference's zero-initialised index
+    i1 = (i1 < 0) ? 0 : TR.perm[ct.off + i1];
+    v.corr_idx[g] = i1;
+    if constexpr (D == 12) {
+        v.corr_dist[g] = stored_dist(v, PHASE_SE3, ct, Q, i1);
+    } else {
+        double Q12[12];
+        Q12[0] = Q[0]; Q12[1] = Q[1]; Q12[2] = Q[2];
+        v.corr_dist[g] = stored_dist(v, PHASE_R3, ct, Q12, i1);
+    }
+}
+
+}  // namespace
+
+void launch_nn_se3(const View& v, hipStream_t s) {
+    hipLaunchKernelGGL(k_nn_group<12>, dim3((v.ngwork + kWaves - 1) / kWaves), dim3(64 * kWaves), 0, s, v);
+}
+void launch_nn_r3(const View& v, hipStream_t s) {
+    hipLaunchKernelGGL(k_nn_group<3>, dim3((v.ngwork + kWaves - 1) / kWaves), dim3(64 * kWaves), 0, s, v);
+}
+
+}  // namespace se3icp

@@ -1,0 +1,56 @@
+// tree.hpp — implicit balanced kd-trees (k_tree.hip) and their query helpers.
+//
+// Tree of a cloud with n points and depth L: node i of level l covers the tree
+// positions [n*i/2^l, n*(i+1)/2^l); heap index 2^l - 1 + i; leaves are level L.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "common.hpp"
+
+namespace se3icp {
+
+constexpr int kLeafMax = 64;  // points per leaf (one wavefront)
+
+struct TreeView {
+    int32_t D;        // 3 or 12
+    int32_t L;        // depth (leaves at level L)
+    int32_t nnodes;   // 2^(L+1) nodes reserved per cloud (heap order)
+    int32_t nclouds;
+    int32_t npts;
+    int32_t ld;
+    const CloudDev* clouds;
+    const int32_t* cloud_of;
+    const float* vec;  // [D][ld] input vectors, original order
+    int32_t* perm;     // [ld] tree position (global slot) -> local point index
+    int32_t* pos;      // [ld] point (global slot) -> local tree position
+    float* tvec;       // [D][ld] vectors in tree order
+    uint32_t* blo;     // [nclouds][nnodes][D] build scratch (orderable bits)
+    uint32_t* bhi;
+    float* lo;         // [nclouds][nnodes][D] node boxes
+    float* hi;
+};
+
+__host__ __device__ __forceinline__ int tree_first(int n, int level, int i) {
+    return (int)(((long long)n * i) >> level);
+}
+// node of level `level` containing local tree position x
+__host__ __device__ __forceinline__ int tree_node_of(int x, int n, int level) {
+    const long long v = ((long long)(x + 1) << level) + n - 1;
+    return (int)(v / n) - 1;
+}
+__host__ __device__ __forceinline__ int tree_heap(int level, int i) { return (1 << level) - 1 + i; }
+
+inline int tree_depth_for(int max_n) {
+    int L = 0;
+    while (((long long)max_n + (1ll << L) - 1) >> L > kLeafMax) ++L;
+    return L;
+}
+
+int build_trees(TreeView t, void* sort_tmp, size_t sort_tmp_bytes, unsigned long long* keys0,
+                unsigned long long* keys1, int32_t* vals1, hipStream_t s);
+size_t tree_sort_temp_bytes(int npts, int end_bit);
+
+}  // namespace se3icp

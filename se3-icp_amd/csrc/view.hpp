@@ -24,6 +24,23 @@ struct CloudSetup {
     double f32_center[3];   // xyz32 = float(p' - f32_center)
 };
 
+// Read-only view of the kd-trees of one dimension (tree.hpp) for the query kernels.
+struct TreeRef {
+    int32_t L;        // depth: leaves at level L
+    int32_t nnodes;   // heap slots per cloud
+    const int32_t* perm;  // [ld] tree position (cloud.off + x) -> local point index
+    const int32_t* pos;   // [ld] point (cloud.off + i) -> local tree position
+    const float* tvec;    // [D][ld] vectors in tree order
+    const float* lo;      // [nclouds][nnodes][D]
+    const float* hi;
+};
+
+// One wavefront of the loop's NN kernel = one leaf (<= 64 queries) of a source tree.
+struct GroupWork {
+    int32_t pair;
+    int32_t leaf;
+};
+
 struct View {
     int32_t ld;        // SoA row stride (total points of the batch, padded to 64)
     int32_t npts;      // real points of the batch (per-point kernels stop here)
@@ -43,20 +60,13 @@ struct View {
     double* cov64;
     double* conf64;
     int32_t* knn;
-    // uniform grid
-    int32_t* cell_cnt;
-    int32_t* cell_start;
-    int32_t* slot;
-    int32_t* sidx;
-    double* sxyz;
     // per-cloud f32 error-bound norms (float bits, atomicMax)
     uint32_t* norm12_bits;
     uint32_t* norm3_bits;
     // loop
     int32_t* corr_idx;
     float* corr_dist;
-    Cand* cand;        // [nsplit * ld]
-    int32_t nsplit;
+    unsigned long long* stats;  // [4] NN work counters: se3 dist evals, se3 box tests, r3 dist evals, r3 box tests
     int32_t* flag_list;
     int32_t* flag_count;  // [1]
     uint64_t* trim_key;   // [npairs]
@@ -65,6 +75,10 @@ struct View {
     const BlockWork* work;
     int32_t nwork;
     int32_t* pair_rechecked;  // [npairs]
+    // kd-trees (k_tree.hip) over the f32 vectors: 3-D points (xyz32) and 12-D SE(3) elements (fr32)
+    TreeRef t3, t12;
+    const GroupWork* gwork;   // [ngwork] source leaves of every pair
+    int32_t ngwork;
 };
 
 // ---- k_setup.hip
@@ -77,16 +91,14 @@ void launch_radius(const View& v, const ChunkWork* chunks, int nchunks, const do
                    double* partial /*[nchunks]*/, hipStream_t s);
 void launch_normalize(const View& v, const ChunkWork* chunks, int nchunks, double* partial /*[nchunks*7]*/,
                       hipStream_t s);
-void launch_grid_count(const View& v, hipStream_t s);
-int launch_grid_scan(const View& v, int32_t ncells_total, void* temp, size_t* temp_bytes, hipStream_t s);
-void launch_grid_scatter(const View& v, hipStream_t s);
 void launch_knn(const View& v, hipStream_t s);
 void launch_frames(const View& v, hipStream_t s);
 
 // ---- k_loop.hip
-void launch_sweep_se3(const View& v, hipStream_t s);
-void launch_sweep_r3(const View& v, hipStream_t s);
-void launch_finalize(const View& v, hipStream_t s);
+// exact 1-NN of every active pair's source points, one wavefront per source leaf,
+// traversing the target kd-tree (12-D in the SE(3) phase, 3-D in the R3 phase)
+void launch_nn_se3(const View& v, hipStream_t s);
+void launch_nn_r3(const View& v, hipStream_t s);
 void launch_recheck(const View& v, int nblocks, hipStream_t s);
 void launch_trim(const View& v, hipStream_t s);
 void launch_reduce(const View& v, const int32_t* pair_wb, const int32_t* pair_wn, hipStream_t s);

@@ -125,14 +125,17 @@ def _street_scene(rng, length: float) -> _Scene:
     return sc
 
 
-def kitti_like_sequence(n_scans: int, seed: int = 4, n_az: int = 1915, n_beams: int = 64, step: float = 1.0,
-                        max_yaw_deg: float = 2.0, range_noise: float = 0.02, max_range: float = 80.0):
+def kitti_like_sequence(n_scans: int, seed: int = 4, n_az: int = 1975, n_beams: int = 64, step: float = 1.0,
+                        max_yaw_deg: float = 2.0, range_noise: float = 0.02, max_range: float = 80.0,
+                        scan_indices=None):
     """Return (scans, poses): scans[k] is an (N_k, 3) float64 cloud in the sensor frame of
-    scan k, poses[k] its 4x4 world pose.  ~120k points per scan at the defaults."""
+    scan k, poses[k] its 4x4 world pose.  ~120k points per scan at the defaults.
+    ``scan_indices`` ray-casts only those scans (others are None); every scan has its
+    own generator stream, so a subset is identical to the same scans of the full run."""
     rng = np.random.Generator(np.random.PCG64(seed))
     sc = _street_scene(rng, step * n_scans)
     elev = np.deg2rad(np.linspace(-24.8, 2.0, n_beams))
-    scans, poses = [], []
+    poses = []
     yaw = 0.0
     pos = np.array([0.0, 0.0, 1.73])
     for k in range(n_scans):
@@ -140,29 +143,38 @@ def kitti_like_sequence(n_scans: int, seed: int = 4, n_az: int = 1915, n_beams: 
             yaw += np.deg2rad(rng.uniform(-max_yaw_deg, max_yaw_deg)) * 0.5
             pos = pos + np.array([np.cos(yaw), np.sin(yaw), 0.0]) * step * rng.uniform(0.9, 1.1)
             pos[1] = np.clip(pos[1], -2.5, 2.5)
-        Rw = rot_3d(0, 0, yaw)
-        az = np.linspace(0, 2 * np.pi, n_az, endpoint=False) + rng.uniform(0, 2 * np.pi / n_az)
-        E, A = np.meshgrid(elev + rng.normal(0, 0.0005, n_beams), az, indexing="ij")
+        poses.append(make_T(rot_3d(0, 0, yaw), pos))
+    want = set(range(n_scans)) if scan_indices is None else set(scan_indices)
+    scans = []
+    for k in range(n_scans):
+        if k not in want:
+            scans.append(None)
+            continue
+        srng = np.random.Generator(np.random.PCG64([seed, k]))
+        Rw, pk = poses[k][:3, :3], poses[k][:3, 3]
+        az = np.linspace(0, 2 * np.pi, n_az, endpoint=False) + srng.uniform(0, 2 * np.pi / n_az)
+        E, A = np.meshgrid(elev + srng.normal(0, 0.0005, n_beams), az, indexing="ij")
         d = np.stack([np.cos(E) * np.cos(A), np.cos(E) * np.sin(A), np.sin(E)], axis=-1).reshape(-1, 3)
         dw = d @ Rw.T
         ts = []
         for c0 in range(0, d.shape[0], 16384):
-            ts.append(sc.cast(pos, dw[c0:c0 + 16384], max_range))
+            ts.append(sc.cast(pk, dw[c0:c0 + 16384], max_range))
         t = np.concatenate(ts)
         ok = np.isfinite(t) & (t > 1.0)
-        t = t[ok] + rng.normal(0, range_noise, ok.sum())
-        pts = d[ok] * t[:, None]
-        scans.append(np.ascontiguousarray(pts))
-        poses.append(make_T(Rw, pos))
+        t = t[ok] + srng.normal(0, range_noise, ok.sum())
+        scans.append(np.ascontiguousarray(d[ok] * t[:, None]))
     return scans, poses
 
 
-def kitti_like_pairs(n_pairs: int, seed: int = 4, **kw):
+def kitti_like_pairs(n_pairs: int, seed: int = 4, first: int = 0, total_pairs: int | None = None, **kw):
     """Consecutive-scan pairs (source = scan i+1, target = scan i, examples/benchmark_kitti.cpp:130-131)
-    with ground truth T = pose[i]^-1 pose[i+1]."""
-    scans, poses = kitti_like_sequence(n_pairs + 1, seed=seed, **kw)
+    with ground truth T = pose[i]^-1 pose[i+1].  Pairs first .. first+n_pairs-1 of a
+    sequence of total_pairs (default n_pairs) pairs."""
+    total = (first + n_pairs) if total_pairs is None else total_pairs
+    idx = range(first, first + n_pairs + 1)
+    scans, poses = kitti_like_sequence(total + 1, seed=seed, scan_indices=idx, **kw)
     pairs, gts = [], []
-    for i in range(n_pairs):
+    for i in range(first, first + n_pairs):
         pairs.append((scans[i + 1], scans[i]))
         gts.append(np.linalg.inv(poses[i]) @ poses[i + 1])
     return pairs, gts

@@ -276,8 +276,8 @@ def nearest_neighbors(query, data, device: int = 0):
 
 
 def last_kernel_times(device: int = 0) -> dict:
-    out = (C.c_double * 10)()
+    out = (C.c_double * 12)()
     _lib.check(_lib.load().se3icp_last_kernel_times(device, out))
-    keys = ["sweep_se3_ms", "sweep_r3_ms", "finalize_ms", "recheck_ms", "trim_ms", "reduce_ms", "setup_ms",
-            "sweep_se3_launches", "se3_pairs_evaluated", "r3_pairs_evaluated"]
+    keys = ["nn_se3_ms", "nn_r3_ms", "recheck_ms", "trim_ms", "reduce_ms", "setup_ms", "nn_se3_launches",
+            "nn_r3_launches", "se3_dist_evals", "se3_box_tests", "r3_dist_evals", "r3_box_tests"]
     return dict(zip(keys, list(out)))
