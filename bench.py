@@ -152,8 +152,12 @@ def main():
         rot_errs = [rot_err_deg(r.T, g) for r, g in zip(last, gts)]
         tr_errs = [float(np.linalg.norm(r.T[:3, 3] - g[:3, 3])) for r, g in zip(last, gts)]
         # dominant kernel + roofline (HIP events around every launch, on the engine's stream)
-        kms = {k: ktot.get(k, 0.0) for k in ["nn_se3_ms", "nn_r3_ms", "recheck_ms", "trim_ms", "reduce_ms"]}
-        dom = max(["nn_se3_ms", "nn_r3_ms"], key=lambda k: kms[k])
+        kms = {k: ktot.get(k, 0.0) for k in ["nn_se3_ms", "nn_r3_ms", "recheck_ms", "trim_ms", "reduce_ms", "lrf_ms"]}
+        nq = max(1.0, ktot.get("lrf_queries", 0.0))
+        lrf_work = {"queries_per_step": ktot.get("lrf_queries", 0.0) / args.steps,
+                    "leaves_per_query": round(ktot.get("lrf_leaves", 0.0) / nq, 2),
+                    "merges_per_query": round(ktot.get("lrf_merges", 0.0) / nq, 2)}
+        dom = max(["nn_se3_ms", "nn_r3_ms"], key=lambda k: kms[k])  # dominant kernel of the ICP loop
         if dom == "nn_se3_ms":
             D, evals, boxes, nl, kname = 12, ktot["se3_dist_evals"], ktot["se3_box_tests"], ktot["nn_se3_launches"], \
                 "k_nn_group<12>"
@@ -193,6 +197,7 @@ def main():
             "iterations_per_pair_mean": round(iters_all / total_pairs, 2),
             "accuracy_vs_gt": {"rot_deg_max": round(max(rot_errs), 4), "trans_m_max": round(max(tr_errs), 4)},
             "kernel_ms_per_step": {k: round(v / args.steps, 3) for k, v in kms.items()},
+            "lrf_work": lrf_work,
             "roofline": {
                 "kernel": kname,
                 "bound": "mfma",

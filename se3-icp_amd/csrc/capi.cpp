@@ -273,7 +273,7 @@ int se3icp_set_profiling(int device, int on) {
     return 0;
 }
 
-int se3icp_last_kernel_times(int device, double* out /* [12] */) {
+int se3icp_last_kernel_times(int device, double* out /* [16] */) {
     Engine* e = usable_engine(device);
     if (!e || !out) return SE3ICP_ERR_NO_DEVICE;
     const auto& k = e->kernel_times();
@@ -289,6 +289,10 @@ int se3icp_last_kernel_times(int device, double* out /* [12] */) {
     out[9] = k.se3_box_tests;
     out[10] = k.r3_dist_evals;
     out[11] = k.r3_box_tests;
+    out[12] = k.lrf_ms;
+    out[13] = k.lrf_queries;
+    out[14] = k.lrf_leaves;
+    out[15] = k.lrf_merges;
     return 0;
 }
 

@@ -34,35 +34,39 @@ __device__ inline d3 jacobi_smallest_evec(double a00, double a01, double a02, do
             const int p = (r == 2) ? 1 : 0;
             const int q = (r == 0) ? 1 : 2;
             const double apq = a[p][q];
-            if (apq == 0.0) continue;
-            const double theta = (a[q][q] - a[p][p]) / (2.0 * apq);
-            const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-            const double c = 1.0 / sqrt(t * t + 1.0);
-            const double s = t * c;
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const double akp = a[k][p], akq = a[k][q];
-                a[k][p] = c * akp - s * akq;
-                a[k][q] = s * akp + c * akq;
-            }
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const double apk = a[p][k], aqk = a[q][k];
-                a[p][k] = c * apk - s * aqk;
-                a[q][k] = s * apk + c * aqk;
-            }
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const double vkp = v[k][p], vkq = v[k][q];
-                v[k][p] = c * vkp - s * vkq;
-                v[k][q] = s * vkp + c * vkq;
+            if (apq != 0.0) {
+                const double theta = (a[q][q] - a[p][p]) / (2.0 * apq);
+                const double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+                const double c = 1.0 / sqrt(t * t + 1.0);
+                const double s = t * c;
+    #pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const double akp = a[k][p], akq = a[k][q];
+                    a[k][p] = c * akp - s * akq;
+                    a[k][q] = s * akp + c * akq;
+                }
+    #pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const double apk = a[p][k], aqk = a[q][k];
+                    a[p][k] = c * apk - s * aqk;
+                    a[q][k] = s * apk + c * aqk;
+                }
+    #pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const double vkp = v[k][p], vkq = v[k][q];
+                    v[k][p] = c * vkp - s * vkq;
+                    v[k][q] = s * vkp + c * vkq;
+                }
             }
         }
     }
-    int m = 0;
-    if (a[1][1] < a[m][m]) m = 1;
-    if (a[2][2] < a[m][m]) m = 2;
-    return d3{v[0][m], v[1][m], v[2][m]};
+    // column of the smallest diagonal entry, as a 0/1-weighted sum: a select between
+    // array elements would be turned back into a runtime-indexed (scratch) load
+    const bool m1 = a[1][1] < a[0][0];
+    const bool m2 = a[2][2] < (m1 ? a[1][1] : a[0][0]);
+    const double w2 = m2 ? 1.0 : 0.0, w1 = (!m2 && m1) ? 1.0 : 0.0, w0 = 1.0 - w1 - w2;
+    return d3{w0 * v[0][0] + w1 * v[0][1] + w2 * v[0][2], w0 * v[1][0] + w1 * v[1][1] + w2 * v[1][2],
+              w0 * v[2][0] + w1 * v[2][1] + w2 * v[2][2]};
 }
 
 // Open3D FastEigen3x3 helpers (Geometric Tools "RobustEigenSymmetric3x3").

@@ -88,7 +88,7 @@ Engine::~Engine() {
     if (!ok_) return;
     (void)hipSetDevice(dev_);
     DevBuf* all[] = {&d_clouds_, &d_setup_, &d_pairs_, &d_cloud_of_, &d_inptr_, &d_in_, &d_xyz64_, &d_xyz32_,
-                     &d_fr64_, &d_fr32_, &d_nrm64_, &d_cov64_, &d_conf64_, &d_knn_, &d_norm12_, &d_norm3_,
+                     &d_fr64_, &d_fr32_, &d_nrm64_, &d_cov64_, &d_conf64_, &d_knn_,
                      &d_corr_idx_, &d_corr_dist_, &d_flag_list_, &d_flag_count_, &d_trim_key_, &d_red_partial_,
                      &d_red_out_, &d_work_, &d_gwork_, &d_wb_, &d_wn_, &d_chunks_, &d_partial_, &d_centers_,
                      &d_rechecked_, &d_keys0_, &d_keys1_, &d_vals1_, &d_sort_tmp_, &d_stats_,
@@ -121,16 +121,17 @@ T* Engine::ensure(DevBuf& b, size_t count) {
     return static_cast<T*>(b.p);
 }
 
-int Engine::alloc_points(int64_t ntot, int kmax) {
+int Engine::alloc_points(int64_t ntot, int kmax, bool knn_list) {
     if (ntot >= (int64_t)1 << 30) return SE3ICP_ERR_INVALID_ARG;
     ntot_ = ntot;
     ld_ = (int)((std::max<int64_t>(ntot, 1) + 63) / 64 * 64);
     kmax_ = std::max(kmax, 1);
+    knn_list_ = knn_list;
     const size_t L = (size_t)ld_;
     bool ok = ensure<int32_t>(d_cloud_of_, L) && ensure<double>(d_in_, 3 * L) && ensure<double>(d_xyz64_, 3 * L) &&
               ensure<float>(d_xyz32_, 3 * L) && ensure<double>(d_fr64_, 12 * L) && ensure<float>(d_fr32_, 12 * L) &&
               ensure<double>(d_nrm64_, 3 * L) && ensure<double>(d_cov64_, 6 * L) && ensure<double>(d_conf64_, L) &&
-              ensure<int32_t>(d_knn_, L * kmax_) && ensure<int32_t>(d_corr_idx_, L) && ensure<float>(d_corr_dist_, L) &&
+              (!knn_list || ensure<int32_t>(d_knn_, L * kmax_)) && ensure<int32_t>(d_corr_idx_, L) && ensure<float>(d_corr_dist_, L) &&
               ensure<int32_t>(d_flag_list_, L) && ensure<int32_t>(d_flag_count_, 4) &&
               ensure<unsigned long long>(d_keys0_, L) && ensure<unsigned long long>(d_keys1_, L) &&
               ensure<int32_t>(d_vals1_, L) && ensure<unsigned long long>(d_stats_, 4 * kStatSlots);
@@ -159,9 +160,7 @@ View Engine::view() const {
     v.nrm64 = (double*)d_nrm64_.p;
     v.cov64 = (double*)d_cov64_.p;
     v.conf64 = (double*)d_conf64_.p;
-    v.knn = (int32_t*)d_knn_.p;
-    v.norm12_bits = (uint32_t*)d_norm12_.p;
-    v.norm3_bits = (uint32_t*)d_norm3_.p;
+    v.knn = knn_list_ ? (int32_t*)d_knn_.p : nullptr;
     v.corr_idx = (int32_t*)d_corr_idx_.p;
     v.corr_dist = (float*)d_corr_dist_.p;
     v.stats = (unsigned long long*)d_stats_.p;
@@ -181,6 +180,7 @@ View Engine::view() const {
         r.perm = (const int32_t*)t.perm.p;
         r.pos = (const int32_t*)t.pos.p;
         r.tvec = (const float*)t.vec.p;
+        r.tvec64 = (const double*)t.vec64.p;
         r.lo = (const float*)t.lo.p;
         r.hi = (const float*)t.hi.p;
         return r;
@@ -193,12 +193,12 @@ View Engine::view() const {
 }
 
 // ----------------------------------------------------------------------------- kd-trees
-int Engine::build_tree(int D, const float* vec, hipStream_t s) {
+int Engine::build_tree(int D, const float* vec, hipStream_t s, const double* vec64) {
     TreeBufs& tb = (D == 12) ? t12_ : t3_;
     const int nnodes = 2 << tree_L_;
     const size_t nb = (size_t)nclouds_ * nnodes * D;
     if (!ensure<uint32_t>(tb.blo, nb) || !ensure<uint32_t>(tb.bhi, nb) || !ensure<float>(tb.lo, nb) ||
-        !ensure<float>(tb.hi, nb))
+        !ensure<float>(tb.hi, nb) || (vec64 && !ensure<double>(tb.vec64, (size_t)D * ld_)))
         return SE3ICP_ERR_OUT_OF_MEMORY;
     int cbits = 0;
     while ((1 << cbits) < nclouds_) ++cbits;
@@ -217,6 +217,8 @@ int Engine::build_tree(int D, const float* vec, hipStream_t s) {
     t.perm = (int32_t*)tb.perm.p;
     t.pos = (int32_t*)tb.pos.p;
     t.tvec = (float*)tb.vec.p;
+    t.vec64 = vec64;
+    t.tvec64 = vec64 ? (double*)tb.vec64.p : nullptr;
     t.blo = (uint32_t*)tb.blo.p;
     t.bhi = (uint32_t*)tb.bhi.p;
     t.lo = (float*)tb.lo.p;
@@ -224,6 +226,27 @@ int Engine::build_tree(int D, const float* vec, hipStream_t s) {
     if (build_trees(t, d_sort_tmp_.p, d_sort_tmp_.bytes, (unsigned long long*)d_keys0_.p,
                     (unsigned long long*)d_keys1_.p, (int32_t*)d_vals1_.p, s) != 0)
         return SE3ICP_ERR_HIP;
+    return 0;
+}
+
+// Upper bound of |x| over each cloud's tree vectors, from the (inflated) root box.
+int Engine::root_norms(const TreeBufs& tb, int D, std::vector<float>* out, hipStream_t s) {
+    const int nnodes = 2 << tree_L_;
+    std::vector<float> lo((size_t)nclouds_ * D), hi((size_t)nclouds_ * D);
+    HIPCHK(hipMemcpy2DAsync(lo.data(), sizeof(float) * D, tb.lo.p, sizeof(float) * D * nnodes, sizeof(float) * D,
+                            nclouds_, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpy2DAsync(hi.data(), sizeof(float) * D, tb.hi.p, sizeof(float) * D * nnodes, sizeof(float) * D,
+                            nclouds_, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    out->assign(nclouds_, 0.f);
+    for (int c = 0; c < nclouds_; ++c) {
+        double n2 = 0;
+        for (int d = 0; d < D; ++d) {
+            const double m = std::max(std::fabs((double)lo[(size_t)c * D + d]), std::fabs((double)hi[(size_t)c * D + d]));
+            n2 += m * m;
+        }
+        (*out)[c] = (float)(std::sqrt(n2) * (1.0 + 1e-6));
+    }
     return 0;
 }
 
@@ -261,8 +284,7 @@ int Engine::setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool nor
     const int nch = (int)h_chunks_.size();
     if (!ensure<CloudDev>(d_clouds_, nclouds_) || !ensure<CloudSetup>(d_setup_, nclouds_) ||
         !ensure<ChunkWork>(d_chunks_, nch) || !ensure<const double*>(d_inptr_, nclouds_) ||
-        !ensure<double>(d_partial_, (size_t)nch * 9) || !ensure<double>(d_centers_, 3 * (size_t)nclouds_) ||
-        !ensure<uint32_t>(d_norm12_, nclouds_) || !ensure<uint32_t>(d_norm3_, nclouds_))
+        !ensure<double>(d_partial_, (size_t)nch * 9) || !ensure<double>(d_centers_, 3 * (size_t)nclouds_))
         return SE3ICP_ERR_OUT_OF_MEMORY;
     if (pinned(h_partial_, h_partial_cap_, (size_t)nch * 9 + 8)) return SE3ICP_ERR_OUT_OF_MEMORY;
     HIPCHK(hipMemcpyAsync(d_clouds_.p, h_clouds_.data(), sizeof(CloudDev) * nclouds_, hipMemcpyHostToDevice, s));
@@ -328,15 +350,30 @@ int Engine::setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool nor
     HIPCHK(hipGetLastError());
 
     // 4) 3-D kd-trees of every cloud (kNN for TOLDI / normals, and the R3 NN of the loop)
-    int rc = build_tree(3, (const float*)d_xyz32_.p, s);
+    int rc = build_tree(3, (const float*)d_xyz32_.p, s, (const double*)d_xyz64_.p);
     if (rc) return rc;
     v = view();
-    HIPCHK(hipMemsetAsync(d_norm12_.p, 0, sizeof(uint32_t) * nclouds_, s));
-    HIPCHK(hipMemsetAsync(d_norm3_.p, 0, sizeof(uint32_t) * nclouds_, s));
     bool any_knn = false;
     for (int c = 0; c < nclouds_; ++c) any_knn |= h_setup_[c].k_knn > 0;
-    if (any_knn) launch_knn(v, s);
-    launch_frames(v, s);
+    if (any_knn) {
+        HIPCHK(hipMemsetAsync(d_stats_.p, 0, sizeof(unsigned long long) * 4 * kStatSlots, s));
+        HIPCHK(hipEventRecord(ev_[6], s));
+        launch_lrf(v, knn_list_ ? 1 : 0, s);
+        HIPCHK(hipEventRecord(ev_[7], s));
+        HIPCHK(hipGetLastError());
+        unsigned long long stats[4 * kStatSlots];
+        HIPCHK(hipMemcpyAsync(stats, d_stats_.p, sizeof(stats), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        double sum[4] = {0, 0, 0, 0};
+        for (int i = 0; i < kStatSlots; ++i)
+            for (int k = 0; k < 4; ++k) sum[k] += (double)stats[4 * i + k];
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, ev_[6], ev_[7]));
+        ktimes_.lrf_ms = ms;
+        ktimes_.lrf_queries = sum[0];
+        ktimes_.lrf_leaves = sum[1];
+        ktimes_.lrf_merges = sum[2];
+    }
     HIPCHK(hipGetLastError());
     // 5) 12-D kd-trees over the alpha/beta-weighted SE(3) elements
     have12_ = build12;
@@ -433,10 +470,11 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     HIPCHK(hipMemcpyAsync(d_gwork_.p, h_gwork_.data(), sizeof(GroupWork) * ngwork_, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemsetAsync(d_corr_idx_.p, 0xff, sizeof(int32_t) * ld_, s));  // no previous match yet
     HIPCHK(hipMemsetAsync(d_stats_.p, 0, sizeof(unsigned long long) * 4 * kStatSlots, s));
-    std::vector<uint32_t> n12(nclouds_), n3(nclouds_);
-    HIPCHK(hipMemcpyAsync(n12.data(), d_norm12_.p, sizeof(uint32_t) * nclouds_, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpyAsync(n3.data(), d_norm3_.p, sizeof(uint32_t) * nclouds_, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    // norm bounds of the target search vectors (f32 error certificate) from the root boxes
+    std::vector<float> n12, n3;
+    rc = root_norms(t3_, 3, &n3, s);
+    if (!rc && se3) rc = root_norms(t12_, 12, &n12, s);
+    if (rc) return rc;
     const double t_setup = wall_ms();
     ktimes_.setup_ms = t_setup - t_begin;
 
@@ -465,11 +503,8 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         P.cf = mi.kind == KIND_CF;
         P.trim = st[p].trim;
         P.nkeep = st[p].nkeep;
-        float f12, f3;
-        std::memcpy(&f12, &n12[2 * p + 1], 4);
-        std::memcpy(&f3, &n3[2 * p + 1], 4);
-        P.tgt_norm12 = f12;
-        P.tgt_norm3 = f3;
+        P.tgt_norm12 = se3 ? n12[2 * p + 1] : 0.f;
+        P.tgt_norm3 = n3[2 * p + 1];
         for (int a = 0; a < 3; ++a) P.f32_center[a] = h_setup_[2 * p].f32_center[a];
     }
     View v = view();
@@ -607,7 +642,7 @@ int Engine::knn_self(const double* xyz, int64_t n, int k, int32_t* idx) {
     if (k > kMaxKnn) return SE3ICP_ERR_K_TOO_LARGE;
     HIPCHK(hipSetDevice(dev_));
     npairs_ = 0;
-    int rc = alloc_points(n, k);
+    int rc = alloc_points(n, k, true);
     if (rc) return rc;
     std::vector<CloudReq> cl(1);
     cl[0].in = xyz;

@@ -31,6 +31,8 @@ struct KernelTimes {
     // work actually done by the NN kernels (device counters): lane-distance evaluations
     // in leaf sweeps and lane-box tests in the traversal
     double se3_dist_evals = 0, se3_box_tests = 0, r3_dist_evals = 0, r3_box_tests = 0;
+    // fused kNN/TOLDI/normals kernel of the setup: time, queries, leaves scanned, sorts
+    double lrf_ms = 0, lrf_queries = 0, lrf_leaves = 0, lrf_merges = 0;
 };
 
 class Engine {
@@ -63,14 +65,15 @@ class Engine {
         CloudSetup st{};
     };
     struct TreeBufs {
-        DevBuf perm, pos, vec, blo, bhi, lo, hi;
+        DevBuf perm, pos, vec, vec64, blo, bhi, lo, hi;
     };
     int init();
     template <class T>
     T* ensure(DevBuf& b, size_t count);
-    int alloc_points(int64_t ntot, int kmax);
+    int alloc_points(int64_t ntot, int kmax, bool knn_list = false);
     // build the D-dimensional kd-trees of every cloud over `vec` ([D][ld] f32)
-    int build_tree(int D, const float* vec, hipStream_t s);
+    int build_tree(int D, const float* vec, hipStream_t s, const double* vec64 = nullptr);
+    int root_norms(const TreeBufs& tb, int D, std::vector<float>* out, hipStream_t s);
     // ingest -> (normalize) -> 3-D kd-trees -> kNN -> frames (-> 12-D kd-trees) for a
     // list of clouds.  When `normalize_pairs` is set, clouds (2p, 2p+1) are normalized
     // together with the reference's preprocessing and scale[p] receives the factor.
@@ -89,7 +92,7 @@ class Engine {
     int nclouds_ = 0, npairs_ = 0;
     int64_t ntot_ = 0;
     int ld_ = 0, kmax_ = 1, nwork_ = 0, ngwork_ = 0, tree_L_ = 0;
-    bool have12_ = false;
+    bool have12_ = false, knn_list_ = false;
     std::vector<CloudDev> h_clouds_;
     std::vector<CloudSetup> h_setup_;
     std::vector<BlockWork> h_work_;
@@ -100,7 +103,7 @@ class Engine {
 
     // device buffers
     DevBuf d_clouds_, d_setup_, d_pairs_, d_cloud_of_, d_inptr_, d_in_, d_xyz64_, d_xyz32_, d_fr64_, d_fr32_, d_nrm64_,
-        d_cov64_, d_conf64_, d_knn_, d_norm12_, d_norm3_, d_corr_idx_, d_corr_dist_, d_flag_list_, d_flag_count_,
+        d_cov64_, d_conf64_, d_knn_, d_corr_idx_, d_corr_dist_, d_flag_list_, d_flag_count_,
         d_trim_key_, d_red_partial_, d_red_out_, d_work_, d_gwork_, d_wb_, d_wn_, d_chunks_, d_partial_, d_centers_,
         d_rechecked_, d_keys0_, d_keys1_, d_vals1_, d_sort_tmp_, d_stats_;
     TreeBufs t3_, t12_;

@@ -1,18 +1,24 @@
-// k_knn.hip — exact k nearest neighbours of every point in its own cloud
-// (KDTreeFlann::SearchKNN, ISR.cpp:253 for TOLDI and Open3D EstimateNormals for the
-// normals), one wavefront per query point, over the cloud's 3-D kd-tree (k_tree.hip).
-//
-// The wave first scans the query's own leaf, then walks the tree depth first
-// (nearer child first) and visits a node only while the node's box can still hold a
-// point at or below the current k-th distance.  Candidates are kept as (d2, index)
-// keys in f64 with nanoflann's arithmetic; the top list (<= 128) and a staging area
-// share one 256-entry LDS buffer that a register bitonic network re-sorts when full.
-// Ties go to the lowest index.
+// k_knn.hip — per-point local geometry from the k nearest neighbours, fused:
+//   * exact kNN of the point in its own cloud (KDTreeFlann::SearchKNN, ISR.cpp:253),
+//   * the TOLDI local reference frame -> alpha/beta-weighted SE(3) 12-vector
+//     (computeSingleTOLDISE3Frame ISR.cpp:241-316, weights ISR.cpp:597-607),
+//   * Open3D EstimateNormals on the k_nrm nearest (ISR.cpp:643, :43) and the GICP
+//     covariance Rx diag(eps,1,1) Rx^T (ISR.cpp:33-52).
+// One wavefront per point, points taken in kd-tree order so that neighbouring waves
+// touch the same leaves.  The wave scans the point's own leaf, then climbs the tree
+// and descends into each sibling subtree whose box can still hold a point at or below
+// the current k-th distance (register stack, near child first).  Candidates are
+// (d2, index) keys in f64 with nanoflann's arithmetic (ties -> lowest index), kept in
+// a 256-entry LDS buffer re-sorted by a register bitonic network.  The TOLDI and
+// normal sums over neighbour ranks are then wave reductions (the reference sums them
+// sequentially; the difference is rounding only).
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
 #include <climits>
+#include <cstdlib>
 
+#include "devmath.hpp"
 #include "tree.hpp"
 #include "view.hpp"
 
@@ -22,7 +28,6 @@ namespace {
 
 constexpr int kWaves = 4;
 constexpr int kBuf = 256;
-constexpr int kStack = 64;
 
 __device__ __forceinline__ double l2_3(double ax, double ay, double az, double bx, double by, double bz) {
 #pragma clang fp contract(off)
@@ -32,6 +37,12 @@ __device__ __forceinline__ double l2_3(double ax, double ay, double az, double b
 
 __device__ __forceinline__ bool key_less(double da, int ia, double db, int ib) {
     return da < db || (da == db && ia < ib);
+}
+
+__device__ __forceinline__ double wsum(double x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
 }
 
 // ascending sort of the wave's 256 (d2, idx) keys: 4 keys per lane, bitonic network,
@@ -59,7 +70,8 @@ __device__ __forceinline__ void wave_bitonic256(double* bd, int* bi, int lane, i
                     const bool up = (e & k) == 0;
                     const bool lower = (e & jd) == 0;
                     const bool take = (lower == up) ? key_less(pd, pi, kd[s], ki[s]) : key_less(kd[s], ki[s], pd, pi);
-                    if (take) { kd[s] = pd; ki[s] = pi; }
+                    kd[s] = take ? pd : kd[s];
+                    ki[s] = take ? pi : ki[s];
                 }
             } else {
 #pragma unroll
@@ -68,10 +80,10 @@ __device__ __forceinline__ void wave_bitonic256(double* bd, int* bi, int lane, i
                         const int t = s | jd;
                         const bool up = ((lane * 4 + s) & k) == 0;
                         const bool sw = up ? key_less(kd[t], ki[t], kd[s], ki[s]) : key_less(kd[s], ki[s], kd[t], ki[t]);
-                        if (sw) {
-                            const double td = kd[s]; kd[s] = kd[t]; kd[t] = td;
-                            const int ti = ki[s]; ki[s] = ki[t]; ki[t] = ti;
-                        }
+                        const double ds = kd[s], dt = kd[t];
+                        const int is = ki[s], it = ki[t];
+                        kd[s] = sw ? dt : ds; kd[t] = sw ? ds : dt;
+                        ki[s] = sw ? it : is; ki[t] = sw ? is : it;
                     }
                 }
             }
@@ -84,7 +96,7 @@ __device__ __forceinline__ void wave_bitonic256(double* bd, int* bi, int lane, i
     }
 }
 
-// squared distance from q to a 3-D box (f32, conservative)
+// squared distance from q to a 3-D box (f32; the boxes are inflated to bound the f64 points)
 __device__ __forceinline__ float box_lb3(const float* lo, const float* hi, float qx, float qy, float qz) {
     const float dx = fmaxf(fmaxf(lo[0] - qx, qx - hi[0]), 0.f);
     const float dy = fmaxf(fmaxf(lo[1] - qy, qy - hi[1]), 0.f);
@@ -92,50 +104,63 @@ __device__ __forceinline__ float box_lb3(const float* lo, const float* hi, float
     return dx * dx + dy * dy + dz * dz;
 }
 
-__global__ __launch_bounds__(256) void k_knn_tree(View v) {
+template <int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_lrf(View v, int write_knn, int dbg_skip) {
     __shared__ double s_d[kWaves][kBuf];
     __shared__ int s_i[kWaves][kBuf];
-    __shared__ int s_stack[kWaves][kStack];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int g = blockIdx.x * kWaves + wid;
-    if (g >= v.npts) return;
-    const int c = v.cloud_of[g];
-    const int K = v.setup[c].k_knn;
+    // global slot of the 3-D tree order; made wave-uniform so that the per-cloud records
+    // and the node boxes below are scalar loads
+    const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wid);
+    if (w >= v.npts) return;
+    const int c = v.cloud_of[w];
+    const CloudSetup st = v.setup[c];
+    const int K = st.k_knn;
     if (K == 0) return;
     const CloudDev cl = v.clouds[c];
     const TreeRef T = v.t3;
+    const int n = cl.n;
+    const int gp = cl.off + T.perm[w];  // the query point
     double* bd = s_d[wid];
     int* bi = s_i[wid];
-    int* stk = s_stack[wid];
-    const double qx = v.xyz64[g], qy = v.xyz64[v.ld + g], qz = v.xyz64[2 * (size_t)v.ld + g];
-    const float fx = v.xyz32[g], fy = v.xyz32[v.ld + g], fz = v.xyz32[2 * (size_t)v.ld + g];
+    const double* X = v.xyz64 + cl.off;
+    const double* Y = v.xyz64 + v.ld + cl.off;
+    const double* Z = v.xyz64 + 2 * (size_t)v.ld + cl.off;
+    const double* TX = T.tvec64;  // tree-ordered f64 coordinates: one coalesced load per leaf
+    const double* TY = T.tvec64 + v.ld;
+    const double* TZ = T.tvec64 + 2 * (size_t)v.ld;
+    const double qx = TX[w], qy = TY[w], qz = TZ[w];
+    const float fx = T.tvec[w], fy = T.tvec[v.ld + w], fz = T.tvec[2 * (size_t)v.ld + w];
     const float* box_lo = T.lo + (size_t)c * T.nnodes * 3;
     const float* box_hi = T.hi + (size_t)c * T.nnodes * 3;
-    const int Kw = min(K, cl.n);
+    const int Kw = min(K, n);
     const int first_leaf = (1 << T.L) - 1;
-    const int own = first_leaf + tree_node_of(T.pos[g], cl.n, T.L);
-    int nTop = 0, nStg = 0;
+    const int own = first_leaf + tree_node_of(w - cl.off, n, T.L);
+
+    // ---------------------------------------------------------------- kNN
+    int nTop = 0, nStg = 0, n_leaves = 0, n_merges = 0;
     double thr = DBL_MAX;
     int thr_i = INT_MAX;
-
-    auto merge = [&]() {
+    auto merge = [&]() __attribute__((always_inline)) {
         __builtin_amdgcn_wave_barrier();
         wave_bitonic256(bd, bi, lane, nTop + nStg);
         __builtin_amdgcn_wave_barrier();
         nTop = min(Kw, nTop + nStg);
         nStg = 0;
+        ++n_merges;
         if (nTop == Kw) { thr = bd[Kw - 1]; thr_i = bi[Kw - 1]; }
     };
-    auto leaf = [&](int h) {
+    auto leaf = [&](int h) __attribute__((always_inline)) {
         const int i = h - first_leaf;
-        const int a = tree_first(cl.n, T.L, i), b = tree_first(cl.n, T.L, i + 1);
+        ++n_leaves;
+        const int a = tree_first(n, T.L, i), b = tree_first(n, T.L, i + 1);
         bool acc = false;
         double d = DBL_MAX;
         int li = INT_MAX;
         if (lane < b - a) {
-            li = T.perm[cl.off + a + lane];
-            const int gp = cl.off + li;
-            d = l2_3(qx, qy, qz, v.xyz64[gp], v.xyz64[v.ld + gp], v.xyz64[2 * (size_t)v.ld + gp]);
+            const int slot = cl.off + a + lane;
+            li = T.perm[slot];
+            d = l2_3(qx, qy, qz, TX[slot], TY[slot], TZ[slot]);
             acc = (nTop < Kw) || key_less(d, li, thr, thr_i);
         }
         const unsigned long long m = __ballot(acc);
@@ -145,44 +170,180 @@ __global__ __launch_bounds__(256) void k_knn_tree(View v) {
             bi[at] = li;
         }
         nStg += __popcll(m);
-        if (nTop + nStg > kBuf - kLeafMax) merge();
+        // establish the k-th distance as soon as k candidates exist, then merge when full
+        if ((nTop < Kw && nTop + nStg >= Kw) || nTop + nStg > kBuf - kLeafMax) merge();
+    };
+    auto open = [&](int h) __attribute__((always_inline)) {  // may the subtree at h hold a better candidate?
+        if (nTop < Kw) return true;
+        const float lb = box_lb3(box_lo + 3 * h, box_hi + 3 * h, fx, fy, fz);
+        return (double)lb * (1.0 - 1e-6) <= thr;
     };
 
     leaf(own);
-    int sp = 0;
-    if (lane == 0) stk[0] = 0;
-    sp = 1;
-    while (sp > 0) {
-        __builtin_amdgcn_wave_barrier();
-        const int h = __builtin_amdgcn_readfirstlane(stk[sp - 1]);
-        --sp;
-        if (h >= first_leaf) {
-            if (h != own) leaf(h);
-            continue;
+    for (int node = own; node > 0; node = (node - 1) >> 1) {
+        const int sib = (node & 1) ? node + 1 : node - 1;
+        if (!open(sib)) continue;
+        int stk = 0, sp = 0;  // stack in a VGPR: lane i holds entry i
+        stk = (lane == sp) ? sib : stk;
+        ++sp;
+        while (sp > 0) {
+            const int h = __builtin_amdgcn_readlane(stk, sp - 1);
+            --sp;
+            if (h >= first_leaf) {
+                leaf(h);
+                continue;
+            }
+            const int hl = 2 * h + 1, hr = 2 * h + 2;
+            const float ll = box_lb3(box_lo + 3 * hl, box_hi + 3 * hl, fx, fy, fz);
+            const float lr = box_lb3(box_lo + 3 * hr, box_hi + 3 * hr, fx, fy, fz);
+            const bool vl = (nTop < Kw) || (double)ll * (1.0 - 1e-6) <= thr;
+            const bool vr = (nTop < Kw) || (double)lr * (1.0 - 1e-6) <= thr;
+            const bool lf = ll <= lr;
+            const int nearh = lf ? hl : hr, farh = lf ? hr : hl;
+            if (lf ? vr : vl) { stk = (lane == sp) ? farh : stk; ++sp; }
+            if (lf ? vl : vr) { stk = (lane == sp) ? nearh : stk; ++sp; }
         }
-        const int hl = 2 * h + 1, hr = 2 * h + 2;
-        const float ll = box_lb3(box_lo + 3 * hl, box_hi + 3 * hl, fx, fy, fz);
-        const float lr = box_lb3(box_lo + 3 * hr, box_hi + 3 * hr, fx, fy, fz);
-        // conservative: the f32 bound may exceed the true f64 distance by a few ulps
-        const bool vl = (nTop < Kw) || (double)ll * (1.0 - 1e-6) <= thr;
-        const bool vr = (nTop < Kw) || (double)lr * (1.0 - 1e-6) <= thr;
-        const int nearh = ll <= lr ? hl : hr, farh = ll <= lr ? hr : hl;
-        const bool vnear = ll <= lr ? vl : vr, vfar = ll <= lr ? vr : vl;
-        if (lane == 0) {
-            if (vfar) stk[sp] = farh;
-            if (vnear) stk[sp + (vfar ? 1 : 0)] = nearh;
-        }
-        sp += (vfar ? 1 : 0) + (vnear ? 1 : 0);
     }
     if (nStg > 0) merge();
-    int* out = v.knn + (size_t)g * v.kmax;
-    for (int j = lane; j < K; j += 64) out[j] = j < nTop ? bi[j] : -1;
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {  // work counters (bench diagnostics)
+        unsigned long long* ctr = v.stats + 4 * (w & 63);
+        atomicAdd(ctr + 0, 1ull);
+        atomicAdd(ctr + 1, (unsigned long long)n_leaves);
+        atomicAdd(ctr + 2, (unsigned long long)n_merges);
+    }
+
+    if (write_knn) {
+        int* out = v.knn + (size_t)gp * v.kmax;
+        for (int j = lane; j < K; j += 64) out[j] = j < nTop ? bi[j] : -1;
+    }
+
+    // ---------------------------------------------------------------- TOLDI frame
+    if (st.k_lrf > 0 && !(dbg_skip & 1)) {
+        const int kk = min(st.k_lrf, nTop);
+        const int rz = kk / 3;
+        // neighbour ranks lane+1 and lane+65 (k <= 128) in registers
+        double ax[2], ay[2], az[2];
+        int rk[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            rk[u] = 1 + lane + 64 * u;
+            ax[u] = ay[u] = az[u] = 0.0;
+            if (rk[u] < kk) {
+                const int j = bi[rk[u]];
+                ax[u] = X[j]; ay[u] = Y[j]; az[u] = Z[j];
+            }
+        }
+        const int far = bi[kk - 1];
+        const double fdx = qx - X[far], fdy = qy - Y[far], fdz = qz - Z[far];
+        const double computed_radius = sqrt(fdx * fdx + fdy * fdy + fdz * fdz);  // ISR.cpp:256
+        // ISR.cpp:259-265 centroid quirk: ranks 1 .. rz-1 divided by rz
+        double sx = 0, sy = 0, sz = 0;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            if (rk[u] < rz) { sx += ax[u]; sy += ay[u]; sz += az[u]; }
+        const double cx = wsum(sx) / (double)rz, cy = wsum(sy) / (double)rz, cz = wsum(sz) / (double)rz;
+        // ISR.cpp:268-272 covariance over ranks 1 .. rz
+        double c00 = 0, c01 = 0, c02 = 0, c11 = 0, c12 = 0, c22 = 0;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            if (rk[u] <= rz && rk[u] < kk) {
+                const double ex = ax[u] - cx, ey = ay[u] - cy, ez = az[u] - cz;
+                c00 += ex * ex; c01 += ex * ey; c02 += ex * ez;
+                c11 += ey * ey; c12 += ey * ez; c22 += ez * ez;
+            }
+        c00 = wsum(c00); c01 = wsum(c01); c02 = wsum(c02);
+        c11 = wsum(c11); c12 = wsum(c12); c22 = wsum(c22);
+        d3 nrm = jacobi_smallest_evec(c00, c01, c02, c11, c12, c22);  // ISR.cpp:275-281
+        // ISR.cpp:286-297 over ranks 1 .. kk-1
+        double a0 = 0, a1 = 0, a2 = 0, s0 = 0, s1 = 0, s2 = 0;
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+            if (rk[u] < kk) {
+                const double vx = ax[u] - qx, vy = ay[u] - qy, vz = az[u] - qz;
+                a0 += vx; a1 += vy; a2 += vz;
+                const double an = nrm.x * vx + nrm.y * vy + nrm.z * vz;
+                const double r = computed_radius - sqrt(vx * vx + vy * vy + vz * vz);
+                const double wgt = (r * r) * (an * an);
+                s0 += wgt * vx; s1 += wgt * vy; s2 += wgt * vz;
+            }
+        a0 = wsum(a0); a1 = wsum(a1); a2 = wsum(a2);
+        s0 = wsum(s0); s1 = wsum(s1); s2 = wsum(s2);
+        if (nrm.x * a0 + nrm.y * a1 + nrm.z * a2 < 0.0) nrm = d3{-nrm.x, -nrm.y, -nrm.z};  // ISR.cpp:298
+        const d3 zax = nrm;
+        const d3 accs{s0, s1, s2};
+        d3 xax = accs - dot3(accs, zax) * zax;  // ISR.cpp:302-303 (no |x| = 0 guard, as the reference)
+        xax = (1.0 / sqrt(dot3(xax, xax))) * xax;
+        const d3 yax = cross3(zax, xax);  // ISR.cpp:306
+        if (lane < 12) {
+            const double al = st.alpha, be = st.beta;
+            const double f12[12] = {al * xax.x, al * xax.y, al * xax.z, al * yax.x, al * yax.y, al * yax.z,
+                                    al * zax.x, al * zax.y, al * zax.z, be * qx, be * qy, be * qz};
+            double fv = f12[0];
+#pragma unroll
+            for (int r = 1; r < 12; ++r) fv = (lane == r) ? f12[r] : fv;
+            v.fr64[(size_t)lane * v.ld + gp] = fv;
+            // f32 copy: 12-D search vectors of targets (cf: translation rows = points,
+            // ISR.cpp:834-836) and the kd-tree grouping of sources
+            double f32v = fv;
+            if (st.cf_target && lane >= 9) f32v = lane == 9 ? qx : (lane == 10 ? qy : qz);
+            v.fr32[(size_t)lane * v.ld + gp] = (float)f32v;
+        }
+    }
+
+    // ---------------------------------------------------------------- normals (+ GICP covariance)
+    if (st.k_nrm > 0 && !(dbg_skip & 2)) {
+        const int kn = min(st.k_nrm, nTop);
+        double cu[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        for (int r = lane; r < kn; r += 64) {  // ranks 0 .. kn-1, self included
+            const int j = bi[r];
+            const double x = X[j], y = Y[j], z = Z[j];
+            cu[0] += x; cu[1] += y; cu[2] += z;
+            cu[3] += x * x; cu[4] += x * y; cu[5] += x * z;
+            cu[6] += y * y; cu[7] += y * z; cu[8] += z * z;
+        }
+#pragma unroll
+        for (int i = 0; i < 9; ++i) cu[i] = wsum(cu[i]) / (double)kn;
+        double c00 = 1, c01 = 0, c02 = 0, c11 = 1, c12 = 0, c22 = 1;
+        if (kn >= 3) {
+            c00 = cu[3] - cu[0] * cu[0];
+            c11 = cu[6] - cu[1] * cu[1];
+            c22 = cu[8] - cu[2] * cu[2];
+            c01 = cu[4] - cu[0] * cu[1];
+            c02 = cu[5] - cu[0] * cu[2];
+            c12 = cu[7] - cu[1] * cu[2];
+        }
+        d3 nm = fast_eigen3x3(c00, c01, c02, c11, c12, c22);
+        if (sqrt(dot3(nm, nm)) == 0.0) nm = d3{0, 0, 1};
+        if (lane == 0) {
+            v.nrm64[gp] = nm.x;
+            v.nrm64[v.ld + gp] = nm.y;
+            v.nrm64[2 * (size_t)v.ld + gp] = nm.z;
+            if (st.want_cov) {
+                double cv[6];
+                gicp_cov_from_normal(nm, 1e-3, cv);
+#pragma unroll
+                for (int r = 0; r < 6; ++r) v.cov64[(size_t)r * v.ld + gp] = cv[r];
+            }
+        }
+    }
 }
 
 }  // namespace
 
-void launch_knn(const View& v, hipStream_t s) {
-    hipLaunchKernelGGL(k_knn_tree, dim3((v.npts + kWaves - 1) / kWaves), dim3(64 * kWaves), 0, s, v);
+void launch_lrf(const View& v, int write_knn, hipStream_t s) {
+    static const int wpe = [] {
+        const char* e = getenv("SE3ICP_LRF_WPE");
+        return e ? atoi(e) : 0;
+    }();
+    static const int dbg = [] {  // timing experiments only: skip the TOLDI (1) / normals (2) epilogue
+        const char* e = getenv("SE3ICP_LRF_DEBUG_SKIP");
+        return e ? atoi(e) : 0;
+    }();
+    const dim3 g((v.npts + kWaves - 1) / kWaves), b(64 * kWaves);
+    if (wpe == 8) hipLaunchKernelGGL(k_lrf<8>, g, b, 0, s, v, write_knn, dbg);
+    else if (wpe == 6) hipLaunchKernelGGL(k_lrf<6>, g, b, 0, s, v, write_knn, dbg);
+    else hipLaunchKernelGGL(k_lrf<1>, g, b, 0, s, v, write_knn, dbg);
 }
 
 }  // namespace se3icp

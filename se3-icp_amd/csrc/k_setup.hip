@@ -146,109 +146,6 @@ __global__ __launch_bounds__(256) void k_normalize(View v, const ChunkWork* chun
     }
 }
 
-// ------------------------------------------------------------------ frames
-__device__ __forceinline__ void atomic_max_nonneg(uint32_t* p, float x) {
-    atomicMax(p, __float_as_uint(x));
-}
-
-__global__ __launch_bounds__(256) void k_frames(View v) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= v.npts) return;
-    const int c = v.cloud_of[g];
-    const CloudSetup st = v.setup[c];
-    if (st.k_lrf == 0 && st.k_nrm == 0) return;
-    const CloudDev cl = v.clouds[c];
-    const int* nb = v.knn + (size_t)g * v.kmax;
-    const double* X = v.xyz64 + cl.off;
-    const double* Y = v.xyz64 + v.ld + cl.off;
-    const double* Z = v.xyz64 + 2 * (size_t)v.ld + cl.off;
-    const d3 p{v.xyz64[g], v.xyz64[v.ld + g], v.xyz64[2 * v.ld + g]};
-    if (st.k_lrf > 0) {
-        // computeSingleTOLDISE3Frame, ISR.cpp:241-316
-        const int kk = min(st.k_lrf, cl.n);
-        const int far = nb[kk - 1];
-        const double computed_radius = sqrt(dot3(p - mk3(X[far], Y[far], Z[far]), p - mk3(X[far], Y[far], Z[far])));
-        const int rz = kk / 3;
-        d3 cen{0, 0, 0};
-        for (int i = 1; i < rz; ++i) { const int j = nb[i]; cen = cen + mk3(X[j], Y[j], Z[j]); }
-        cen = d3{cen.x / (double)rz, cen.y / (double)rz, cen.z / (double)rz};
-        double c00 = 0, c01 = 0, c02 = 0, c11 = 0, c12 = 0, c22 = 0;
-        for (int i = 1; i < rz + 1; ++i) {
-            const int j = nb[i];
-            const d3 q = mk3(X[j], Y[j], Z[j]) - cen;
-            c00 += q.x * q.x; c01 += q.x * q.y; c02 += q.x * q.z;
-            c11 += q.y * q.y; c12 += q.y * q.z; c22 += q.z * q.z;
-        }
-        d3 n = jacobi_smallest_evec(c00, c01, c02, c11, c12, c22);
-        d3 acc{0, 0, 0}, accs{0, 0, 0};
-        for (int i = 1; i < kk; ++i) {
-            const int j = nb[i];
-            const d3 a = mk3(X[j], Y[j], Z[j]) - p;
-            acc = acc + a;
-            const double an = dot3(n, a);
-            const double r = computed_radius - sqrt(dot3(a, a));
-            accs = accs + ((r * r) * (an * an)) * a;
-        }
-        if (dot3(n, acc) < 0.0) n = d3{-n.x, -n.y, -n.z};
-        const d3 zax = n;
-        d3 xax = accs - dot3(accs, zax) * zax;
-        xax = (1.0 / sqrt(dot3(xax, xax))) * xax;
-        const d3 yax = cross3(zax, xax);
-        const double al = st.alpha, be = st.beta;
-        double f[12] = {al * xax.x, al * xax.y, al * xax.z, al * yax.x, al * yax.y, al * yax.z,
-                        al * zax.x, al * zax.y, al * zax.z, be * p.x, be * p.y, be * p.z};
-#pragma unroll
-        for (int r = 0; r < 12; ++r) v.fr64[(size_t)r * v.ld + g] = f[r];
-        // f32 copy: the 12-D search vectors of targets, the kd-tree grouping of sources
-        if (st.cf_target) { f[9] = p.x; f[10] = p.y; f[11] = p.z; }
-        double n2 = 0;
-#pragma unroll
-        for (int r = 0; r < 12; ++r) {
-            v.fr32[(size_t)r * v.ld + g] = (float)f[r];
-            n2 += f[r] * f[r];
-        }
-        if (st.is_target) atomic_max_nonneg(&v.norm12_bits[c], (float)(sqrt(n2) * (1.0 + 1e-6)));
-    }
-    if (st.k_nrm > 0) {
-        // EstimatePerPointCovariances -> ComputeCovariance (cumulants, incl. self) -> FastEigen3x3
-        const int kn = min(st.k_nrm, cl.n);
-        double c00 = 1, c01 = 0, c02 = 0, c11 = 1, c12 = 0, c22 = 1;
-        if (kn >= 3) {
-            double cu[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-            for (int i = 0; i < kn; ++i) {
-                const int j = nb[i];
-                const double x = X[j], y = Y[j], z = Z[j];
-                cu[0] += x; cu[1] += y; cu[2] += z;
-                cu[3] += x * x; cu[4] += x * y; cu[5] += x * z;
-                cu[6] += y * y; cu[7] += y * z; cu[8] += z * z;
-            }
-#pragma unroll
-            for (int i = 0; i < 9; ++i) cu[i] /= (double)kn;
-            c00 = cu[3] - cu[0] * cu[0];
-            c11 = cu[6] - cu[1] * cu[1];
-            c22 = cu[8] - cu[2] * cu[2];
-            c01 = cu[4] - cu[0] * cu[1];
-            c02 = cu[5] - cu[0] * cu[2];
-            c12 = cu[7] - cu[1] * cu[2];
-        }
-        d3 n = fast_eigen3x3(c00, c01, c02, c11, c12, c22);
-        if (sqrt(dot3(n, n)) == 0.0) n = d3{0, 0, 1};
-        v.nrm64[g] = n.x;
-        v.nrm64[v.ld + g] = n.y;
-        v.nrm64[2 * (size_t)v.ld + g] = n.z;
-        if (st.want_cov) {
-            double cv[6];
-            gicp_cov_from_normal(n, 1e-3, cv);
-#pragma unroll
-            for (int r = 0; r < 6; ++r) v.cov64[(size_t)r * v.ld + g] = cv[r];
-        }
-    }
-    if (st.is_target) {
-        const double fx = p.x - st.f32_center[0], fy = p.y - st.f32_center[1], fz = p.z - st.f32_center[2];
-        atomic_max_nonneg(&v.norm3_bits[c], (float)(sqrt(fx * fx + fy * fy + fz * fz) * (1.0 + 1e-6)));
-    }
-}
-
 }  // namespace
 
 // ------------------------------------------------------------------ launchers
@@ -261,9 +158,6 @@ void launch_radius(const View& v, const ChunkWork* chunks, int nchunks, const do
 }
 void launch_normalize(const View& v, const ChunkWork* chunks, int nchunks, double* partial, hipStream_t s) {
     if (nchunks > 0) hipLaunchKernelGGL(k_normalize, dim3(nchunks), dim3(256), 0, s, v, chunks, partial);
-}
-void launch_frames(const View& v, hipStream_t s) {
-    hipLaunchKernelGGL(k_frames, dim3((v.npts + 255) / 256), dim3(256), 0, s, v);
 }
 
 }  // namespace se3icp

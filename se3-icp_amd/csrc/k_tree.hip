@@ -119,6 +119,8 @@ __global__ __launch_bounds__(256) void k_tree_finish(TreeView t) {
         const int p = t.perm[g];
         t.pos[cl.off + p] = g - cl.off;
         for (int d = 0; d < t.D; ++d) t.tvec[(size_t)d * t.ld + g] = t.vec[(size_t)d * t.ld + cl.off + p];
+        if (t.tvec64)
+            for (int d = 0; d < t.D; ++d) t.tvec64[(size_t)d * t.ld + g] = t.vec64[(size_t)d * t.ld + cl.off + p];
     }
     // f32 boxes, inflated so that they bound the underlying f64 values
     const size_t nb = (size_t)t.nclouds * t.nnodes * t.D;

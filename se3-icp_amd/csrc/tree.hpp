@@ -27,6 +27,8 @@ struct TreeView {
     int32_t* perm;     // [ld] tree position (global slot) -> local point index
     int32_t* pos;      // [ld] point (global slot) -> local tree position
     float* tvec;       // [D][ld] vectors in tree order
+    const double* vec64;  // optional [D][ld] f64 vectors (original order) ...
+    double* tvec64;       // ... copied into tree order (3-D trees: coalesced leaf loads)
     uint32_t* blo;     // [nclouds][nnodes][D] build scratch (orderable bits)
     uint32_t* bhi;
     float* lo;         // [nclouds][nnodes][D] node boxes

@@ -31,6 +31,7 @@ struct TreeRef {
     const int32_t* perm;  // [ld] tree position (cloud.off + x) -> local point index
     const int32_t* pos;   // [ld] point (cloud.off + i) -> local tree position
     const float* tvec;    // [D][ld] vectors in tree order
+    const double* tvec64; // [D][ld] f64 vectors in tree order (3-D trees only)
     const float* lo;      // [nclouds][nnodes][D]
     const float* hi;
 };
@@ -61,8 +62,6 @@ struct View {
     double* conf64;
     int32_t* knn;
     // per-cloud f32 error-bound norms (float bits, atomicMax)
-    uint32_t* norm12_bits;
-    uint32_t* norm3_bits;
     // loop
     int32_t* corr_idx;
     float* corr_dist;
@@ -91,8 +90,8 @@ void launch_radius(const View& v, const ChunkWork* chunks, int nchunks, const do
                    double* partial /*[nchunks]*/, hipStream_t s);
 void launch_normalize(const View& v, const ChunkWork* chunks, int nchunks, double* partial /*[nchunks*7]*/,
                       hipStream_t s);
-void launch_knn(const View& v, hipStream_t s);
-void launch_frames(const View& v, hipStream_t s);
+// fused kNN + TOLDI frame + normals/GICP covariance (k_knn.hip); knn list only if v.knn
+void launch_lrf(const View& v, int write_knn, hipStream_t s);
 
 // ---- k_loop.hip
 // exact 1-NN of every active pair's source points, one wavefront per source leaf,
