@@ -113,6 +113,7 @@ def main():
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     iters = 0
+    rechecked = 0
     loop_ms = 0.0
     ktot: dict = {}
     last = None
@@ -122,6 +123,7 @@ def main():
         for k, v in kt.items():
             ktot[k] = ktot.get(k, 0.0) + v
         iters += sum(r.num_iterations for r in res)
+        rechecked += sum(r.num_rechecked for r in res)
         loop_ms += res[0].time_loop_ms
         last = res
         log(f"rank {rank}: step {s} done ({sum(r.num_iterations for r in res)} iterations)")
@@ -198,6 +200,7 @@ def main():
             "accuracy_vs_gt": {"rot_deg_max": round(max(rot_errs), 4), "trans_m_max": round(max(tr_errs), 4)},
             "kernel_ms_per_step": {k: round(v / args.steps, 3) for k, v in kms.items()},
             "lrf_work": lrf_work,
+            "rechecked_queries_per_step": rechecked / args.steps,
             "roofline": {
                 "kernel": kname,
                 "bound": "mfma",

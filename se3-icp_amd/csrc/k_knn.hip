@@ -45,26 +45,29 @@ __device__ __forceinline__ double wsum(double x) {
     return x;
 }
 
-// ascending sort of the wave's 256 (d2, idx) keys: 4 keys per lane, bitonic network,
-// cross-lane stages through __shfl
-__device__ __forceinline__ void wave_bitonic256(double* bd, int* bi, int lane, int cnt) {
-    double kd[4];
-    int ki[4];
+// ascending sort of the wave's first 64*PER (d2, idx) keys (PER per lane, entry
+// lane*PER+s; entries >= cnt are padding): register bitonic network, cross-lane stages
+// through __shfl
+template <int PER>
+__device__ __forceinline__ void wave_bitonic(double* bd, int* bi, int lane, int cnt) {
+    constexpr int N = 64 * PER;
+    double kd[PER];
+    int ki[PER];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        const int e = lane * 4 + s;
+    for (int s = 0; s < PER; ++s) {
+        const int e = lane * PER + s;
         kd[s] = e < cnt ? bd[e] : DBL_MAX;
         ki[s] = e < cnt ? bi[e] : INT_MAX;
     }
 #pragma unroll
-    for (int k = 2; k <= 256; k <<= 1) {
+    for (int k = 2; k <= N; k <<= 1) {
 #pragma unroll
         for (int jd = k >> 1; jd > 0; jd >>= 1) {
-            if (jd >= 4) {
-                const int pl = lane ^ (jd >> 2);
+            if (jd >= PER) {
+                const int pl = lane ^ (jd / PER);
 #pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    const int e = lane * 4 + s;
+                for (int s = 0; s < PER; ++s) {
+                    const int e = lane * PER + s;
                     const double pd = __shfl(kd[s], pl, 64);
                     const int pi = __shfl(ki[s], pl, 64);
                     const bool up = (e & k) == 0;
@@ -75,10 +78,10 @@ __device__ __forceinline__ void wave_bitonic256(double* bd, int* bi, int lane, i
                 }
             } else {
 #pragma unroll
-                for (int s = 0; s < 4; ++s) {
+                for (int s = 0; s < PER; ++s) {
                     if ((s & jd) == 0) {
                         const int t = s | jd;
-                        const bool up = ((lane * 4 + s) & k) == 0;
+                        const bool up = ((lane * PER + s) & k) == 0;
                         const bool sw = up ? key_less(kd[t], ki[t], kd[s], ki[s]) : key_less(kd[s], ki[s], kd[t], ki[t]);
                         const double ds = kd[s], dt = kd[t];
                         const int is = ki[s], it = ki[t];
@@ -90,10 +93,17 @@ __device__ __forceinline__ void wave_bitonic256(double* bd, int* bi, int lane, i
         }
     }
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        bd[lane * 4 + s] = kd[s];
-        bi[lane * 4 + s] = ki[s];
+    for (int s = 0; s < PER; ++s) {
+        bd[lane * PER + s] = kd[s];
+        bi[lane * PER + s] = ki[s];
     }
+}
+
+// bits of the f32 value >= d (d >= 0): the f32 keys preserve <= of the f64 distances
+__device__ __forceinline__ unsigned f32_up_bits(double d) {
+    float f = (float)d;
+    if ((double)f < d) f = __uint_as_float(__float_as_uint(f) + 1u);
+    return __float_as_uint(f);
 }
 
 // squared distance from q to a 3-D box (f32; the boxes are inflated to bound the f64 points)
@@ -138,17 +148,63 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     const int own = first_leaf + tree_node_of(w - cl.off, n, T.L);
 
     // ---------------------------------------------------------------- kNN
-    int nTop = 0, nStg = 0, n_leaves = 0, n_merges = 0;
+    // Candidates accepted by the current bound are appended, unsorted, to the wave's
+    // buffer.  Once Kw candidates exist (and whenever the buffer is full) the bound is
+    // tightened to the Kw-th smallest f32-rounded-up distance, found by bisection over
+    // the f32 bit patterns with ballot counts, and the buffer is compacted; only the
+    // survivors are sorted exactly, once, at the end.  The bound is an upper bound of the
+    // true Kw-th distance, so no member of the exact top-Kw is ever dropped.
+    int nb = 0, n_leaves = 0, n_sel = 0;
+    bool have_thr = false;
     double thr = DBL_MAX;
-    int thr_i = INT_MAX;
-    auto merge = [&]() __attribute__((always_inline)) {
+    int thr_i = INT_MAX;  // < INT_MAX only after an exact truncation (ties at thr resolved by index)
+    auto select_thr = [&]() __attribute__((always_inline)) {
         __builtin_amdgcn_wave_barrier();
-        wave_bitonic256(bd, bi, lane, nTop + nStg);
+        ++n_sel;
+        double dk[4];
+        int ik[4];
+        unsigned u[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int e = s * 64 + lane;
+            dk[s] = e < nb ? bd[e] : DBL_MAX;
+            ik[s] = e < nb ? bi[e] : INT_MAX;
+            u[s] = e < nb ? f32_up_bits(dk[s]) : 0xffffffffu;
+        }
+        unsigned lo = 0, hi = 0x7f800000u;  // count(u <= hi) = nb >= Kw
+        while (lo < hi) {
+            const unsigned mid = lo + ((hi - lo) >> 1);
+            int cnt = 0;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) cnt += __popcll(__ballot(u[s] <= mid));
+            if (cnt >= Kw) hi = mid; else lo = mid + 1;
+        }
+        const double t = (double)__uint_as_float(lo);
+        if (t < thr) { thr = t; thr_i = INT_MAX; }
         __builtin_amdgcn_wave_barrier();
-        nTop = min(Kw, nTop + nStg);
-        nStg = 0;
-        ++n_merges;
-        if (nTop == Kw) { thr = bd[Kw - 1]; thr_i = bi[Kw - 1]; }
+        int base = 0;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const bool keep = dk[s] < thr || (dk[s] == thr && ik[s] <= thr_i);
+            const unsigned long long m = __ballot(keep);
+            if (keep) {
+                const int at = base + __popcll(m & ((1ull << lane) - 1ull));
+                bd[at] = dk[s];
+                bi[at] = ik[s];
+            }
+            base += __popcll(m);
+        }
+        nb = base;
+        have_thr = true;
+        if (nb > kBuf - kLeafMax) {  // massive ties at the bound: exact sort and truncation
+            __builtin_amdgcn_wave_barrier();
+            wave_bitonic<4>(bd, bi, lane, nb);
+            __builtin_amdgcn_wave_barrier();
+            nb = Kw;
+            thr = bd[Kw - 1];
+            thr_i = bi[Kw - 1];
+        }
+        __builtin_amdgcn_wave_barrier();
     };
     auto leaf = [&](int h) __attribute__((always_inline)) {
         const int i = h - first_leaf;
@@ -161,28 +217,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             const int slot = cl.off + a + lane;
             li = T.perm[slot];
             d = l2_3(qx, qy, qz, TX[slot], TY[slot], TZ[slot]);
-            acc = (nTop < Kw) || key_less(d, li, thr, thr_i);
+            acc = !have_thr || d < thr || (d == thr && li <= thr_i);
         }
         const unsigned long long m = __ballot(acc);
         if (acc) {
-            const int at = nTop + nStg + __popcll(m & ((1ull << lane) - 1ull));
+            const int at = nb + __popcll(m & ((1ull << lane) - 1ull));
             bd[at] = d;
             bi[at] = li;
         }
-        nStg += __popcll(m);
-        // establish the k-th distance as soon as k candidates exist, then merge when full
-        if ((nTop < Kw && nTop + nStg >= Kw) || nTop + nStg > kBuf - kLeafMax) merge();
+        nb += __popcll(m);
+        if ((!have_thr && nb >= Kw) || nb > kBuf - kLeafMax) select_thr();
     };
-    auto open = [&](int h) __attribute__((always_inline)) {  // may the subtree at h hold a better candidate?
-        if (nTop < Kw) return true;
-        const float lb = box_lb3(box_lo + 3 * h, box_hi + 3 * h, fx, fy, fz);
-        return (double)lb * (1.0 - 1e-6) <= thr;
+    auto open = [&](float lb) __attribute__((always_inline)) {  // may a box at lb hold a candidate?
+        return !have_thr || (double)lb * (1.0 - 1e-6) <= thr;
     };
 
     leaf(own);
     for (int node = own; node > 0; node = (node - 1) >> 1) {
         const int sib = (node & 1) ? node + 1 : node - 1;
-        if (!open(sib)) continue;
+        if (!open(box_lb3(box_lo + 3 * sib, box_hi + 3 * sib, fx, fy, fz))) continue;
         int stk = 0, sp = 0;  // stack in a VGPR: lane i holds entry i
         stk = (lane == sp) ? sib : stk;
         ++sp;
@@ -196,21 +249,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
             const int hl = 2 * h + 1, hr = 2 * h + 2;
             const float ll = box_lb3(box_lo + 3 * hl, box_hi + 3 * hl, fx, fy, fz);
             const float lr = box_lb3(box_lo + 3 * hr, box_hi + 3 * hr, fx, fy, fz);
-            const bool vl = (nTop < Kw) || (double)ll * (1.0 - 1e-6) <= thr;
-            const bool vr = (nTop < Kw) || (double)lr * (1.0 - 1e-6) <= thr;
+            const bool vl = open(ll), vr = open(lr);
             const bool lf = ll <= lr;
             const int nearh = lf ? hl : hr, farh = lf ? hr : hl;
             if (lf ? vr : vl) { stk = (lane == sp) ? farh : stk; ++sp; }
             if (lf ? vl : vr) { stk = (lane == sp) ? nearh : stk; ++sp; }
         }
     }
-    if (nStg > 0) merge();
+    // exact order of the survivors
+    if (have_thr && nb > 128) select_thr();
     __builtin_amdgcn_wave_barrier();
+    if (nb <= 128) wave_bitonic<2>(bd, bi, lane, nb);
+    else wave_bitonic<4>(bd, bi, lane, nb);
+    __builtin_amdgcn_wave_barrier();
+    const int nTop = min(Kw, nb);
     if (lane == 0) {  // work counters (bench diagnostics)
         unsigned long long* ctr = v.stats + 4 * (w & 63);
         atomicAdd(ctr + 0, 1ull);
         atomicAdd(ctr + 1, (unsigned long long)n_leaves);
-        atomicAdd(ctr + 2, (unsigned long long)n_merges);
+        atomicAdd(ctr + 2, (unsigned long long)n_sel);
     }
 
     if (write_knn) {

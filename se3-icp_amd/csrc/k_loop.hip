@@ -17,6 +17,7 @@
 #include <cmath>
 
 #include "loopdev.hpp"
+#include "tree.hpp"
 
 namespace se3icp {
 
@@ -25,55 +26,92 @@ namespace {
 using namespace loopdev;
 
 // ------------------------------------------------------------------ recheck (exact f64)
-__global__ __launch_bounds__(256) void k_recheck(View v) {
-    __shared__ double s_d[4];
-    __shared__ int s_i[4];
-    const int cnt = *v.flag_count;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int f = blockIdx.x; f < cnt; f += gridDim.x) {
-        const int g = v.flag_list[f];
-        const int pair = v.cloud_of[g] >> 1;
-        const PairDev* P = v.pairs + pair;
-        const int phase = P->phase;
-        const CloudDev ct = v.clouds[P->tgt];
-        const bool cf = P->cf != 0;
-        double T[12], Q[12];
-        load_T(P, T);
-        double bd = DBL_MAX;
-        int bi = INT_MAX;
-        if (phase == PHASE_SE3) {
-            query_f64<12>(v, T, g, Q);
-            for (int j = threadIdx.x; j < ct.n; j += blockDim.x) {
-                double b[12];
-                target12(v, ct, cf, j, b);
-                const double d = l2_nanoflann12(Q, b);
-                if (key_less(d, j, bd, bi)) { bd = d; bi = j; }
-            }
-        } else {
-            query_f64<3>(v, T, g, Q);
-            for (int j = threadIdx.x; j < ct.n; j += blockDim.x) {
-                const int gt = ct.off + j;
-                const double b[3] = {v.xyz64[gt], v.xyz64[v.ld + gt], v.xyz64[2 * (size_t)v.ld + gt]};
-                const double d = l2_nanoflann3(Q, b);
-                if (key_less(d, j, bd, bi)) { bd = d; bi = j; }
-            }
-        }
+// One wavefront per flagged query: exact f64 1-NN over the target kd-tree of the phase.
+// The f32 node boxes were inflated to bound the f64 vectors (k_tree.hip), so a box
+// lower bound computed in f64 against the f64 query prunes exactly; boxes whose bound
+// equals the best distance are still opened (a lower index may tie).  Seeded with the
+// f32 winner that k_nn_group stored in corr_idx.
+template <int D>
+__device__ __forceinline__ void recheck_one(const View& v, const PairDev* P, const CloudDev& ct, int g, int lane) {
+    const bool cf = P->cf != 0;
+    const TreeRef TR = (D == 12) ? v.t12 : v.t3;
+    double T[12], Q[D], qs[D];
+    load_T(P, T);
+    query_f64<D>(v, T, g, Q);
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            const double od = __shfl_xor(bd, o, 64);
-            const int oi = __shfl_xor(bi, o, 64);
-            if (key_less(od, oi, bd, bi)) { bd = od; bi = oi; }
+    for (int r = 0; r < D; ++r) qs[r] = (D == 3) ? Q[r] - P->f32_center[r] : Q[r];
+    auto dist = [&](int j) __attribute__((always_inline)) {
+        if constexpr (D == 12) {
+            double b[12];
+            target12(v, ct, cf, j, b);
+            return l2_nanoflann12(Q, b);
+        } else {
+            const int gt = ct.off + j;
+            const double b[3] = {v.xyz64[gt], v.xyz64[v.ld + gt], v.xyz64[2 * (size_t)v.ld + gt]};
+            return l2_nanoflann3(Q, b);
         }
-        if (lane == 0) { s_d[wid] = bd; s_i[wid] = bi; }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            for (int k = 1; k < 4; ++k)
-                if (key_less(s_d[k], s_i[k], bd, bi)) { bd = s_d[k]; bi = s_i[k]; }
-            if (bi == INT_MAX) bi = 0;
-            v.corr_idx[g] = bi;
-            v.corr_dist[g] = stored_dist(v, phase, ct, Q, bi);
+    };
+    const float* box_lo = TR.lo + (size_t)P->tgt * TR.nnodes * D;
+    const float* box_hi = TR.hi + (size_t)P->tgt * TR.nnodes * D;
+    auto lbound = [&](int h) __attribute__((always_inline)) {
+        double s = 0.0;
+#pragma unroll
+        for (int r = 0; r < D; ++r) {
+            const double e = fmax(fmax((double)box_lo[h * D + r] - qs[r], qs[r] - (double)box_hi[h * D + r]), 0.0);
+            s += e * e;
         }
-        __syncthreads();
+        return s * (1.0 - 1e-12);
+    };
+    int bi = v.corr_idx[g];
+    if (bi < 0 || bi >= ct.n) bi = 0;
+    double bd = dist(bi);
+    const int first_leaf = (1 << TR.L) - 1;
+    int stk = 0, sp = 1;  // register stack: lane i holds entry i
+    while (sp > 0) {
+        const int h = __builtin_amdgcn_readlane(stk, sp - 1);
+        --sp;
+        if (h >= first_leaf) {
+            const int li = h - first_leaf;
+            const int ta = tree_first(ct.n, TR.L, li), tb = tree_first(ct.n, TR.L, li + 1);
+            double d = DBL_MAX;
+            int j = INT_MAX;
+            if (lane < tb - ta) {
+                j = TR.perm[ct.off + ta + lane];
+                d = dist(j);
+            }
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {
+                const double od = __shfl_xor(d, o, 64);
+                const int oj = __shfl_xor(j, o, 64);
+                if (key_less(od, oj, d, j)) { d = od; j = oj; }
+            }
+            if (key_less(d, j, bd, bi)) { bd = d; bi = j; }
+            continue;
+        }
+        const int hl = 2 * h + 1, hr = 2 * h + 2;
+        const double ll = lbound(hl), lr = lbound(hr);
+        const bool vl = ll <= bd, vr = lr <= bd;
+        const bool lf = ll <= lr;
+        const int nearh = lf ? hl : hr, farh = lf ? hr : hl;
+        if (lf ? vr : vl) { stk = (lane == sp) ? farh : stk; ++sp; }
+        if (lf ? vl : vr) { stk = (lane == sp) ? nearh : stk; ++sp; }
+    }
+    if (lane == 0) {
+        v.corr_idx[g] = bi;
+        v.corr_dist[g] = stored_dist(v, P->phase, ct, Q, bi);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_recheck(View v) {
+    const int cnt = *v.flag_count;
+    const int lane = threadIdx.x & 63;
+    const int w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    for (int f = w0; f < cnt; f += gridDim.x * 4) {
+        const int g = v.flag_list[f];
+        const PairDev* P = v.pairs + (v.cloud_of[g] >> 1);
+        const CloudDev ct = v.clouds[P->tgt];
+        if (P->phase == PHASE_SE3) recheck_one<12>(v, P, ct, g, lane);
+        else if (P->phase == PHASE_R3) recheck_one<3>(v, P, ct, g, lane);
     }
 }
 
@@ -82,13 +120,63 @@ __device__ __forceinline__ unsigned long long trim_key_of(const float* dist, int
     return ((unsigned long long)__float_as_uint(dist[base + i]) << 32) | (unsigned)i;
 }
 
-// One 1024-thread block per trimming pair: MSB radix select (8-bit digits) of the
-// nkeep-th smallest key.  High digits are counted with wave-aggregated atomics
-// (distances of neighbouring queries share their exponent byte).
+// One wave finds the bin holding the k-th smallest element (k >= 1) of a histogram of
+// 64*PER bins (lane l owns bins l*PER .. l*PER+PER-1); returns the bin and the count
+// of elements in the bins before it.
+template <int PER>
+__device__ __forceinline__ void wave_find_bin(const unsigned* hist, unsigned k, int lane, int* bin,
+                                              unsigned* before) {
+    unsigned h[PER];
+    unsigned t = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) { h[j] = hist[lane * PER + j]; t += h[j]; }
+    unsigned incl = t;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    const unsigned long long m = __ballot(incl >= k);
+    const int owner = m ? __ffsll((long long)m) - 1 : 63;
+    if (lane == owner) {
+        unsigned cum = incl - t;
+        int b = lane * PER + PER - 1;
+#pragma unroll
+        for (int j = 0; j < PER; ++j) {
+            if (cum + h[j] >= k) { b = lane * PER + j; break; }
+            cum += h[j];
+        }
+        *bin = b;
+        *before = cum;
+    }
+}
+
+// wave-aggregated LDS histogram increment: lanes with equal digits add once
+__device__ __forceinline__ void hist_add_aggregated(unsigned* hist, bool act, unsigned dig, int lane) {
+    unsigned long long am = __ballot(act);
+    while (am) {
+        const int leader = __ffsll((long long)am) - 1;
+        const unsigned ld = __shfl(dig, leader, 64);
+        const unsigned long long same = __ballot(act && dig == ld);
+        if (lane == leader) atomicAdd(&hist[ld], (unsigned)__popcll(same));
+        if (dig == ld) act = false;
+        am &= ~same;
+    }
+}
+
+constexpr int kTrimList = 4096;
+
+// One 1024-thread block per trimming pair: the nkeep-th smallest 64-bit key
+// (float distance bits << 32 | query index) by MSB radix select.  The first digit
+// is the top 12 bits; further 8-bit digits are counted over all keys (global re-reads)
+// until the selected bin holds at most kTrimList keys, which are then compacted into
+// LDS where the remaining digits are resolved.
 __global__ __launch_bounds__(1024) void k_trim(View v) {
-    __shared__ unsigned int hist[256];
-    __shared__ unsigned long long s_prefix, s_mask;
-    __shared__ int s_k;
+    __shared__ unsigned hist[4096];
+    __shared__ unsigned long long s_list[kTrimList];
+    __shared__ unsigned s_cnt;
+    __shared__ int s_bin;
+    __shared__ unsigned s_before;
     const PairDev* P = v.pairs + blockIdx.x;
     if (P->phase == PHASE_IDLE || !P->trim) return;
     const CloudDev cs = v.clouds[P->src];
@@ -97,53 +185,85 @@ __global__ __launch_bounds__(1024) void k_trim(View v) {
         if (threadIdx.x == 0) v.trim_key[blockIdx.x] = 0ull;  // keep none (handled by reduce)
         return;
     }
-    if (threadIdx.x == 0) { s_prefix = 0; s_mask = 0; s_k = P->nkeep; }
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    for (int shift = 56; shift >= 0; shift -= 8) {
-        if (threadIdx.x < 256) hist[threadIdx.x] = 0;
-        __syncthreads();
-        const unsigned long long prefix = s_prefix, mask = s_mask;
-        const bool aggregate = shift >= 48;
-        for (int i0 = 0; i0 < n; i0 += blockDim.x) {
-            const int i = i0 + threadIdx.x;
-            bool act = false;
-            unsigned dig = 0;
-            if (i < n) {
-                const unsigned long long key = trim_key_of(v.corr_dist, cs.off, i);
-                act = (key & mask) == prefix;
-                dig = (unsigned)(key >> shift) & 255u;
-            }
-            if (aggregate) {
-                unsigned long long am = __ballot(act);
-                while (am) {
-                    const int leader = __ffsll((long long)am) - 1;
-                    const unsigned ld = __shfl(dig, leader, 64);
-                    const unsigned long long same = __ballot(act && dig == ld);
-                    if (lane == leader) atomicAdd(&hist[ld], (unsigned)__popcll(same));
-                    if (dig == ld) act = false;
-                    am &= ~same;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const unsigned* dist = reinterpret_cast<const unsigned*>(v.corr_dist) + cs.off;
+    constexpr int U = 8;  // independent loads in flight per thread
+    unsigned long long prefix = 0, mask = 0;
+    unsigned k = (unsigned)P->nkeep;  // rank (1-based) within the keys matching prefix/mask
+    unsigned sel_count = (unsigned)n;
+    int pos = 0;                      // key bits resolved (from the top)
+    bool in_lds = false;
+    unsigned cnt = 0;
+    while (pos < 64) {
+        const int w = pos == 0 ? 12 : min(8, 64 - pos);
+        const int sh = 64 - pos - w;
+        const unsigned dmask = (1u << w) - 1u;
+        if (!in_lds && sel_count <= (unsigned)kTrimList) {
+            // compact the keys matching the prefix into LDS
+            if (threadIdx.x == 0) s_cnt = 0;
+            __syncthreads();
+            for (int i0 = 0; i0 < n; i0 += U * blockDim.x) {
+                unsigned u[U];
+#pragma unroll
+                for (int j = 0; j < U; ++j) {
+                    const int i = i0 + j * blockDim.x + threadIdx.x;
+                    u[j] = i < n ? dist[i] : 0xffffffffu;
                 }
-            } else if (act) {
-                atomicAdd(&hist[dig], 1u);
+#pragma unroll
+                for (int j = 0; j < U; ++j) {
+                    const int i = i0 + j * blockDim.x + threadIdx.x;
+                    const unsigned long long key = ((unsigned long long)u[j] << 32) | (unsigned)i;
+                    const bool sel = i < n && (key & mask) == prefix;
+                    const unsigned long long m = __ballot(sel);
+                    if (m == 0) continue;
+                    unsigned base = 0;
+                    if (lane == 0) base = atomicAdd(&s_cnt, (unsigned)__popcll(m));
+                    base = __shfl(base, 0, 64);
+                    if (sel) s_list[base + (unsigned)__popcll(m & ((1ull << lane) - 1ull))] = key;
+                }
+            }
+            __syncthreads();
+            cnt = s_cnt;
+            in_lds = true;
+        }
+        for (int i = threadIdx.x; i <= (int)dmask; i += blockDim.x) hist[i] = 0;
+        __syncthreads();
+        if (in_lds) {
+            for (unsigned e = threadIdx.x; e < cnt; e += blockDim.x) {
+                const unsigned long long key = s_list[e];
+                if ((key & mask) == prefix) atomicAdd(&hist[(unsigned)(key >> sh) & dmask], 1u);
+            }
+        } else {
+            for (int i0 = 0; i0 < n; i0 += U * blockDim.x) {
+                unsigned u[U];
+#pragma unroll
+                for (int j = 0; j < U; ++j) {
+                    const int i = i0 + j * blockDim.x + threadIdx.x;
+                    u[j] = i < n ? dist[i] : 0xffffffffu;
+                }
+#pragma unroll
+                for (int j = 0; j < U; ++j) {
+                    const int i = i0 + j * blockDim.x + threadIdx.x;
+                    const unsigned long long key = ((unsigned long long)u[j] << 32) | (unsigned)i;
+                    if (i < n && (key & mask) == prefix) atomicAdd(&hist[(unsigned)(key >> sh) & dmask], 1u);
+                }
             }
         }
         __syncthreads();
-        if (threadIdx.x == 0) {
-            unsigned cum = 0;
-            int k = s_k;
-            int sel = 255;
-            for (int b = 0; b < 256; ++b) {
-                if (cum + hist[b] >= (unsigned)k) { sel = b; break; }
-                cum += hist[b];
-            }
-            s_k = k - (int)cum;
-            s_prefix = prefix | ((unsigned long long)sel << shift);
-            s_mask = mask | (255ull << shift);
+        if (wid == 0) {
+            if (w == 12) wave_find_bin<64>(hist, k, lane, &s_bin, &s_before);
+            else wave_find_bin<4>(hist, k, lane, &s_bin, &s_before);
         }
+        __syncthreads();
+        const unsigned bin = (unsigned)s_bin;
+        k -= s_before;
+        sel_count = hist[bin];
+        prefix |= (unsigned long long)bin << sh;
+        mask |= (unsigned long long)dmask << sh;
+        pos += w;
         __syncthreads();
     }
-    if (threadIdx.x == 0) v.trim_key[blockIdx.x] = s_prefix;
+    if (threadIdx.x == 0) v.trim_key[blockIdx.x] = prefix;
 }
 
 // ------------------------------------------------------------------ reduce
