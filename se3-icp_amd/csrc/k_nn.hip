@@ -25,7 +25,10 @@ namespace {
 using namespace loopdev;
 
 constexpr int kWaves = 4;
-constexpr int kStack = 64;
+
+// packed f32 pairs: v_pk_add_f32 / v_pk_fma_f32 issue two lanes' worth of f32 math per
+// instruction (the f32 vector peak of gfx950 assumes them)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 template <int D>
 __device__ __forceinline__ float box_lb(const float* lo, const float* hi, const float* q) {
@@ -42,9 +45,9 @@ template <int D>
 __global__ __launch_bounds__(256) void k_nn_group(View v) {
     constexpr int NV = (D + 3) / 4;
     __shared__ float4 s_tile[kWaves][kLeafMax * NV];
-    __shared__ int s_stack[kWaves][kStack];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const int gi = blockIdx.x * kWaves + wid;
+    // wave-uniform work item: the pair record, node boxes and leaf ranges become scalar loads
+    const int gi = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wid);
     if (gi >= v.ngwork) return;
     const GroupWork w = v.gwork[gi];
     const PairDev* P = v.pairs + w.pair;
@@ -74,6 +77,9 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
         na = (float)sqrt(n2) * 1.000001f;
     }
     const float nb = (D == 12) ? P->tgt_norm12 : P->tgt_norm3;
+    f32x2 q2[(D + 1) / 2];
+#pragma unroll
+    for (int r = 0; r < D / 2; ++r) q2[r] = f32x2{q[2 * r], q[2 * r + 1]};
     const float* tv = TR.tvec + ct.off;
     const size_t ld = v.ld;
 
@@ -98,13 +104,11 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
     const float* box_hi = TR.hi + (size_t)P->tgt * TR.nnodes * D;
     const int first_leaf = (1 << TR.L) - 1;
     float4* tile = s_tile[wid];
-    int* stk = s_stack[wid];
-    if (lane == 0) stk[0] = 0;
+    int stk = 0;  // DFS stack in a VGPR: lane i holds entry i (depth <= 2L+1 < 64)
     int sp = 1;
     unsigned n_eval = 0, n_box = 0;  // wave-uniform work counters (roofline accounting)
     while (sp > 0) {
-        __builtin_amdgcn_wave_barrier();
-        const int h = __builtin_amdgcn_readfirstlane(stk[sp - 1]);
+        const int h = __builtin_amdgcn_readlane(stk, sp - 1);
         --sp;
         if (h >= first_leaf) {
             const int li = h - first_leaf;
@@ -123,20 +127,17 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
             for (int j = 0; j < cnt; ++j) {
                 float acc;
                 if constexpr (D == 12) {
+                    // two interleaved FMA chains (even / odd dimensions) and one add: within
+                    // the D-term chain bound f32_err assumes
                     const float4 A = tile[j * 3], B = tile[j * 3 + 1], C = tile[j * 3 + 2];
-                    float e;
-                    e = q[0] - A.x; acc = e * e;
-                    e = q[1] - A.y; acc = fmaf(e, e, acc);
-                    e = q[2] - A.z; acc = fmaf(e, e, acc);
-                    e = q[3] - A.w; acc = fmaf(e, e, acc);
-                    e = q[4] - B.x; acc = fmaf(e, e, acc);
-                    e = q[5] - B.y; acc = fmaf(e, e, acc);
-                    e = q[6] - B.z; acc = fmaf(e, e, acc);
-                    e = q[7] - B.w; acc = fmaf(e, e, acc);
-                    e = q[8] - C.x; acc = fmaf(e, e, acc);
-                    e = q[9] - C.y; acc = fmaf(e, e, acc);
-                    e = q[10] - C.z; acc = fmaf(e, e, acc);
-                    e = q[11] - C.w; acc = fmaf(e, e, acc);
+                    f32x2 e, s2;
+                    e = q2[0] - f32x2{A.x, A.y}; s2 = e * e;
+                    e = q2[1] - f32x2{A.z, A.w}; s2 = __builtin_elementwise_fma(e, e, s2);
+                    e = q2[2] - f32x2{B.x, B.y}; s2 = __builtin_elementwise_fma(e, e, s2);
+                    e = q2[3] - f32x2{B.z, B.w}; s2 = __builtin_elementwise_fma(e, e, s2);
+                    e = q2[4] - f32x2{C.x, C.y}; s2 = __builtin_elementwise_fma(e, e, s2);
+                    e = q2[5] - f32x2{C.z, C.w}; s2 = __builtin_elementwise_fma(e, e, s2);
+                    acc = s2.x + s2.y;
                 } else {
                     const float4 A = tile[j];
                     float e;
@@ -163,12 +164,8 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
         const bool left_first = __builtin_amdgcn_readfirstlane(ll <= lr ? 1 : 0) != 0;
         const int nearh = left_first ? hl : hr, farh = left_first ? hr : hl;
         const bool vnear = left_first ? vl : vr, vfar = left_first ? vr : vl;
-        __builtin_amdgcn_wave_barrier();
-        if (lane == 0) {
-            if (vfar) stk[sp] = farh;
-            if (vnear) stk[sp + (vfar ? 1 : 0)] = nearh;
-        }
-        sp += (vfar ? 1 : 0) + (vnear ? 1 : 0);
+        if (vfar) { stk = (lane == sp) ? farh : stk; ++sp; }
+        if (vnear) { stk = (lane == sp) ? nearh : stk; ++sp; }
     }
 
     if (lane == 0) {  // 64 lanes per evaluation; 64 counter slots against contention

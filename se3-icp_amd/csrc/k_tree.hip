@@ -4,10 +4,12 @@
 // SE(3) NN, ISR.cpp:586-587, 626).  Here one implicit, balanced tree per cloud is built
 // level-synchronously for all clouds at once:
 //   level l: every node i covers tree positions [n*i/2^l, n*(i+1)/2^l) of its cloud;
-//   its bounding box is reduced (wave-segmented reduction + one atomic per segment), the
-//   widest dimension is picked, and ONE global radix sort of (cloud, node, coordinate)
-//   keys re-orders every node's range so that its lower half forms the left child
-//   (a median split).  After L levels the leaves hold <= 64 points: one wavefront.
+//   its widest dimension is estimated from the bounding box of every kSplitSample-th
+//   point (wave-segmented reduction + one atomic per segment), and ONE global radix
+//   sort of (cloud, node, coordinate) keys re-orders every node's range so that its
+//   lower half forms the left child (a median split).  After L levels the leaves hold
+//   <= 64 points: one wavefront.  The exact boxes are then computed bottom-up: a
+//   wave per leaf over the tree-ordered vectors, then unions of the children.
 // Outputs per cloud: perm (tree position -> point), pos (inverse), the vectors in tree
 // order (coalesced leaf loads) and f32 AABBs of all 2^(L+1)-1 nodes (heap order),
 // inflated by a few ulps so the f32 boxes bound the f64 points they stand for.
@@ -43,9 +45,11 @@ __global__ __launch_bounds__(256) void k_tree_init(TreeView t) {
 
 // Bounding boxes of the nodes of one level: each wave reduces its contiguous runs of
 // equal (cloud, node) with a segmented shuffle reduction; run heads issue the atomics.
+constexpr int kSplitSample = 8;  // every 8th tree position decides a node's split dimension
+
 template <int D>
 __global__ __launch_bounds__(256) void k_tree_bbox(TreeView t, int level) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int g = (blockIdx.x * blockDim.x + threadIdx.x) * kSplitSample;
     const int lane = threadIdx.x & 63;
     const bool valid = g < t.npts;
     int c = -1, node = -1;
@@ -122,20 +126,55 @@ __global__ __launch_bounds__(256) void k_tree_finish(TreeView t) {
         if (t.tvec64)
             for (int d = 0; d < t.D; ++d) t.tvec64[(size_t)d * t.ld + g] = t.vec64[(size_t)d * t.ld + cl.off + p];
     }
-    // f32 boxes, inflated so that they bound the underlying f64 values
-    const size_t nb = (size_t)t.nclouds * t.nnodes * t.D;
-    for (size_t i = g; i < nb; i += (size_t)gridDim.x * blockDim.x) {
-        const uint32_t ul = t.blo[i], uh = t.bhi[i];
-        float lo = ord_float(ul), hi = ord_float(uh);
-        if (ul == 0xffffffffu || uh == 0u || lo > hi) {  // empty node: box that no query reaches
-            lo = INFINITY;
-            hi = -INFINITY;
-        } else {
-            lo = lo - (fabsf(lo) * 4.8e-7f + 1e-30f);
-            hi = hi + (fabsf(hi) * 4.8e-7f + 1e-30f);
+}
+
+// exact f32 box of every leaf from the tree-ordered vectors (one wave per leaf),
+// inflated so that it bounds the f64 values the f32 vectors were rounded from
+template <int D>
+__global__ __launch_bounds__(256) void k_tree_leafbox(TreeView t) {
+    const int lane = threadIdx.x & 63;
+    const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int nleaf = 1 << t.L;
+    if (w >= t.nclouds * nleaf) return;
+    const int c = w / nleaf, i = w % nleaf;
+    const CloudDev cl = t.clouds[c];
+    const int a = tree_first(cl.n, t.L, i), b = tree_first(cl.n, t.L, i + 1);
+    const bool valid = lane < b - a;
+    const size_t base = ((size_t)c * t.nnodes + tree_heap(t.L, i)) * D;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        float lo = INFINITY, hi = -INFINITY;
+        if (valid) lo = hi = t.tvec[(size_t)d * t.ld + cl.off + a + lane];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            lo = fminf(lo, __shfl_xor(lo, o, 64));
+            hi = fmaxf(hi, __shfl_xor(hi, o, 64));
         }
-        t.lo[i] = lo;
-        t.hi[i] = hi;
+        if (lane == 0) {
+            if (lo <= hi) {
+                lo = lo - (fabsf(lo) * 4.8e-7f + 1e-30f);
+                hi = hi + (fabsf(hi) * 4.8e-7f + 1e-30f);
+            }
+            t.lo[base + d] = lo;  // empty leaf: [inf, -inf], a box no query reaches
+            t.hi[base + d] = hi;
+        }
+    }
+}
+
+// internal boxes = unions of the children, level by level (one block per cloud)
+__global__ __launch_bounds__(1024) void k_tree_up(TreeView t) {
+    const int c = blockIdx.x;
+    for (int l = t.L - 1; l >= 0; --l) {
+        const int items = (1 << l) * t.D;
+        for (int it = threadIdx.x; it < items; it += blockDim.x) {
+            const int i = it / t.D, d = it % t.D;
+            const int h = tree_heap(l, i);
+            const size_t o = (size_t)c * t.nnodes * t.D;
+            const size_t cl = o + (size_t)(2 * h + 1) * t.D + d, cr = o + (size_t)(2 * h + 2) * t.D + d;
+            t.lo[o + (size_t)h * t.D + d] = fminf(t.lo[cl], t.lo[cr]);
+            t.hi[o + (size_t)h * t.D + d] = fmaxf(t.hi[cl], t.hi[cr]);
+        }
+        __syncthreads();
     }
 }
 
@@ -144,6 +183,7 @@ __global__ __launch_bounds__(256) void k_tree_finish(TreeView t) {
 int build_trees(TreeView t, void* sort_tmp, size_t sort_tmp_bytes, unsigned long long* keys0,
                 unsigned long long* keys1, int32_t* vals1, hipStream_t s) {
     const int nb = (t.npts + 255) / 256;
+    const int nbs = (t.npts + 256 * kSplitSample - 1) / (256 * kSplitSample);
     const int gfill = std::max(nb, 64);
     auto bbox = (t.D == 12) ? k_tree_bbox<12> : k_tree_bbox<3>;
     hipLaunchKernelGGL(k_tree_init, dim3(gfill), dim3(256), 0, s, t);
@@ -151,15 +191,17 @@ int build_trees(TreeView t, void* sort_tmp, size_t sort_tmp_bytes, unsigned long
     while ((1 << cbits) < t.nclouds) ++cbits;
     const int end_bit = 32 + t.L + cbits;
     for (int l = 0; l < t.L; ++l) {
-        hipLaunchKernelGGL(bbox, dim3(nb), dim3(256), 0, s, t, l);
+        hipLaunchKernelGGL(bbox, dim3(nbs), dim3(256), 0, s, t, l);
         hipLaunchKernelGGL(k_tree_keys, dim3(nb), dim3(256), 0, s, t, l, keys0, vals1);
         size_t bytes = sort_tmp_bytes;
         if (hipcub::DeviceRadixSort::SortPairs(sort_tmp, bytes, keys0, keys1, vals1, t.perm, t.npts, 0, end_bit, s) !=
             hipSuccess)
             return -1;
     }
-    hipLaunchKernelGGL(bbox, dim3(nb), dim3(256), 0, s, t, t.L);
-    hipLaunchKernelGGL(k_tree_finish, dim3(gfill), dim3(256), 0, s, t);
+    hipLaunchKernelGGL(k_tree_finish, dim3(nb), dim3(256), 0, s, t);
+    const int nleaves = t.nclouds << t.L;
+    hipLaunchKernelGGL(t.D == 12 ? k_tree_leafbox<12> : k_tree_leafbox<3>, dim3((nleaves + 3) / 4), dim3(256), 0, s, t);
+    hipLaunchKernelGGL(k_tree_up, dim3(t.nclouds), dim3(1024), 0, s, t);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
