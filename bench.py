@@ -75,7 +75,7 @@ def main():
 
     import torch
     import se3icp
-    from se3icp import datasets
+    from se3icp import datasets, sharding
 
     se3icp.load()
     torch.cuda.set_device(local)
@@ -86,7 +86,8 @@ def main():
 
     P = args.pairs_per_gpu
     t0 = time.time()
-    pairs, gts = datasets.kitti_like_pairs(P, seed=4, first=rank * P, total_pairs=world * P, n_az=args.n_az)
+    first, count = sharding.shard(world * P, world, rank)  # weak scaling: P pairs per rank
+    pairs, gts = datasets.kitti_like_pairs(count, seed=4, first=first, total_pairs=world * P, n_az=args.n_az)
     npts = [p[0].shape[0] for p in pairs] + [p[1].shape[0] for p in pairs]
     log(f"rank {rank}: generated {P} pairs in {time.time() - t0:.1f}s, points/cloud "
         f"min {min(npts)} mean {np.mean(npts):.0f} max {max(npts)}")
@@ -133,19 +134,8 @@ def main():
     elapsed = time.perf_counter() - t_start
 
     # ---- cross-rank: max time, summed work, RCCL gather of the per-pair results
-    stats = torch.tensor([elapsed, float(iters), loop_ms / 1000.0], dtype=torch.float64, device=dev)
-    poses = torch.tensor(np.stack([r.T for r in last]), dtype=torch.float64, device=dev)
-    if dist:
-        t_max = stats[[0, 2]].clone()
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        tot = stats[1:2].clone()
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        gathered = [torch.empty_like(poses) for _ in range(world)]
-        dist.all_gather(gathered, poses)
-        elapsed, loop_s, iters_all = float(t_max[0]), float(t_max[1]), float(tot[0])
-    else:
-        loop_s, iters_all = loop_ms / 1000.0, float(iters)
-        gathered = [poses]
+    elapsed, loop_s, iters_all, poses_all = sharding.exchange_results(
+        dist, dev, elapsed, loop_ms / 1000.0, iters, np.stack([r.T for r in last]))
 
     if rank == 0:
         total_pairs = world * P * args.steps
@@ -219,32 +209,41 @@ def main():
             "cpu_baseline": None,
         }
         if world == 1 and args.cpu_baseline == "auto":
-            out["cpu_baseline"], out["parity_vs_cpu"] = cpu_baseline(pairs[0], last[0], args.cpu_threads)
+            out["cpu_baseline"], out["parity_vs_cpu"] = cpu_baseline(pairs, last, args.cpu_threads)
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
 
 
-def cpu_baseline(pair, gpu_res, threads):
-    """The oracle (C++/OpenMP restatement of the reference, kd-tree NN) on one pair of the
-    same workload, timed end to end on the host cores."""
+def cpu_baseline(pairs, gpu_res, threads, min_seconds=10.0, max_pairs=32):
+    """The oracle (C++/OpenMP restatement of the reference, kd-tree NN) on a bounded sample
+    of the same workload: the rank's pairs in order (cycled), until >= min_seconds of host
+    time or max_pairs registrations, timed end to end on the host cores."""
     from oracle import refcpu
     n = max(1, min(threads, os.cpu_count() or 1))
     refcpu.set_num_threads(n)
     p = refcpu.default_params(estimated_overlap=0.7, max_num_se3_iterations=10, mse=1e-7, mse_switch_error=5e-7,
                               number_of_nn_for_LRF=90)
-    log(f"cpu baseline: oracle on 1 pair with {n} threads ...")
-    t0 = time.perf_counter()
-    r = refcpu.register(pair[0], pair[1], refcpu.RUN_SE3_ICP, "gicp", p)
-    dt = time.perf_counter() - t0
-    log(f"cpu baseline: {r['num_iterations']} iterations in {dt:.2f}s")
-    base = {"value": round(r["num_iterations"] / dt, 4), "unit": "ICP iterations/s", "cores": n,
+    log(f"cpu baseline: oracle with {n} threads, >= {min_seconds:.0f} s sample ...")
+    iters, t_all, done, first = 0, 0.0, 0, None
+    while done < max_pairs and (t_all < min_seconds or done == 0):
+        src, tgt = pairs[done % len(pairs)]
+        t0 = time.perf_counter()
+        r = refcpu.register(src, tgt, refcpu.RUN_SE3_ICP, "gicp", p)
+        t_all += time.perf_counter() - t0
+        iters += r["num_iterations"]
+        if first is None:
+            first = r
+        done += 1
+    log(f"cpu baseline: {done} registrations, {iters} iterations in {t_all:.2f}s")
+    npts = int(np.mean([pr[0].shape[0] + pr[1].shape[0] for pr in pairs]) / 2)
+    base = {"value": round(iters / t_all, 4), "unit": "ICP iterations/s", "cores": n,
             "kind": "port",
-            "sample": f"1 pair (source {pair[0].shape[0]} / target {pair[1].shape[0]} pts), end to end incl. "
-                      f"setup: {r['num_iterations']} iterations in {dt:.2f} s; loop {r['time_loop_ms']:.0f} ms, "
-                      f"setup {r['time_setup_ms']:.0f} ms"}
-    parity = {"pose_frobenius": float(np.linalg.norm(gpu_res.T - r["T"])),
-              "iterations_gpu": gpu_res.num_iterations, "iterations_cpu": r["num_iterations"]}
+            "sample": f"{done} registrations of the rank's KITTI-like pairs (~{npts} pts/cloud, se3_gicp, same "
+                      f"params), end to end incl. setup: {iters} iterations in {t_all:.2f} s "
+                      f"({done / t_all:.3f} pairs/s)"}
+    parity = {"pose_frobenius": float(np.linalg.norm(gpu_res[0].T - first["T"])),
+              "iterations_gpu": gpu_res[0].num_iterations, "iterations_cpu": first["num_iterations"]}
     return base, parity
 
 

@@ -1,0 +1,49 @@
+"""Pair sharding across ranks and the end-of-batch result exchange.
+
+SURVEY.md §8(e): every scan pair is an independent registration (the reference's
+drivers make one IterativeSE3Registration per pair, examples/benchmark_kitti.cpp:128),
+so a batch of B pairs is split into contiguous blocks of B/G pairs per GPU and each rank
+registers its block with no data-path collective.  The only exchange is at the end: the
+max of the ranks' wall times (the job's time), the sum of their iteration counts and an
+all-gather of the per-pair poses (RCCL over xGMI on the GPU box; gloo in the CPU tests).
+The gathered poses are bitwise those of a single-rank run over the same pairs: no
+arithmetic crosses ranks.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def shard(n_pairs_total: int, world: int, rank: int) -> tuple[int, int]:
+    """Contiguous block [first, first + count) of the pair list owned by `rank`
+    (remainder pairs go to the lowest ranks)."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} of world {world}")
+    base, rem = divmod(n_pairs_total, world)
+    count = base + (1 if rank < rem else 0)
+    first = rank * base + min(rank, rem)
+    return first, count
+
+
+def exchange_results(dist, device, elapsed_s: float, loop_s: float, iterations: int, poses: np.ndarray):
+    """Cross-rank reduction of one timed region.
+
+    Returns (elapsed_max, loop_max, iterations_sum, poses_all) where poses_all stacks every
+    rank's [n, 4, 4] poses in rank order.  `dist` is torch.distributed (or None for one
+    rank); `device` the tensor device of the backend (cuda for nccl/RCCL, cpu for gloo).
+    Every rank must hold the same number of pairs (the gather is fixed-size).
+    """
+    import torch
+
+    poses = np.ascontiguousarray(poses, dtype=np.float64).reshape(-1, 4, 4)
+    if dist is None:
+        return float(elapsed_s), float(loop_s), int(iterations), poses
+    t_max = torch.tensor([float(elapsed_s), float(loop_s)], dtype=torch.float64, device=device)
+    dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+    tot = torch.tensor([float(iterations)], dtype=torch.float64, device=device)
+    dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    mine = torch.from_numpy(poses).to(device)
+    gathered = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
+    dist.all_gather(gathered, mine)
+    allp = np.concatenate([g.cpu().numpy() for g in gathered])
+    return float(t_max[0]), float(t_max[1]), int(round(float(tot[0]))), allp

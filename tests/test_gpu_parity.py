@@ -187,3 +187,58 @@ def test_rgbd_batch_with_cf(se3icp_mod, refcpu):
     for (s, t), g in zip(pairs, got):
         ref = refcpu.register(s, t, refcpu.RUN_SE3_ICP_CF, "gicp", rp)
         assert np.linalg.norm(g.T - ref["T"]) <= 1e-5, (g.T, ref["T"])
+
+
+@pytest.mark.parametrize("variant", ["pt2pt", "pt2pl", "gicp"])
+def test_fixture_se3_pure_matches_oracle(se3icp_mod, refcpu, fixture_clouds, variant):
+    src, tgt = fixture_clouds
+    reg = se3icp_mod.IterativeSE3Registration()
+    reg.setSourceCloud(src)
+    reg.setTargetCloud(tgt)
+    reg.estimated_overlap_ = 1.0
+    reg.max_num_se3_iterations_ = 10
+    reg.mse_ = 0.00001
+    reg.mse_switch_error_ = 5 * reg.mse_
+    reg.number_of_nn_for_LRF_ = 90
+    assert reg.run_se3_pure(variant) == 0
+    ref = refcpu.register(src, tgt, refcpu.RUN_SE3_PURE, variant, refcpu.cli_params())
+    assert np.linalg.norm(reg.current_estimated_T_ - ref["T"]) <= 1e-5
+    assert abs(reg.num_iterations_ - ref["num_iterations"]) <= 1
+    assert reg.num_pure_se3_iterations_ == reg.num_iterations_ or \
+        abs(reg.num_pure_se3_iterations_ - ref["num_pure_se3_iterations"]) <= 1
+
+
+def test_cli_on_fixture_matches_oracle(refcpu, fixture_clouds):
+    """The drop-in CLI (examples/run_registration_method.cpp) on the fixture, README.md:64."""
+    import os
+    import subprocess
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    exe = os.path.join(root, "se3-icp_amd", "bin", "run_registration_method")
+    out = subprocess.run([exe, "se3_pt2pl", os.path.join(here, "golden", "fixture_source.ply"),
+                          os.path.join(here, "golden", "fixture_target.ply")], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr
+    lines = out.stdout.splitlines()
+    assert "source point cloud size = 4167" in lines and "target point cloud size = 4167" in lines
+    assert "Running SE(3)-ICP variant: pt2pl" in lines
+    k = lines.index("Estimated transformation = ")
+    T = np.array([[float(x) for x in lines[k + 1 + r].split()] for r in range(4)])
+    src, tgt = fixture_clouds
+    ref = refcpu.register(src, tgt, refcpu.RUN_SE3_ICP, "pt2pl", refcpu.cli_params())
+    # Eigen's default stream format prints 6 significant digits
+    assert np.allclose(T, ref["T"], rtol=1e-5, atol=1e-5)
+
+
+def test_kitti_full_size_pair_matches_oracle(se3icp_mod, refcpu):
+    """BASELINE.json's size (~120k points per cloud), one pair, against the oracle."""
+    from se3icp import datasets
+    pairs, gts = datasets.kitti_like_pairs(1, seed=4, first=5, total_pairs=8)
+    assert pairs[0][0].shape[0] > 100_000
+    got = se3icp_mod.register_batch(pairs, "se3_gicp", se3icp_mod.kitti_params())[0]
+    rp = refcpu.default_params(estimated_overlap=0.7, max_num_se3_iterations=10, mse=1e-7, mse_switch_error=5e-7,
+                               number_of_nn_for_LRF=90)
+    ref = refcpu.register(pairs[0][0], pairs[0][1], refcpu.RUN_SE3_ICP, "gicp", rp)
+    assert np.linalg.norm(got.T - ref["T"]) <= 1e-5
+    assert got.num_iterations == ref["num_iterations"]
+    assert got.num_pure_se3_iterations == ref["num_pure_se3_iterations"]
