@@ -16,7 +16,6 @@
 
 #include <cfloat>
 #include <climits>
-#include <cstdlib>
 
 #include "devmath.hpp"
 #include "tree.hpp"
@@ -28,6 +27,7 @@ namespace {
 
 constexpr int kWaves = 4;
 constexpr int kBuf = 256;
+constexpr int kQ = 8;  // queries per wave (consecutive tree positions)
 
 __device__ __forceinline__ double l2_3(double ax, double ay, double az, double bx, double by, double bz) {
 #pragma clang fp contract(off)
@@ -114,274 +114,362 @@ __device__ __forceinline__ float box_lb3(const float* lo, const float* hi, float
     return dx * dx + dy * dy + dz * dz;
 }
 
-template <int WPE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void k_lrf(View v, int write_knn, int dbg_skip) {
+// Per-query state parked in LDS between the kNN pass and the batched eigen-solves
+// (slots of s_park[wave][query]).
+enum ParkSlot { PK_C = 0, PK_NC = 6, PK_R = 12, PK_KK = 13, PK_GP = 14, PK_FLAGS = 15, PK_N = 16 };
+
+__global__ __launch_bounds__(256) void k_lrf(View v, int write_knn) {
     __shared__ double s_d[kWaves][kBuf];
     __shared__ int s_i[kWaves][kBuf];
+    __shared__ int s_nb[kWaves][kQ][kMaxKnn];  // the queries' sorted neighbour lists (TOLDI ranks)
+    __shared__ double s_park[kWaves][kQ][PK_N];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    // global slot of the 3-D tree order; made wave-uniform so that the per-cloud records
-    // and the node boxes below are scalar loads
-    const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wid);
-    if (w >= v.npts) return;
-    const int c = v.cloud_of[w];
-    const CloudSetup st = v.setup[c];
-    const int K = st.k_knn;
-    if (K == 0) return;
-    const CloudDev cl = v.clouds[c];
+    // first global slot (3-D tree order) of the wave's kQ queries; wave-uniform so that
+    // the per-cloud records and the node boxes are scalar loads
+    const int w0 = __builtin_amdgcn_readfirstlane((blockIdx.x * kWaves + wid) * kQ);
+    if (w0 >= v.npts) return;
     const TreeRef T = v.t3;
-    const int n = cl.n;
-    const int gp = cl.off + T.perm[w];  // the query point
     double* bd = s_d[wid];
     int* bi = s_i[wid];
-    const double* X = v.xyz64 + cl.off;
-    const double* Y = v.xyz64 + v.ld + cl.off;
-    const double* Z = v.xyz64 + 2 * (size_t)v.ld + cl.off;
     const double* TX = T.tvec64;  // tree-ordered f64 coordinates: one coalesced load per leaf
     const double* TY = T.tvec64 + v.ld;
     const double* TZ = T.tvec64 + 2 * (size_t)v.ld;
-    const double qx = TX[w], qy = TY[w], qz = TZ[w];
-    const float fx = T.tvec[w], fy = T.tvec[v.ld + w], fz = T.tvec[2 * (size_t)v.ld + w];
-    const float* box_lo = T.lo + (size_t)c * T.nnodes * 3;
-    const float* box_hi = T.hi + (size_t)c * T.nnodes * 3;
-    const int Kw = min(K, n);
     const int first_leaf = (1 << T.L) - 1;
-    const int own = first_leaf + tree_node_of(w - cl.off, n, T.L);
+    double* park = &s_park[wid][0][0];
+    if (lane < kQ) park[lane * PK_N + PK_FLAGS] = 0.0;
+    // previous query of the wave (same cloud): its k-th distance bounds the next one's
+    int prev_c = -1, prev_K = 0;
+    double prev_kth = 0.0, pqx = 0.0, pqy = 0.0, pqz = 0.0;
+    unsigned n_queries = 0, n_leaves = 0, n_sel = 0;
 
-    // ---------------------------------------------------------------- kNN
-    // Candidates accepted by the current bound are appended, unsorted, to the wave's
-    // buffer.  Once Kw candidates exist (and whenever the buffer is full) the bound is
-    // tightened to the Kw-th smallest f32-rounded-up distance, found by bisection over
-    // the f32 bit patterns with ballot counts, and the buffer is compacted; only the
-    // survivors are sorted exactly, once, at the end.  The bound is an upper bound of the
-    // true Kw-th distance, so no member of the exact top-Kw is ever dropped.
-    int nb = 0, n_leaves = 0, n_sel = 0;
-    bool have_thr = false;
-    double thr = DBL_MAX;
-    int thr_i = INT_MAX;  // < INT_MAX only after an exact truncation (ties at thr resolved by index)
-    auto select_thr = [&]() __attribute__((always_inline)) {
-        __builtin_amdgcn_wave_barrier();
-        ++n_sel;
-        double dk[4];
-        int ik[4];
-        unsigned u[4];
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const int e = s * 64 + lane;
-            dk[s] = e < nb ? bd[e] : DBL_MAX;
-            ik[s] = e < nb ? bi[e] : INT_MAX;
-            u[s] = e < nb ? f32_up_bits(dk[s]) : 0xffffffffu;
-        }
-        unsigned lo = 0, hi = 0x7f800000u;  // count(u <= hi) = nb >= Kw
-        while (lo < hi) {
-            const unsigned mid = lo + ((hi - lo) >> 1);
-            int cnt = 0;
-#pragma unroll
-            for (int s = 0; s < 4; ++s) cnt += __popcll(__ballot(u[s] <= mid));
-            if (cnt >= Kw) hi = mid; else lo = mid + 1;
-        }
-        const double t = (double)__uint_as_float(lo);
-        if (t < thr) { thr = t; thr_i = INT_MAX; }
-        __builtin_amdgcn_wave_barrier();
-        int base = 0;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            const bool keep = dk[s] < thr || (dk[s] == thr && ik[s] <= thr_i);
-            const unsigned long long m = __ballot(keep);
-            if (keep) {
-                const int at = base + __popcll(m & ((1ull << lane) - 1ull));
-                bd[at] = dk[s];
-                bi[at] = ik[s];
-            }
-            base += __popcll(m);
-        }
-        nb = base;
-        have_thr = true;
-        if (nb > kBuf - kLeafMax) {  // massive ties at the bound: exact sort and truncation
-            __builtin_amdgcn_wave_barrier();
-            wave_bitonic<4>(bd, bi, lane, nb);
-            __builtin_amdgcn_wave_barrier();
-            nb = Kw;
-            thr = bd[Kw - 1];
-            thr_i = bi[Kw - 1];
-        }
-        __builtin_amdgcn_wave_barrier();
-    };
-    auto leaf = [&](int h) __attribute__((always_inline)) {
-        const int i = h - first_leaf;
-        ++n_leaves;
-        const int a = tree_first(n, T.L, i), b = tree_first(n, T.L, i + 1);
-        bool acc = false;
-        double d = DBL_MAX;
-        int li = INT_MAX;
-        if (lane < b - a) {
-            const int slot = cl.off + a + lane;
-            li = T.perm[slot];
-            d = l2_3(qx, qy, qz, TX[slot], TY[slot], TZ[slot]);
-            acc = !have_thr || d < thr || (d == thr && li <= thr_i);
-        }
-        const unsigned long long m = __ballot(acc);
-        if (acc) {
-            const int at = nb + __popcll(m & ((1ull << lane) - 1ull));
-            bd[at] = d;
-            bi[at] = li;
-        }
-        nb += __popcll(m);
-        if ((!have_thr && nb >= Kw) || nb > kBuf - kLeafMax) select_thr();
-    };
-    auto open = [&](float lb) __attribute__((always_inline)) {  // may a box at lb hold a candidate?
-        return !have_thr || (double)lb * (1.0 - 1e-6) <= thr;
-    };
+    for (int j = 0; j < kQ; ++j) {
+        const int w = w0 + j;
+        if (w >= v.npts) break;
+        const int c = v.cloud_of[w];
+        const CloudSetup st = v.setup[c];
+        const int K = st.k_knn;
+        if (K == 0) continue;
+        const CloudDev cl = v.clouds[c];
+        const int n = cl.n;
+        const int gp = cl.off + T.perm[w];
+        const double* X = v.xyz64 + cl.off;
+        const double* Y = v.xyz64 + v.ld + cl.off;
+        const double* Z = v.xyz64 + 2 * (size_t)v.ld + cl.off;
+        const double qx = TX[w], qy = TY[w], qz = TZ[w];
+        const float fx = T.tvec[w], fy = T.tvec[v.ld + w], fz = T.tvec[2 * (size_t)v.ld + w];
+        const float* box_lo = T.lo + (size_t)c * T.nnodes * 3;
+        const float* box_hi = T.hi + (size_t)c * T.nnodes * 3;
+        const int Kw = min(K, n);
+        const int own = first_leaf + tree_node_of(w - cl.off, n, T.L);
+        ++n_queries;
 
-    leaf(own);
-    for (int node = own; node > 0; node = (node - 1) >> 1) {
-        const int sib = (node & 1) ? node + 1 : node - 1;
-        if (!open(box_lb3(box_lo + 3 * sib, box_hi + 3 * sib, fx, fy, fz))) continue;
-        int stk = 0, sp = 0;  // stack in a VGPR: lane i holds entry i
-        stk = (lane == sp) ? sib : stk;
-        ++sp;
-        while (sp > 0) {
-            const int h = __builtin_amdgcn_readlane(stk, sp - 1);
-            --sp;
-            if (h >= first_leaf) {
-                leaf(h);
-                continue;
-            }
-            const int hl = 2 * h + 1, hr = 2 * h + 2;
-            const float ll = box_lb3(box_lo + 3 * hl, box_hi + 3 * hl, fx, fy, fz);
-            const float lr = box_lb3(box_lo + 3 * hr, box_hi + 3 * hr, fx, fy, fz);
-            const bool vl = open(ll), vr = open(lr);
-            const bool lf = ll <= lr;
-            const int nearh = lf ? hl : hr, farh = lf ? hr : hl;
-            if (lf ? vr : vl) { stk = (lane == sp) ? farh : stk; ++sp; }
-            if (lf ? vl : vr) { stk = (lane == sp) ? nearh : stk; ++sp; }
+        // ------------------------------------------------------------ kNN
+        // Candidates accepted by the current bound are appended, unsorted, to the wave's
+        // buffer.  Once Kw candidates exist (and whenever the buffer is full) the bound is
+        // tightened to the Kw-th smallest f32-rounded-up distance, found by bisection
+        // over the f32 bit patterns with ballot counts, and the buffer is compacted; the
+        // survivors are sorted exactly, once, at the end.  The bound always stays >= the
+        // true Kw-th distance, so no member of the exact top-Kw is dropped.  The previous
+        // query's k-th distance plus the distance between the two queries (triangle
+        // inequality) is such a bound from the start.
+        int nb = 0;
+        bool have_thr = false;
+        double thr = DBL_MAX;
+        int thr_i = INT_MAX;  // < INT_MAX only after an exact truncation (ties resolved by index)
+        if (prev_c == c && prev_K == K) {
+            const double dx = qx - pqx, dy = qy - pqy, dz = qz - pqz;
+            const double r = sqrt(prev_kth) + sqrt(dx * dx + dy * dy + dz * dz);
+            thr = r * r * (1.0 + 1e-12);
+            have_thr = true;
         }
+        auto select_thr = [&]() __attribute__((always_inline)) {
+            __builtin_amdgcn_wave_barrier();
+            ++n_sel;
+            double dk[4];
+            int ik[4];
+            unsigned u[4];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int e = s * 64 + lane;
+                dk[s] = e < nb ? bd[e] : DBL_MAX;
+                ik[s] = e < nb ? bi[e] : INT_MAX;
+                u[s] = e < nb ? f32_up_bits(dk[s]) : 0xffffffffu;
+            }
+            unsigned lo = 0, hi = 0x7f800000u;  // count(u <= hi) = nb >= Kw
+            while (lo < hi) {
+                const unsigned mid = lo + ((hi - lo) >> 1);
+                int cnt = 0;
+#pragma unroll
+                for (int s = 0; s < 4; ++s) cnt += __popcll(__ballot(u[s] <= mid));
+                if (cnt >= Kw) hi = mid; else lo = mid + 1;
+            }
+            const double t = (double)__uint_as_float(lo);
+            if (t < thr) { thr = t; thr_i = INT_MAX; }
+            __builtin_amdgcn_wave_barrier();
+            int base = 0;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const bool keep = dk[s] < thr || (dk[s] == thr && ik[s] <= thr_i);
+                const unsigned long long m = __ballot(keep);
+                if (keep) {
+                    const int at = base + __popcll(m & ((1ull << lane) - 1ull));
+                    bd[at] = dk[s];
+                    bi[at] = ik[s];
+                }
+                base += __popcll(m);
+            }
+            nb = base;
+            have_thr = true;
+            if (nb > kBuf - kLeafMax) {  // massive ties at the bound: exact sort and truncation
+                __builtin_amdgcn_wave_barrier();
+                wave_bitonic<4>(bd, bi, lane, nb);
+                __builtin_amdgcn_wave_barrier();
+                nb = Kw;
+                thr = bd[Kw - 1];
+                thr_i = bi[Kw - 1];
+            }
+            __builtin_amdgcn_wave_barrier();
+        };
+        auto leaf = [&](int h) __attribute__((always_inline)) {
+            const int i = h - first_leaf;
+            ++n_leaves;
+            const int a = tree_first(n, T.L, i), b = tree_first(n, T.L, i + 1);
+            bool acc = false;
+            double d = DBL_MAX;
+            int li = INT_MAX;
+            if (lane < b - a) {
+                const int slot = cl.off + a + lane;
+                li = T.perm[slot];
+                d = l2_3(qx, qy, qz, TX[slot], TY[slot], TZ[slot]);
+                acc = !have_thr || d < thr || (d == thr && li <= thr_i);
+            }
+            const unsigned long long m = __ballot(acc);
+            if (acc) {
+                const int at = nb + __popcll(m & ((1ull << lane) - 1ull));
+                bd[at] = d;
+                bi[at] = li;
+            }
+            nb += __popcll(m);
+            if ((!have_thr && nb >= Kw) || nb > kBuf - kLeafMax) select_thr();
+        };
+        auto open = [&](float lb) __attribute__((always_inline)) {  // may a box at lb hold a candidate?
+            return !have_thr || (double)lb * (1.0 - 1e-6) <= thr;
+        };
+
+        leaf(own);
+        for (int node = own; node > 0; node = (node - 1) >> 1) {
+            const int sib = (node & 1) ? node + 1 : node - 1;
+            if (!open(box_lb3(box_lo + 3 * sib, box_hi + 3 * sib, fx, fy, fz))) continue;
+            int stk = 0, sp = 0;  // stack in a VGPR: lane i holds entry i
+            stk = (lane == sp) ? sib : stk;
+            ++sp;
+            while (sp > 0) {
+                const int h = __builtin_amdgcn_readlane(stk, sp - 1);
+                --sp;
+                if (h >= first_leaf) {
+                    leaf(h);
+                    continue;
+                }
+                const int hl = 2 * h + 1, hr = 2 * h + 2;
+                const float ll = box_lb3(box_lo + 3 * hl, box_hi + 3 * hl, fx, fy, fz);
+                const float lr = box_lb3(box_lo + 3 * hr, box_hi + 3 * hr, fx, fy, fz);
+                const bool vl = open(ll), vr = open(lr);
+                const bool lf = ll <= lr;
+                const int nearh = lf ? hl : hr, farh = lf ? hr : hl;
+                if (lf ? vr : vl) { stk = (lane == sp) ? farh : stk; ++sp; }
+                if (lf ? vl : vr) { stk = (lane == sp) ? nearh : stk; ++sp; }
+            }
+        }
+        // exact order of the survivors
+        if (nb > 128) select_thr();
+        __builtin_amdgcn_wave_barrier();
+        if (nb <= 128) wave_bitonic<2>(bd, bi, lane, nb);
+        else wave_bitonic<4>(bd, bi, lane, nb);
+        __builtin_amdgcn_wave_barrier();
+        const int nTop = min(Kw, nb);
+        if (nTop == Kw) {
+            prev_c = c;
+            prev_K = K;
+            prev_kth = bd[Kw - 1];
+            pqx = qx; pqy = qy; pqz = qz;
+        } else {
+            prev_c = -1;
+        }
+        if (write_knn) {
+            int* out = v.knn + (size_t)gp * v.kmax;
+            for (int r = lane; r < K; r += 64) out[r] = r < nTop ? bi[r] : -1;
+        }
+        double* pj = park + j * PK_N;
+        int flags = 0;
+
+        // ------------------------------------------------------------ TOLDI sums (ISR.cpp:241-281)
+        if (st.k_lrf > 0) {
+            const int kk = min(st.k_lrf, nTop);
+            const int rz = kk / 3;
+            int* nbl = s_nb[wid][j];
+            for (int r = lane; r < kk; r += 64) nbl[r] = bi[r];
+            double ax[2], ay[2], az[2];
+            int rk[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {  // neighbour ranks lane+1 and lane+65 (k <= 128)
+                rk[u] = 1 + lane + 64 * u;
+                ax[u] = ay[u] = az[u] = 0.0;
+                if (rk[u] <= rz && rk[u] < kk) {
+                    const int q = bi[rk[u]];
+                    ax[u] = X[q]; ay[u] = Y[q]; az[u] = Z[q];
+                }
+            }
+            const int far = bi[kk - 1];
+            const double fdx = qx - X[far], fdy = qy - Y[far], fdz = qz - Z[far];
+            const double computed_radius = sqrt(fdx * fdx + fdy * fdy + fdz * fdz);  // ISR.cpp:256
+            // ISR.cpp:259-265 centroid quirk: ranks 1 .. rz-1 divided by rz
+            double sx = 0, sy = 0, sz = 0;
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                if (rk[u] < rz) { sx += ax[u]; sy += ay[u]; sz += az[u]; }
+            const double cx = wsum(sx) / (double)rz, cy = wsum(sy) / (double)rz, cz = wsum(sz) / (double)rz;
+            // ISR.cpp:268-272 covariance over ranks 1 .. rz
+            double c6[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+                if (rk[u] <= rz && rk[u] < kk) {
+                    const double ex = ax[u] - cx, ey = ay[u] - cy, ez = az[u] - cz;
+                    c6[0] += ex * ex; c6[1] += ex * ey; c6[2] += ex * ez;
+                    c6[3] += ey * ey; c6[4] += ey * ez; c6[5] += ez * ez;
+                }
+#pragma unroll
+            for (int i = 0; i < 6; ++i) c6[i] = wsum(c6[i]);
+            if (lane == 0) {
+#pragma unroll
+                for (int i = 0; i < 6; ++i) pj[PK_C + i] = c6[i];
+                pj[PK_R] = computed_radius;
+                pj[PK_KK] = (double)kk;
+            }
+            flags |= 1;
+        }
+
+        // ------------------------------------------------------------ normals covariance
+        // EstimateNormals (ISR.cpp:643, :43): Open3D cumulants over ranks 0 .. kn-1, self included
+        if (st.k_nrm > 0) {
+            const int kn = min(st.k_nrm, nTop);
+            double cu[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+            for (int r = lane; r < kn; r += 64) {
+                const int q = bi[r];
+                const double x = X[q], y = Y[q], z = Z[q];
+                cu[0] += x; cu[1] += y; cu[2] += z;
+                cu[3] += x * x; cu[4] += x * y; cu[5] += x * z;
+                cu[6] += y * y; cu[7] += y * z; cu[8] += z * z;
+            }
+#pragma unroll
+            for (int i = 0; i < 9; ++i) cu[i] = wsum(cu[i]) / (double)kn;
+            double n6[6] = {1, 0, 0, 1, 0, 1};
+            if (kn >= 3) {
+                n6[0] = cu[3] - cu[0] * cu[0];
+                n6[1] = cu[4] - cu[0] * cu[1];
+                n6[2] = cu[5] - cu[0] * cu[2];
+                n6[3] = cu[6] - cu[1] * cu[1];
+                n6[4] = cu[7] - cu[1] * cu[2];
+                n6[5] = cu[8] - cu[2] * cu[2];
+            }
+            if (lane == 0) {
+#pragma unroll
+                for (int i = 0; i < 6; ++i) pj[PK_NC + i] = n6[i];
+            }
+            flags |= 2;
+        }
+        if (lane == 0) {
+            pj[PK_GP] = (double)gp;
+            pj[PK_FLAGS] = (double)flags;
+        }
+        __builtin_amdgcn_wave_barrier();
     }
-    // exact order of the survivors
-    if (have_thr && nb > 128) select_thr();
-    __builtin_amdgcn_wave_barrier();
-    if (nb <= 128) wave_bitonic<2>(bd, bi, lane, nb);
-    else wave_bitonic<4>(bd, bi, lane, nb);
-    __builtin_amdgcn_wave_barrier();
-    const int nTop = min(Kw, nb);
     if (lane == 0) {  // work counters (bench diagnostics)
-        unsigned long long* ctr = v.stats + 4 * (w & 63);
-        atomicAdd(ctr + 0, 1ull);
+        unsigned long long* ctr = v.stats + 4 * ((w0 / kQ) & 63);
+        atomicAdd(ctr + 0, (unsigned long long)n_queries);
         atomicAdd(ctr + 1, (unsigned long long)n_leaves);
         atomicAdd(ctr + 2, (unsigned long long)n_sel);
     }
 
-    if (write_knn) {
-        int* out = v.knn + (size_t)gp * v.kmax;
-        for (int j = lane; j < K; j += 64) out[j] = j < nTop ? bi[j] : -1;
+    // ---------------------------------------------------------------- batched eigen-solves
+    // lane j < kQ solves query j's 3x3 problems: one solve per kQ queries instead of one
+    // per query on a whole wave
+    __builtin_amdgcn_wave_barrier();
+    const double* pl = park + (lane < kQ ? lane : 0) * PK_N;
+    const int my_flags = lane < kQ ? (int)pl[PK_FLAGS] : 0;
+    const int my_gp = (int)pl[PK_GP];
+    d3 zn{0, 0, 0};
+    if (my_flags & 1) zn = jacobi_smallest_evec(pl[PK_C], pl[PK_C + 1], pl[PK_C + 2], pl[PK_C + 3], pl[PK_C + 4], pl[PK_C + 5]);
+    if (my_flags & 2) {
+        const int c = v.cloud_of[w0 + lane];
+        d3 nm = fast_eigen3x3(pl[PK_NC], pl[PK_NC + 1], pl[PK_NC + 2], pl[PK_NC + 3], pl[PK_NC + 4], pl[PK_NC + 5]);
+        if (sqrt(dot3(nm, nm)) == 0.0) nm = d3{0, 0, 1};
+        const int gp = my_gp;
+        v.nrm64[gp] = nm.x;
+        v.nrm64[v.ld + gp] = nm.y;
+        v.nrm64[2 * (size_t)v.ld + gp] = nm.z;
+        if (v.setup[c].want_cov) {
+            double cv[6];
+            gicp_cov_from_normal(nm, 1e-3, cv);
+#pragma unroll
+            for (int r = 0; r < 6; ++r) v.cov64[(size_t)r * v.ld + gp] = cv[r];
+        }
     }
 
-    // ---------------------------------------------------------------- TOLDI frame
-    if (st.k_lrf > 0 && !(dbg_skip & 1)) {
-        const int kk = min(st.k_lrf, nTop);
-        const int rz = kk / 3;
-        // neighbour ranks lane+1 and lane+65 (k <= 128) in registers
-        double ax[2], ay[2], az[2];
-        int rk[2];
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            rk[u] = 1 + lane + 64 * u;
-            ax[u] = ay[u] = az[u] = 0.0;
-            if (rk[u] < kk) {
-                const int j = bi[rk[u]];
-                ax[u] = X[j]; ay[u] = Y[j]; az[u] = Z[j];
-            }
-        }
-        const int far = bi[kk - 1];
-        const double fdx = qx - X[far], fdy = qy - Y[far], fdz = qz - Z[far];
-        const double computed_radius = sqrt(fdx * fdx + fdy * fdy + fdz * fdz);  // ISR.cpp:256
-        // ISR.cpp:259-265 centroid quirk: ranks 1 .. rz-1 divided by rz
-        double sx = 0, sy = 0, sz = 0;
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-            if (rk[u] < rz) { sx += ax[u]; sy += ay[u]; sz += az[u]; }
-        const double cx = wsum(sx) / (double)rz, cy = wsum(sy) / (double)rz, cz = wsum(sz) / (double)rz;
-        // ISR.cpp:268-272 covariance over ranks 1 .. rz
-        double c00 = 0, c01 = 0, c02 = 0, c11 = 0, c12 = 0, c22 = 0;
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-            if (rk[u] <= rz && rk[u] < kk) {
-                const double ex = ax[u] - cx, ey = ay[u] - cy, ez = az[u] - cz;
-                c00 += ex * ex; c01 += ex * ey; c02 += ex * ez;
-                c11 += ey * ey; c12 += ey * ez; c22 += ez * ez;
-            }
-        c00 = wsum(c00); c01 = wsum(c01); c02 = wsum(c02);
-        c11 = wsum(c11); c12 = wsum(c12); c22 = wsum(c22);
-        d3 nrm = jacobi_smallest_evec(c00, c01, c02, c11, c12, c22);  // ISR.cpp:275-281
-        // ISR.cpp:286-297 over ranks 1 .. kk-1
+    // ---------------------------------------------------------------- TOLDI axes (ISR.cpp:286-306)
+    double acc3[3] = {0, 0, 0}, accs3[3] = {0, 0, 0};
+    for (int j = 0; j < kQ; ++j) {
+        const double* pj = park + j * PK_N;
+        if (!((int)pj[PK_FLAGS] & 1)) continue;
+        const int w = w0 + j;
+        const int c = v.cloud_of[w];
+        const CloudDev cl = v.clouds[c];
+        const double* X = v.xyz64 + cl.off;
+        const double* Y = v.xyz64 + v.ld + cl.off;
+        const double* Z = v.xyz64 + 2 * (size_t)v.ld + cl.off;
+        const double qx = TX[w], qy = TY[w], qz = TZ[w];
+        const double nx = __shfl(zn.x, j, 64), ny = __shfl(zn.y, j, 64), nz = __shfl(zn.z, j, 64);
+        const double R = pj[PK_R];
+        const int kk = (int)pj[PK_KK];
+        const int* nbl = s_nb[wid][j];
         double a0 = 0, a1 = 0, a2 = 0, s0 = 0, s1 = 0, s2 = 0;
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-            if (rk[u] < kk) {
-                const double vx = ax[u] - qx, vy = ay[u] - qy, vz = az[u] - qz;
-                a0 += vx; a1 += vy; a2 += vz;
-                const double an = nrm.x * vx + nrm.y * vy + nrm.z * vz;
-                const double r = computed_radius - sqrt(vx * vx + vy * vy + vz * vz);
-                const double wgt = (r * r) * (an * an);
-                s0 += wgt * vx; s1 += wgt * vy; s2 += wgt * vz;
-            }
+        for (int r = 1 + lane; r < kk; r += 64) {
+            const int q = nbl[r];
+            const double vx = X[q] - qx, vy = Y[q] - qy, vz = Z[q] - qz;
+            a0 += vx; a1 += vy; a2 += vz;
+            const double an = nx * vx + ny * vy + nz * vz;
+            const double rr = R - sqrt(vx * vx + vy * vy + vz * vz);
+            const double wgt = (rr * rr) * (an * an);
+            s0 += wgt * vx; s1 += wgt * vy; s2 += wgt * vz;
+        }
         a0 = wsum(a0); a1 = wsum(a1); a2 = wsum(a2);
         s0 = wsum(s0); s1 = wsum(s1); s2 = wsum(s2);
-        if (nrm.x * a0 + nrm.y * a1 + nrm.z * a2 < 0.0) nrm = d3{-nrm.x, -nrm.y, -nrm.z};  // ISR.cpp:298
+        if (lane == j) {
+            acc3[0] = a0; acc3[1] = a1; acc3[2] = a2;
+            accs3[0] = s0; accs3[1] = s1; accs3[2] = s2;
+        }
+    }
+    if (my_flags & 1) {
+        const int w = w0 + lane;
+        const CloudSetup st = v.setup[v.cloud_of[w]];
+        const double qx = TX[w], qy = TY[w], qz = TZ[w];
+        d3 nrm = zn;
+        if (nrm.x * acc3[0] + nrm.y * acc3[1] + nrm.z * acc3[2] < 0.0) nrm = d3{-nrm.x, -nrm.y, -nrm.z};  // ISR.cpp:298
         const d3 zax = nrm;
-        const d3 accs{s0, s1, s2};
+        const d3 accs{accs3[0], accs3[1], accs3[2]};
         d3 xax = accs - dot3(accs, zax) * zax;  // ISR.cpp:302-303 (no |x| = 0 guard, as the reference)
         xax = (1.0 / sqrt(dot3(xax, xax))) * xax;
         const d3 yax = cross3(zax, xax);  // ISR.cpp:306
-        if (lane < 12) {
-            const double al = st.alpha, be = st.beta;
-            const double f12[12] = {al * xax.x, al * xax.y, al * xax.z, al * yax.x, al * yax.y, al * yax.z,
-                                    al * zax.x, al * zax.y, al * zax.z, be * qx, be * qy, be * qz};
-            double fv = f12[0];
+        const double al = st.alpha, be = st.beta;
+        const double f12[12] = {al * xax.x, al * xax.y, al * xax.z, al * yax.x, al * yax.y, al * yax.z,
+                                al * zax.x, al * zax.y, al * zax.z, be * qx, be * qy, be * qz};
+        const int gp = my_gp;
 #pragma unroll
-            for (int r = 1; r < 12; ++r) fv = (lane == r) ? f12[r] : fv;
-            v.fr64[(size_t)lane * v.ld + gp] = fv;
+        for (int r = 0; r < 12; ++r) {
+            v.fr64[(size_t)r * v.ld + gp] = f12[r];
             // f32 copy: 12-D search vectors of targets (cf: translation rows = points,
             // ISR.cpp:834-836) and the kd-tree grouping of sources
-            double f32v = fv;
-            if (st.cf_target && lane >= 9) f32v = lane == 9 ? qx : (lane == 10 ? qy : qz);
-            v.fr32[(size_t)lane * v.ld + gp] = (float)f32v;
-        }
-    }
-
-    // ---------------------------------------------------------------- normals (+ GICP covariance)
-    if (st.k_nrm > 0 && !(dbg_skip & 2)) {
-        const int kn = min(st.k_nrm, nTop);
-        double cu[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-        for (int r = lane; r < kn; r += 64) {  // ranks 0 .. kn-1, self included
-            const int j = bi[r];
-            const double x = X[j], y = Y[j], z = Z[j];
-            cu[0] += x; cu[1] += y; cu[2] += z;
-            cu[3] += x * x; cu[4] += x * y; cu[5] += x * z;
-            cu[6] += y * y; cu[7] += y * z; cu[8] += z * z;
-        }
-#pragma unroll
-        for (int i = 0; i < 9; ++i) cu[i] = wsum(cu[i]) / (double)kn;
-        double c00 = 1, c01 = 0, c02 = 0, c11 = 1, c12 = 0, c22 = 1;
-        if (kn >= 3) {
-            c00 = cu[3] - cu[0] * cu[0];
-            c11 = cu[6] - cu[1] * cu[1];
-            c22 = cu[8] - cu[2] * cu[2];
-            c01 = cu[4] - cu[0] * cu[1];
-            c02 = cu[5] - cu[0] * cu[2];
-            c12 = cu[7] - cu[1] * cu[2];
-        }
-        d3 nm = fast_eigen3x3(c00, c01, c02, c11, c12, c22);
-        if (sqrt(dot3(nm, nm)) == 0.0) nm = d3{0, 0, 1};
-        if (lane == 0) {
-            v.nrm64[gp] = nm.x;
-            v.nrm64[v.ld + gp] = nm.y;
-            v.nrm64[2 * (size_t)v.ld + gp] = nm.z;
-            if (st.want_cov) {
-                double cv[6];
-                gicp_cov_from_normal(nm, 1e-3, cv);
-#pragma unroll
-                for (int r = 0; r < 6; ++r) v.cov64[(size_t)r * v.ld + gp] = cv[r];
-            }
+            const double f32v = (st.cf_target && r >= 9) ? (r == 9 ? qx : (r == 10 ? qy : qz)) : f12[r];
+            v.fr32[(size_t)r * v.ld + gp] = (float)f32v;
         }
     }
 }
@@ -389,18 +477,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
 }  // namespace
 
 void launch_lrf(const View& v, int write_knn, hipStream_t s) {
-    static const int wpe = [] {
-        const char* e = getenv("SE3ICP_LRF_WPE");
-        return e ? atoi(e) : 0;
-    }();
-    static const int dbg = [] {  // timing experiments only: skip the TOLDI (1) / normals (2) epilogue
-        const char* e = getenv("SE3ICP_LRF_DEBUG_SKIP");
-        return e ? atoi(e) : 0;
-    }();
-    const dim3 g((v.npts + kWaves - 1) / kWaves), b(64 * kWaves);
-    if (wpe == 8) hipLaunchKernelGGL(k_lrf<8>, g, b, 0, s, v, write_knn, dbg);
-    else if (wpe == 6) hipLaunchKernelGGL(k_lrf<6>, g, b, 0, s, v, write_knn, dbg);
-    else hipLaunchKernelGGL(k_lrf<1>, g, b, 0, s, v, write_knn, dbg);
+    const int nw = (v.npts + kQ - 1) / kQ;
+    hipLaunchKernelGGL(k_lrf, dim3((nw + kWaves - 1) / kWaves), dim3(64 * kWaves), 0, s, v, write_knn);
 }
 
 }  // namespace se3icp
