@@ -5,6 +5,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -81,6 +82,7 @@ int Engine::init() {
     HIPCHK(hipSetDevice(dev_));
     HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     for (auto& e : ev_) HIPCHK(hipEventCreate(&e));
+    if (const char* e = std::getenv("SE3ICP_L12_EXTRA")) l12_extra_ = std::max(0, std::min(2, std::atoi(e)));
     return 0;
 }
 
@@ -172,11 +174,11 @@ View Engine::view() const {
     v.work = (const BlockWork*)d_work_.p;
     v.nwork = nwork_;
     v.pair_rechecked = (int32_t*)d_rechecked_.p;
-    const int nnodes = 2 << tree_L_;
     auto ref = [&](const TreeBufs& t) {
         TreeRef r{};
-        r.L = tree_L_;
-        r.nnodes = nnodes;
+        r.L = t.L;
+        r.GL = tree_L_;
+        r.nnodes = 2 << t.L;
         r.perm = (const int32_t*)t.perm.p;
         r.pos = (const int32_t*)t.pos.p;
         r.tvec = (const float*)t.vec.p;
@@ -195,18 +197,19 @@ View Engine::view() const {
 // ----------------------------------------------------------------------------- kd-trees
 int Engine::build_tree(int D, const float* vec, hipStream_t s, const double* vec64) {
     TreeBufs& tb = (D == 12) ? t12_ : t3_;
-    const int nnodes = 2 << tree_L_;
+    tb.L = tree_L_ + (D == 12 ? l12_extra_ : 0);
+    const int nnodes = 2 << tb.L;
     const size_t nb = (size_t)nclouds_ * nnodes * D;
     if (!ensure<uint32_t>(tb.blo, nb) || !ensure<uint32_t>(tb.bhi, nb) || !ensure<float>(tb.lo, nb) ||
         !ensure<float>(tb.hi, nb) || (vec64 && !ensure<double>(tb.vec64, (size_t)D * ld_)))
         return SE3ICP_ERR_OUT_OF_MEMORY;
     int cbits = 0;
     while ((1 << cbits) < nclouds_) ++cbits;
-    const size_t need = tree_sort_temp_bytes((int)ntot_, 32 + tree_L_ + cbits);
+    const size_t need = tree_sort_temp_bytes((int)ntot_, 32 + tb.L + cbits);
     if (!ensure<char>(d_sort_tmp_, need)) return SE3ICP_ERR_OUT_OF_MEMORY;
     TreeView t{};
     t.D = D;
-    t.L = tree_L_;
+    t.L = tb.L;
     t.nnodes = nnodes;
     t.nclouds = nclouds_;
     t.npts = (int32_t)ntot_;
@@ -231,7 +234,7 @@ int Engine::build_tree(int D, const float* vec, hipStream_t s, const double* vec
 
 // Upper bound of |x| over each cloud's tree vectors, from the (inflated) root box.
 int Engine::root_norms(const TreeBufs& tb, int D, std::vector<float>* out, hipStream_t s) {
-    const int nnodes = 2 << tree_L_;
+    const int nnodes = 2 << tb.L;
     std::vector<float> lo((size_t)nclouds_ * D), hi((size_t)nclouds_ * D);
     HIPCHK(hipMemcpy2DAsync(lo.data(), sizeof(float) * D, tb.lo.p, sizeof(float) * D * nnodes, sizeof(float) * D,
                             nclouds_, hipMemcpyDeviceToHost, s));

@@ -66,6 +66,7 @@ class Engine {
     };
     struct TreeBufs {
         DevBuf perm, pos, vec, vec64, blo, bhi, lo, hi;
+        int L = 0;  // depth of the trees in these buffers
     };
     int init();
     template <class T>
@@ -93,6 +94,7 @@ class Engine {
     int64_t ntot_ = 0;
     int ld_ = 0, kmax_ = 1, nwork_ = 0, ngwork_ = 0, tree_L_ = 0;
     bool have12_ = false, knn_list_ = false;
+    int l12_extra_ = 1;  // extra levels of the 12-D trees: target leaves of <= 32 (finer pruning)
     std::vector<CloudDev> h_clouds_;
     std::vector<CloudSetup> h_setup_;
     std::vector<BlockWork> h_work_;

@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
     if (phase != (D == 12 ? PHASE_SE3 : PHASE_R3)) return;
     const CloudDev cs = v.clouds[P->src], ct = v.clouds[P->tgt];
     const TreeRef TR = (D == 12) ? v.t12 : v.t3;
-    const int a = tree_first(cs.n, TR.L, w.leaf), b = tree_first(cs.n, TR.L, w.leaf + 1);
+    const int a = tree_first(cs.n, TR.GL, w.leaf), b = tree_first(cs.n, TR.GL, w.leaf + 1);
     if (b <= a) return;
     const bool valid = lane < b - a;
     const int g = cs.off + (valid ? TR.perm[cs.off + a + lane] : TR.perm[cs.off + a]);

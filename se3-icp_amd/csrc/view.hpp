@@ -27,6 +27,7 @@ struct CloudSetup {
 // Read-only view of the kd-trees of one dimension (tree.hpp) for the query kernels.
 struct TreeRef {
     int32_t L;        // depth: leaves at level L
+    int32_t GL;       // level whose nodes are the loop's query groups (<= 64 points)
     int32_t nnodes;   // heap slots per cloud
     const int32_t* perm;  // [ld] tree position (cloud.off + x) -> local point index
     const int32_t* pos;   // [ld] point (cloud.off + i) -> local tree position
