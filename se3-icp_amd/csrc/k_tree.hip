@@ -116,6 +116,35 @@ __global__ __launch_bounds__(256) void k_tree_keys(TreeView t, int level, unsign
     vals[g] = p;
 }
 
+// 32-bit variant: key = ((cloud << level) | node) << qbits | q, with q the coordinate
+// quantised to qbits over the node's (sampled) extent.  Any partition at the median
+// position yields a valid tree -- the boxes are computed exactly afterwards -- so ties
+// from the quantisation only cost split quality, and the sort needs 3-4 digit passes
+// of 4-byte keys instead of 5-6 of 8-byte keys.
+__global__ __launch_bounds__(256) void k_tree_keys32(TreeView t, int level, int qbits, uint32_t* keys, int32_t* vals) {
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= t.npts) return;
+    const int c = t.cloud_of[g];
+    const CloudDev cl = t.clouds[c];
+    const int node = tree_node_of(g - cl.off, cl.n, level);
+    const size_t base = ((size_t)c * t.nnodes + tree_heap(level, node)) * t.D;
+    int best = 0;
+    float ext = -1.f, lo = 0.f;
+    for (int d = 0; d < t.D; ++d) {
+        const float l = ord_float(t.blo[base + d]);
+        const float e = ord_float(t.bhi[base + d]) - l;
+        if (e > ext) { ext = e; best = d; lo = l; }
+    }
+    const int p = t.perm[g];
+    const float x = t.vec[(size_t)best * t.ld + cl.off + p];
+    const float qmax = (float)((1u << qbits) - 1u);
+    float qf = (ext > 0.f && ext < INFINITY) ? (x - lo) * (qmax / ext) : 0.f;
+    qf = fminf(fmaxf(qf, 0.f), qmax);  // NaN -> 0
+    const uint32_t q = (uint32_t)qf;
+    keys[g] = ((((uint32_t)c << level) | (uint32_t)node) << qbits) | q;
+    vals[g] = p;
+}
+
 __global__ __launch_bounds__(256) void k_tree_finish(TreeView t) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g < t.npts) {
@@ -192,11 +221,25 @@ int build_trees(TreeView t, void* sort_tmp, size_t sort_tmp_bytes, unsigned long
     const int end_bit = 32 + t.L + cbits;
     for (int l = 0; l < t.L; ++l) {
         hipLaunchKernelGGL(bbox, dim3(nbs), dim3(256), 0, s, t, l);
-        hipLaunchKernelGGL(k_tree_keys, dim3(nb), dim3(256), 0, s, t, l, keys0, vals1);
+        // 24-bit keys (3 passes) while >= 8 quantisation bits remain, then 32-bit keys,
+        // then the exact 64-bit keys (very large batches only)
+        const int q24 = 24 - cbits - l, q32 = 32 - cbits - l;
         size_t bytes = sort_tmp_bytes;
-        if (hipcub::DeviceRadixSort::SortPairs(sort_tmp, bytes, keys0, keys1, vals1, t.perm, t.npts, 0, end_bit, s) !=
-            hipSuccess)
-            return -1;
+        if (q24 >= 8 || q32 >= 8) {
+            const int qb = q24 >= 8 ? q24 : q32;
+            const int eb = q24 >= 8 ? 24 : 32;
+            uint32_t* k0 = reinterpret_cast<uint32_t*>(keys0);
+            uint32_t* k1 = reinterpret_cast<uint32_t*>(keys1);
+            hipLaunchKernelGGL(k_tree_keys32, dim3(nb), dim3(256), 0, s, t, l, qb, k0, vals1);
+            if (hipcub::DeviceRadixSort::SortPairs(sort_tmp, bytes, k0, k1, vals1, t.perm, t.npts, 0, eb, s) !=
+                hipSuccess)
+                return -1;
+        } else {
+            hipLaunchKernelGGL(k_tree_keys, dim3(nb), dim3(256), 0, s, t, l, keys0, vals1);
+            if (hipcub::DeviceRadixSort::SortPairs(sort_tmp, bytes, keys0, keys1, vals1, t.perm, t.npts, 0, end_bit,
+                                                   s) != hipSuccess)
+                return -1;
+        }
     }
     hipLaunchKernelGGL(k_tree_finish, dim3(nb), dim3(256), 0, s, t);
     const int nleaves = t.nclouds << t.L;
@@ -206,10 +249,12 @@ int build_trees(TreeView t, void* sort_tmp, size_t sort_tmp_bytes, unsigned long
 }
 
 size_t tree_sort_temp_bytes(int npts, int end_bit) {
-    size_t bytes = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                       (int32_t*)nullptr, (int32_t*)nullptr, npts, 0, end_bit, (hipStream_t)0);
-    return bytes;
+    size_t b64 = 0, b32 = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b64, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                             (int32_t*)nullptr, (int32_t*)nullptr, npts, 0, end_bit, (hipStream_t)0);
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b32, (uint32_t*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr,
+                                             (int32_t*)nullptr, npts, 0, 32, (hipStream_t)0);
+    return std::max(b64, b32);
 }
 
 }  // namespace se3icp
