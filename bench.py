@@ -115,6 +115,7 @@ def main():
     t_start = time.perf_counter()
     iters = 0
     rechecked = 0
+    setup_ms = 0.0
     loop_ms = 0.0
     ktot: dict = {}
     last = None
@@ -126,6 +127,7 @@ def main():
         iters += sum(r.num_iterations for r in res)
         rechecked += sum(r.num_rechecked for r in res)
         loop_ms += res[0].time_loop_ms
+        setup_ms += res[0].time_setup_ms
         last = res
         log(f"rank {rank}: step {s} done ({sum(r.num_iterations for r in res)} iterations)")
     torch.cuda.synchronize()
@@ -191,6 +193,7 @@ def main():
             "kernel_ms_per_step": {k: round(v / args.steps, 3) for k, v in kms.items()},
             "lrf_work": lrf_work,
             "rechecked_queries_per_step": rechecked / args.steps,
+            "phase_ms_per_step": {"setup": round(setup_ms / args.steps, 3), "loop": round(loop_ms / args.steps, 3)},
             "roofline": {
                 "kernel": kname,
                 "bound": "mfma",

@@ -116,9 +116,15 @@ __device__ __forceinline__ float box_lb3(const float* lo, const float* hi, float
 
 // Per-query state parked in LDS between the kNN pass and the batched eigen-solves
 // (slots of s_park[wave][query]).
-enum ParkSlot { PK_C = 0, PK_NC = 6, PK_R = 12, PK_KK = 13, PK_GP = 14, PK_FLAGS = 15, PK_N = 16 };
+enum ParkSlot { PK_C = 0, PK_NC = 6, PK_R = 12, PK_KK = 13, PK_GP = 14, PK_FLAGS = 15, PK_K = 16, PK_N = 17 };
 
-__global__ __launch_bounds__(256) void k_lrf(View v, int write_knn) {
+// The per-cloud records and node boxes are also passed as restrict-qualified arguments:
+// with no possible aliasing store the compiler can serve their wave-uniform reads from
+// the scalar cache (s_load) instead of vector loads.
+__global__ __launch_bounds__(256) void k_lrf(View v, int write_knn, const int32_t* __restrict__ cloud_of,
+                                             const CloudSetup* __restrict__ setup,
+                                             const CloudDev* __restrict__ clouds, const float* __restrict__ tlo,
+                                             const float* __restrict__ thi) {
     __shared__ double s_d[kWaves][kBuf];
     __shared__ int s_i[kWaves][kBuf];
     __shared__ int s_nb[kWaves][kQ][kMaxKnn];  // the queries' sorted neighbour lists (TOLDI ranks)
@@ -145,11 +151,11 @@ __global__ __launch_bounds__(256) void k_lrf(View v, int write_knn) {
     for (int j = 0; j < kQ; ++j) {
         const int w = w0 + j;
         if (w >= v.npts) break;
-        const int c = v.cloud_of[w];
-        const CloudSetup st = v.setup[c];
+        const int c = cloud_of[w];
+        const CloudSetup st = setup[c];
         const int K = st.k_knn;
         if (K == 0) continue;
-        const CloudDev cl = v.clouds[c];
+        const CloudDev cl = clouds[c];
         const int n = cl.n;
         const int gp = cl.off + T.perm[w];
         const double* X = v.xyz64 + cl.off;
@@ -157,8 +163,8 @@ __global__ __launch_bounds__(256) void k_lrf(View v, int write_knn) {
         const double* Z = v.xyz64 + 2 * (size_t)v.ld + cl.off;
         const double qx = TX[w], qy = TY[w], qz = TZ[w];
         const float fx = T.tvec[w], fy = T.tvec[v.ld + w], fz = T.tvec[2 * (size_t)v.ld + w];
-        const float* box_lo = T.lo + (size_t)c * T.nnodes * 3;
-        const float* box_hi = T.hi + (size_t)c * T.nnodes * 3;
+        const float* box_lo = tlo + (size_t)c * T.nnodes * 3;
+        const float* box_hi = thi + (size_t)c * T.nnodes * 3;
         const int Kw = min(K, n);
         const int own = first_leaf + tree_node_of(w - cl.off, n, T.L);
         ++n_queries;
@@ -295,19 +301,26 @@ __global__ __launch_bounds__(256) void k_lrf(View v, int write_knn) {
         } else {
             prev_c = -1;
         }
-        if (write_knn) {
-            int* out = v.knn + (size_t)gp * v.kmax;
-            for (int r = lane; r < K; r += 64) out[r] = r < nTop ? bi[r] : -1;
-        }
+        // the sorted list stays in LDS: the kernel stores nothing to global memory inside
+        // this loop, which lets the compiler keep the per-cloud records and node boxes
+        // on the scalar path
         double* pj = park + j * PK_N;
         int flags = 0;
+        if (write_knn) {
+            int* nbl = s_nb[wid][j];
+            for (int r = lane; r < K; r += 64) nbl[r] = r < nTop ? bi[r] : -1;
+            flags |= 4;
+            if (lane == 0) pj[PK_K] = (double)K;
+        }
 
         // ------------------------------------------------------------ TOLDI sums (ISR.cpp:241-281)
         if (st.k_lrf > 0) {
             const int kk = min(st.k_lrf, nTop);
             const int rz = kk / 3;
-            int* nbl = s_nb[wid][j];
-            for (int r = lane; r < kk; r += 64) nbl[r] = bi[r];
+            if (!write_knn) {
+                int* nbl = s_nb[wid][j];
+                for (int r = lane; r < kk; r += 64) nbl[r] = bi[r];
+            }
             double ax[2], ay[2], az[2];
             int rk[2];
 #pragma unroll
@@ -394,6 +407,15 @@ __global__ __launch_bounds__(256) void k_lrf(View v, int write_knn) {
     // lane j < kQ solves query j's 3x3 problems: one solve per kQ queries instead of one
     // per query on a whole wave
     __builtin_amdgcn_wave_barrier();
+    if (write_knn) {  // se3icp_knn_self: the sorted lists
+        for (int j = 0; j < kQ; ++j) {
+            const double* pj = park + j * PK_N;
+            if (!((int)pj[PK_FLAGS] & 4)) continue;
+            const int K = (int)pj[PK_K];
+            int* out = v.knn + (size_t)(int)pj[PK_GP] * v.kmax;
+            for (int r = lane; r < K; r += 64) out[r] = s_nb[wid][j][r];
+        }
+    }
     const double* pl = park + (lane < kQ ? lane : 0) * PK_N;
     const int my_flags = lane < kQ ? (int)pl[PK_FLAGS] : 0;
     const int my_gp = (int)pl[PK_GP];
@@ -478,7 +500,8 @@ __global__ __launch_bounds__(256) void k_lrf(View v, int write_knn) {
 
 void launch_lrf(const View& v, int write_knn, hipStream_t s) {
     const int nw = (v.npts + kQ - 1) / kQ;
-    hipLaunchKernelGGL(k_lrf, dim3((nw + kWaves - 1) / kWaves), dim3(64 * kWaves), 0, s, v, write_knn);
+    hipLaunchKernelGGL(k_lrf, dim3((nw + kWaves - 1) / kWaves), dim3(64 * kWaves), 0, s, v, write_knn, v.cloud_of,
+                       v.setup, v.clouds, v.t3.lo, v.t3.hi);
 }
 
 }  // namespace se3icp
