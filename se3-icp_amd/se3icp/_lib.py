@@ -36,6 +36,12 @@ EXPORTED_SYMBOLS = [
     "se3icp_register_batch", "se3icp_register_batch_device", "se3icp_register",
     "se3icp_toldi_frames", "se3icp_knn_self", "se3icp_estimate_normals", "se3icp_nn",
     "se3icp_set_profiling", "se3icp_last_kernel_times",
+    # include/se3icp_cc.h: metrics and pose files of the benchmark drivers (host only)
+    "se3icp_cc_rot_3d", "se3icp_cc_angular_error_so3", "se3icp_cc_angular_error_so3_alt",
+    "se3icp_cc_error_filterreg", "se3icp_cc_rot2euler", "se3icp_cc_avg_eul_error",
+    "se3icp_cc_evaluate_lrf_quality", "se3icp_cc_evaluate_trajectory",
+    "se3icp_cc_read_trajectory", "se3icp_cc_read_kitti_poses", "se3icp_cc_read_redwood_log",
+    "se3icp_cc_write_trajectory", "se3icp_cc_write_redwood_log",
 ]
 
 

@@ -13,7 +13,8 @@ from conftest import ROOT
 
 
 def _header_symbols():
-    src = open(os.path.join(ROOT, "include", "se3icp.h")).read()
+    import glob
+    src = "".join(open(f).read() for f in sorted(glob.glob(os.path.join(ROOT, "include", "*.h"))))
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(se3icp_[a-z0-9_]+)\s*\(", src)))
 
