@@ -150,7 +150,9 @@ def main():
         nq = max(1.0, ktot.get("lrf_queries", 0.0))
         lrf_work = {"queries_per_step": ktot.get("lrf_queries", 0.0) / args.steps,
                     "leaves_per_query": round(ktot.get("lrf_leaves", 0.0) / nq, 2),
-                    "merges_per_query": round(ktot.get("lrf_merges", 0.0) / nq, 2)}
+                    "bound_updates_per_query": round(ktot.get("lrf_merges", 0.0) / nq, 2),
+                    "box_tests_per_query": round(ktot.get("lrf_box_tests", 0.0) / nq, 2),
+                    "candidates_per_query": round(ktot.get("lrf_candidates", 0.0) / nq, 2)}
         dom = max(["nn_se3_ms", "nn_r3_ms"], key=lambda k: kms[k])  # dominant kernel of the ICP loop
         if dom == "nn_se3_ms":
             D, evals, boxes, nl, kname = 12, ktot["se3_dist_evals"], ktot["se3_box_tests"], ktot["nn_se3_launches"], \

@@ -273,7 +273,7 @@ int se3icp_set_profiling(int device, int on) {
     return 0;
 }
 
-int se3icp_last_kernel_times(int device, double* out /* [16] */) {
+int se3icp_last_kernel_times(int device, double* out /* [18] */) {
     Engine* e = usable_engine(device);
     if (!e || !out) return SE3ICP_ERR_NO_DEVICE;
     const auto& k = e->kernel_times();
@@ -293,6 +293,8 @@ int se3icp_last_kernel_times(int device, double* out /* [16] */) {
     out[13] = k.lrf_queries;
     out[14] = k.lrf_leaves;
     out[15] = k.lrf_merges;
+    out[16] = k.lrf_box_tests;
+    out[17] = k.lrf_candidates;
     return 0;
 }
 

@@ -67,7 +67,7 @@ int pinned(T*& p, size_t& cap, size_t count) {
     return 0;
 }
 
-constexpr int kStatSlots = 64;  // NN work counters: [64][4] u64
+constexpr int kStatSlots = 64;  // work counters: [64][kStatCols] u64 (spread against atomic contention)
 
 }  // namespace
 
@@ -136,7 +136,7 @@ int Engine::alloc_points(int64_t ntot, int kmax, bool knn_list) {
               (!knn_list || ensure<int32_t>(d_knn_, L * kmax_)) && ensure<int32_t>(d_corr_idx_, L) && ensure<float>(d_corr_dist_, L) &&
               ensure<int32_t>(d_flag_list_, L) && ensure<int32_t>(d_flag_count_, 4) &&
               ensure<unsigned long long>(d_keys0_, L) && ensure<unsigned long long>(d_keys1_, L) &&
-              ensure<int32_t>(d_vals1_, L) && ensure<unsigned long long>(d_stats_, 4 * kStatSlots);
+              ensure<int32_t>(d_vals1_, L) && ensure<unsigned long long>(d_stats_, kStatCols * kStatSlots);
     for (TreeBufs* t : {&t3_, &t12_})
         ok = ok && ensure<int32_t>(t->perm, L) && ensure<int32_t>(t->pos, L);
     ok = ok && ensure<float>(t3_.vec, 3 * L) && ensure<float>(t12_.vec, 12 * L);
@@ -359,23 +359,25 @@ int Engine::setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool nor
     bool any_knn = false;
     for (int c = 0; c < nclouds_; ++c) any_knn |= h_setup_[c].k_knn > 0;
     if (any_knn) {
-        HIPCHK(hipMemsetAsync(d_stats_.p, 0, sizeof(unsigned long long) * 4 * kStatSlots, s));
+        HIPCHK(hipMemsetAsync(d_stats_.p, 0, sizeof(unsigned long long) * kStatCols * kStatSlots, s));
         HIPCHK(hipEventRecord(ev_[6], s));
         launch_lrf(v, knn_list_ ? 1 : 0, s);
         HIPCHK(hipEventRecord(ev_[7], s));
         HIPCHK(hipGetLastError());
-        unsigned long long stats[4 * kStatSlots];
+        unsigned long long stats[kStatCols * kStatSlots];
         HIPCHK(hipMemcpyAsync(stats, d_stats_.p, sizeof(stats), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        double sum[4] = {0, 0, 0, 0};
+        double sum[kStatCols] = {};
         for (int i = 0; i < kStatSlots; ++i)
-            for (int k = 0; k < 4; ++k) sum[k] += (double)stats[4 * i + k];
+            for (int k = 0; k < kStatCols; ++k) sum[k] += (double)stats[kStatCols * i + k];
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, ev_[6], ev_[7]));
         ktimes_.lrf_ms = ms;
         ktimes_.lrf_queries = sum[0];
         ktimes_.lrf_leaves = sum[1];
         ktimes_.lrf_merges = sum[2];
+        ktimes_.lrf_box_tests = sum[3];
+        ktimes_.lrf_candidates = sum[4];
     }
     HIPCHK(hipGetLastError());
     // 5) 12-D kd-trees over the alpha/beta-weighted SE(3) elements
@@ -472,7 +474,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     if (!ensure<GroupWork>(d_gwork_, ngwork_)) return SE3ICP_ERR_OUT_OF_MEMORY;
     HIPCHK(hipMemcpyAsync(d_gwork_.p, h_gwork_.data(), sizeof(GroupWork) * ngwork_, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemsetAsync(d_corr_idx_.p, 0xff, sizeof(int32_t) * ld_, s));  // no previous match yet
-    HIPCHK(hipMemsetAsync(d_stats_.p, 0, sizeof(unsigned long long) * 4 * kStatSlots, s));
+    HIPCHK(hipMemsetAsync(d_stats_.p, 0, sizeof(unsigned long long) * kStatCols * kStatSlots, s));
     // norm bounds of the target search vectors (f32 error certificate) from the root boxes
     std::vector<float> n12, n3;
     rc = root_norms(t3_, 3, &n3, s);
@@ -591,12 +593,12 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     }
     HIPCHK(hipMemcpyAsync(h_rechecked_, d_rechecked_.p, sizeof(int32_t) * npairs, hipMemcpyDeviceToHost, s));
     {
-        unsigned long long stats[4 * kStatSlots];
+        unsigned long long stats[kStatCols * kStatSlots];
         HIPCHK(hipMemcpyAsync(stats, d_stats_.p, sizeof(stats), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
-        double sum[4] = {0, 0, 0, 0};
+        double sum[kStatCols] = {};
         for (int i = 0; i < kStatSlots; ++i)
-            for (int k = 0; k < 4; ++k) sum[k] += (double)stats[4 * i + k];
+            for (int k = 0; k < kStatCols; ++k) sum[k] += (double)stats[kStatCols * i + k];
         ktimes_.se3_dist_evals = sum[0];
         ktimes_.se3_box_tests = sum[1];
         ktimes_.r3_dist_evals = sum[2];

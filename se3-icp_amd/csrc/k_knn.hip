@@ -116,18 +116,20 @@ __device__ __forceinline__ float box_lb3(const float* lo, const float* hi, float
 
 // Per-query state parked in LDS between the kNN pass and the batched eigen-solves
 // (slots of s_park[wave][query]).
-enum ParkSlot { PK_C = 0, PK_NC = 6, PK_R = 12, PK_KK = 13, PK_GP = 14, PK_FLAGS = 15, PK_K = 16, PK_N = 17 };
+enum ParkSlot { PK_C = 0, PK_NC = 6, PK_R = 12, PK_KK = 13, PK_GP = 14, PK_FLAGS = 15, PK_K = 16, PK_NTOP = 17, PK_N = 18 };
 
 // The per-cloud records and node boxes are also passed as restrict-qualified arguments:
 // with no possible aliasing store the compiler can serve their wave-uniform reads from
 // the scalar cache (s_load) instead of vector loads.
-__global__ __launch_bounds__(256) void k_lrf(View v, int write_knn, const int32_t* __restrict__ cloud_of,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_lrf(View v, int write_knn, const int32_t* __restrict__ cloud_of,
                                              const CloudSetup* __restrict__ setup,
                                              const CloudDev* __restrict__ clouds, const float* __restrict__ tlo,
                                              const float* __restrict__ thi) {
     __shared__ double s_d[kWaves][kBuf];
     __shared__ int s_i[kWaves][kBuf];
-    __shared__ int s_nb[kWaves][kQ][kMaxKnn];  // the queries' sorted neighbour lists (TOLDI ranks)
+    // the queries' sorted neighbour lists: dynamic LDS, kQ x v.kmax ints per wave, sized to
+    // the batch's largest k so that five 4-wave blocks fit a CU's 160 KB
+    extern __shared__ int s_dyn[];
     __shared__ double s_park[kWaves][kQ][PK_N];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     // first global slot (3-D tree order) of the wave's kQ queries; wave-uniform so that
@@ -142,11 +144,12 @@ __global__ __launch_bounds__(256) void k_lrf(View v, int write_knn, const int32_
     const double* TZ = T.tvec64 + 2 * (size_t)v.ld;
     const int first_leaf = (1 << T.L) - 1;
     double* park = &s_park[wid][0][0];
+    int* s_nbw = s_dyn + (size_t)wid * kQ * v.kmax;
     if (lane < kQ) park[lane * PK_N + PK_FLAGS] = 0.0;
     // previous query of the wave (same cloud): its k-th distance bounds the next one's
     int prev_c = -1, prev_K = 0;
     double prev_kth = 0.0, pqx = 0.0, pqy = 0.0, pqz = 0.0;
-    unsigned n_queries = 0, n_leaves = 0, n_sel = 0;
+    unsigned n_queries = 0, n_leaves = 0, n_sel = 0, n_box = 0, n_cand = 0;
 
     for (int j = 0; j < kQ; ++j) {
         const int w = w0 + j;
@@ -158,9 +161,6 @@ __global__ __launch_bounds__(256) void k_lrf(View v, int write_knn, const int32_
         const CloudDev cl = clouds[c];
         const int n = cl.n;
         const int gp = cl.off + T.perm[w];
-        const double* X = v.xyz64 + cl.off;
-        const double* Y = v.xyz64 + v.ld + cl.off;
-        const double* Z = v.xyz64 + 2 * (size_t)v.ld + cl.off;
         const double qx = TX[w], qy = TY[w], qz = TZ[w];
         const float fx = T.tvec[w], fy = T.tvec[v.ld + w], fz = T.tvec[2 * (size_t)v.ld + w];
         const float* box_lo = tlo + (size_t)c * T.nnodes * 3;
@@ -181,12 +181,17 @@ __global__ __launch_bounds__(256) void k_lrf(View v, int write_knn, const int32_
         int nb = 0;
         bool have_thr = false;
         double thr = DBL_MAX;
+        float thr_f = INFINITY;  // f32 bound >= thr * (1 + 2e-6): box pruning in f32 (never prunes more)
+        auto set_thr_f = [&]() __attribute__((always_inline)) {
+            thr_f = __uint_as_float(f32_up_bits(thr * (1.0 + 2e-6)));
+        };
         int thr_i = INT_MAX;  // < INT_MAX only after an exact truncation (ties resolved by index)
         if (prev_c == c && prev_K == K) {
             const double dx = qx - pqx, dy = qy - pqy, dz = qz - pqz;
             const double r = sqrt(prev_kth) + sqrt(dx * dx + dy * dy + dz * dz);
             thr = r * r * (1.0 + 1e-12);
             have_thr = true;
+            set_thr_f();
         }
         auto select_thr = [&]() __attribute__((always_inline)) {
             __builtin_amdgcn_wave_barrier();
@@ -210,7 +215,7 @@ __global__ __launch_bounds__(256) void k_lrf(View v, int write_knn, const int32_
                 if (cnt >= Kw) hi = mid; else lo = mid + 1;
             }
             const double t = (double)__uint_as_float(lo);
-            if (t < thr) { thr = t; thr_i = INT_MAX; }
+            if (t < thr) { thr = t; thr_i = INT_MAX; set_thr_f(); }
             __builtin_amdgcn_wave_barrier();
             int base = 0;
 #pragma unroll
@@ -233,6 +238,7 @@ __global__ __launch_bounds__(256) void k_lrf(View v, int write_knn, const int32_
                 nb = Kw;
                 thr = bd[Kw - 1];
                 thr_i = bi[Kw - 1];
+                set_thr_f();
             }
             __builtin_amdgcn_wave_barrier();
         };
@@ -259,12 +265,13 @@ __global__ __launch_bounds__(256) void k_lrf(View v, int write_knn, const int32_
             if ((!have_thr && nb >= Kw) || nb > kBuf - kLeafMax) select_thr();
         };
         auto open = [&](float lb) __attribute__((always_inline)) {  // may a box at lb hold a candidate?
-            return !have_thr || (double)lb * (1.0 - 1e-6) <= thr;
+            return !have_thr || lb <= thr_f;
         };
 
         leaf(own);
         for (int node = own; node > 0; node = (node - 1) >> 1) {
             const int sib = (node & 1) ? node + 1 : node - 1;
+            ++n_box;
             if (!open(box_lb3(box_lo + 3 * sib, box_hi + 3 * sib, fx, fy, fz))) continue;
             int stk = 0, sp = 0;  // stack in a VGPR: lane i holds entry i
             stk = (lane == sp) ? sib : stk;
@@ -277,6 +284,7 @@ __global__ __launch_bounds__(256) void k_lrf(View v, int write_knn, const int32_
                     continue;
                 }
                 const int hl = 2 * h + 1, hr = 2 * h + 2;
+                n_box += 2;
                 const float ll = box_lb3(box_lo + 3 * hl, box_hi + 3 * hl, fx, fy, fz);
                 const float lr = box_lb3(box_lo + 3 * hr, box_hi + 3 * hr, fx, fy, fz);
                 const bool vl = open(ll), vr = open(lr);
@@ -287,6 +295,7 @@ __global__ __launch_bounds__(256) void k_lrf(View v, int write_knn, const int32_
             }
         }
         // exact order of the survivors
+        n_cand += nb;
         if (nb > 128) select_thr();
         __builtin_amdgcn_wave_barrier();
         if (nb <= 128) wave_bitonic<2>(bd, bi, lane, nb);
@@ -301,26 +310,45 @@ __global__ __launch_bounds__(256) void k_lrf(View v, int write_knn, const int32_
         } else {
             prev_c = -1;
         }
-        // the sorted list stays in LDS: the kernel stores nothing to global memory inside
-        // this loop, which lets the compiler keep the per-cloud records and node boxes
-        // on the scalar path
-        double* pj = park + j * PK_N;
-        int flags = 0;
-        if (write_knn) {
-            int* nbl = s_nb[wid][j];
-            for (int r = lane; r < K; r += 64) nbl[r] = r < nTop ? bi[r] : -1;
-            flags |= 4;
-            if (lane == 0) pj[PK_K] = (double)K;
+        // the sorted list stays in LDS (the epilogue below reads it); nothing is stored to
+        // global memory inside this loop, which lets the compiler keep the per-cloud
+        // records and node boxes on the scalar path
+        {
+            int* nbl = (s_nbw + j * v.kmax);
+            const int nstore = write_knn ? K : nTop;
+            for (int r = lane; r < nstore; r += 64) nbl[r] = r < nTop ? bi[r] : -1;
         }
+        if (lane == 0) {
+            double* pj = park + j * PK_N;
+            pj[PK_GP] = (double)gp;
+            pj[PK_K] = (double)K;
+            pj[PK_NTOP] = (double)nTop;
+            pj[PK_FLAGS] = (double)((st.k_lrf > 0 ? 1 : 0) | (st.k_nrm > 0 ? 2 : 0) | (write_knn ? 4 : 0));
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+
+    // ---------------------------------------------------------------- per-query sums
+    // (a separate pass over the parked neighbour lists keeps the kNN loop's live state small)
+    for (int j = 0; j < kQ; ++j) {
+        double* pj = park + j * PK_N;
+        const int flags = (int)pj[PK_FLAGS];
+        if (!(flags & 3)) continue;
+        const int w = w0 + j;
+        const int c = cloud_of[w];
+        const CloudSetup st = setup[c];
+        const CloudDev cl = clouds[c];
+        const double* X = v.xyz64 + cl.off;
+        const double* Y = v.xyz64 + v.ld + cl.off;
+        const double* Z = v.xyz64 + 2 * (size_t)v.ld + cl.off;
+        const double qx = TX[w], qy = TY[w], qz = TZ[w];
+        const int nTop = (int)pj[PK_NTOP];
+        const int* nbl = (s_nbw + j * v.kmax);
 
         // ------------------------------------------------------------ TOLDI sums (ISR.cpp:241-281)
-        if (st.k_lrf > 0) {
+        if (flags & 1) {
             const int kk = min(st.k_lrf, nTop);
             const int rz = kk / 3;
-            if (!write_knn) {
-                int* nbl = s_nb[wid][j];
-                for (int r = lane; r < kk; r += 64) nbl[r] = bi[r];
-            }
             double ax[2], ay[2], az[2];
             int rk[2];
 #pragma unroll
@@ -328,11 +356,11 @@ __global__ __launch_bounds__(256) void k_lrf(View v, int write_knn, const int32_
                 rk[u] = 1 + lane + 64 * u;
                 ax[u] = ay[u] = az[u] = 0.0;
                 if (rk[u] <= rz && rk[u] < kk) {
-                    const int q = bi[rk[u]];
+                    const int q = nbl[rk[u]];
                     ax[u] = X[q]; ay[u] = Y[q]; az[u] = Z[q];
                 }
             }
-            const int far = bi[kk - 1];
+            const int far = nbl[kk - 1];
             const double fdx = qx - X[far], fdy = qy - Y[far], fdz = qz - Z[far];
             const double computed_radius = sqrt(fdx * fdx + fdy * fdy + fdz * fdz);  // ISR.cpp:256
             // ISR.cpp:259-265 centroid quirk: ranks 1 .. rz-1 divided by rz
@@ -358,16 +386,15 @@ __global__ __launch_bounds__(256) void k_lrf(View v, int write_knn, const int32_
                 pj[PK_R] = computed_radius;
                 pj[PK_KK] = (double)kk;
             }
-            flags |= 1;
         }
 
         // ------------------------------------------------------------ normals covariance
         // EstimateNormals (ISR.cpp:643, :43): Open3D cumulants over ranks 0 .. kn-1, self included
-        if (st.k_nrm > 0) {
+        if (flags & 2) {
             const int kn = min(st.k_nrm, nTop);
             double cu[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
             for (int r = lane; r < kn; r += 64) {
-                const int q = bi[r];
+                const int q = nbl[r];
                 const double x = X[q], y = Y[q], z = Z[q];
                 cu[0] += x; cu[1] += y; cu[2] += z;
                 cu[3] += x * x; cu[4] += x * y; cu[5] += x * z;
@@ -388,19 +415,16 @@ __global__ __launch_bounds__(256) void k_lrf(View v, int write_knn, const int32_
 #pragma unroll
                 for (int i = 0; i < 6; ++i) pj[PK_NC + i] = n6[i];
             }
-            flags |= 2;
-        }
-        if (lane == 0) {
-            pj[PK_GP] = (double)gp;
-            pj[PK_FLAGS] = (double)flags;
         }
         __builtin_amdgcn_wave_barrier();
     }
     if (lane == 0) {  // work counters (bench diagnostics)
-        unsigned long long* ctr = v.stats + 4 * ((w0 / kQ) & 63);
+        unsigned long long* ctr = v.stats + kStatCols * ((w0 / kQ) & 63);
         atomicAdd(ctr + 0, (unsigned long long)n_queries);
         atomicAdd(ctr + 1, (unsigned long long)n_leaves);
         atomicAdd(ctr + 2, (unsigned long long)n_sel);
+        atomicAdd(ctr + 3, (unsigned long long)n_box);
+        atomicAdd(ctr + 4, (unsigned long long)n_cand);
     }
 
     // ---------------------------------------------------------------- batched eigen-solves
@@ -413,7 +437,7 @@ __global__ __launch_bounds__(256) void k_lrf(View v, int write_knn, const int32_
             if (!((int)pj[PK_FLAGS] & 4)) continue;
             const int K = (int)pj[PK_K];
             int* out = v.knn + (size_t)(int)pj[PK_GP] * v.kmax;
-            for (int r = lane; r < K; r += 64) out[r] = s_nb[wid][j][r];
+            for (int r = lane; r < K; r += 64) out[r] = s_nbw[j * v.kmax + r];
         }
     }
     const double* pl = park + (lane < kQ ? lane : 0) * PK_N;
@@ -452,7 +476,7 @@ __global__ __launch_bounds__(256) void k_lrf(View v, int write_knn, const int32_
         const double nx = __shfl(zn.x, j, 64), ny = __shfl(zn.y, j, 64), nz = __shfl(zn.z, j, 64);
         const double R = pj[PK_R];
         const int kk = (int)pj[PK_KK];
-        const int* nbl = s_nb[wid][j];
+        const int* nbl = (s_nbw + j * v.kmax);
         double a0 = 0, a1 = 0, a2 = 0, s0 = 0, s1 = 0, s2 = 0;
         for (int r = 1 + lane; r < kk; r += 64) {
             const int q = nbl[r];
@@ -500,7 +524,8 @@ __global__ __launch_bounds__(256) void k_lrf(View v, int write_knn, const int32_
 
 void launch_lrf(const View& v, int write_knn, hipStream_t s) {
     const int nw = (v.npts + kQ - 1) / kQ;
-    hipLaunchKernelGGL(k_lrf, dim3((nw + kWaves - 1) / kWaves), dim3(64 * kWaves), 0, s, v, write_knn, v.cloud_of,
+    const size_t lds = sizeof(int) * (size_t)kWaves * kQ * v.kmax;
+    hipLaunchKernelGGL(k_lrf, dim3((nw + kWaves - 1) / kWaves), dim3(64 * kWaves), lds, s, v, write_knn, v.cloud_of,
                        v.setup, v.clouds, v.t3.lo, v.t3.hi);
 }
 

@@ -169,7 +169,7 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
     }
 
     if (lane == 0) {  // 64 lanes per evaluation; 64 counter slots against contention
-        unsigned long long* st = v.stats + 4 * (gi & 63) + (D == 12 ? 0 : 2);
+        unsigned long long* st = v.stats + kStatCols * (gi & 63) + (D == 12 ? 0 : 2);
         atomicAdd(st, 64ull * n_eval);
         atomicAdd(st + 1, 64ull * n_box);
     }

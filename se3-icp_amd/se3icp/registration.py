@@ -276,9 +276,9 @@ def nearest_neighbors(query, data, device: int = 0):
 
 
 def last_kernel_times(device: int = 0) -> dict:
-    out = (C.c_double * 16)()
+    out = (C.c_double * 18)()
     _lib.check(_lib.load().se3icp_last_kernel_times(device, out))
     keys = ["nn_se3_ms", "nn_r3_ms", "recheck_ms", "trim_ms", "reduce_ms", "setup_ms", "nn_se3_launches",
             "nn_r3_launches", "se3_dist_evals", "se3_box_tests", "r3_dist_evals", "r3_box_tests",
-            "lrf_ms", "lrf_queries", "lrf_leaves", "lrf_merges"]
+            "lrf_ms", "lrf_queries", "lrf_leaves", "lrf_merges", "lrf_box_tests", "lrf_candidates"]
     return dict(zip(keys, list(out)))
