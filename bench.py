@@ -167,7 +167,7 @@ def main():
         flops = evals * flop_dist + boxes * flop_box
         achieved = flops / (t_ms / 1000.0) / 1e12 if t_ms > 0 else 0.0
         nl = max(1.0, nl)
-        traffic, traffic_src = pmc_traffic("k_nn_groupILi12" if D == 12 else "k_nn_groupILi3")
+        traffic, traffic_src = pmc_traffic("k_nn_group<12>" if D == 12 else "k_nn_group<3>")
         out = {
             "metric": "ICP iterations/sec + pairs/sec, ~120k-pt KITTI clouds, 1/2/4/8 GPU",
             "value": round(value, 3),

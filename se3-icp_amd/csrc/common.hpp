@@ -20,7 +20,7 @@ namespace se3icp {
 constexpr int kMaxKnn = 128;      // SE3ICP_MAX_KNN
 constexpr int kBlock = 256;       // threads per block of the streaming/sweep kernels
 constexpr int kRedVals = 28;      // 21 JTJ upper + 6 JTr + 1 mse-sum (pt2pt reuses the slots)
-constexpr int kStatCols = 8;      // columns of the device work-counter table (View::stats)
+constexpr int kStatCols = 12;     // columns of the device work-counter table (View::stats); 8..11: SE3ICP_PROF section cycles
 
 enum Phase : int32_t { PHASE_IDLE = 0, PHASE_SE3 = 1, PHASE_R3 = 2 };
 enum Estimator : int32_t { EST_PT2PT = 0, EST_PT2PL = 1, EST_GICP = 2 };

@@ -378,6 +378,10 @@ int Engine::setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool nor
         ktimes_.lrf_merges = sum[2];
         ktimes_.lrf_box_tests = sum[3];
         ktimes_.lrf_candidates = sum[4];
+#ifdef SE3ICP_PROF
+        std::fprintf(stderr, "[prof] k_lrf cycles/query: knn %.0f sort %.0f sums %.0f finish %.0f (queries %.0f)\n",
+                     sum[8] / sum[0], sum[9] / sum[0], sum[10] / sum[0], sum[11] / sum[0], sum[0]);
+#endif
     }
     HIPCHK(hipGetLastError());
     // 5) 12-D kd-trees over the alpha/beta-weighted SE(3) elements
@@ -603,6 +607,10 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         ktimes_.se3_box_tests = sum[1];
         ktimes_.r3_dist_evals = sum[2];
         ktimes_.r3_box_tests = sum[3];
+#ifdef SE3ICP_PROF
+        std::fprintf(stderr, "[prof] nn12: leaf visits %.0f, lanes wanting a visited leaf %.1f%% of valid lanes\n",
+                     sum[9], 100.0 * sum[8] / std::max(1.0, sum[10]));
+#endif
     }
     const double t_end = wall_ms();
 

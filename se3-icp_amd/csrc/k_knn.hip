@@ -29,14 +29,28 @@ constexpr int kWaves = 4;
 constexpr int kBuf = 256;
 constexpr int kQ = 8;  // queries per wave (consecutive tree positions)
 
+// SE3ICP_PROF builds (make prof): per-section shader-clock cycles into stats columns 8..11
+#ifdef SE3ICP_PROF
+#define PROF_NOW(t) const unsigned long long t = __builtin_readcyclecounter()
+#define PROF_ADD(acc, a, b) acc += (b) - (a)
+#else
+#define PROF_NOW(t) do {} while (0)
+#define PROF_ADD(acc, a, b) do {} while (0)
+#endif
+
 __device__ __forceinline__ double l2_3(double ax, double ay, double az, double bx, double by, double bz) {
 #pragma clang fp contract(off)
     const double d0 = ax - bx, d1 = ay - by, d2 = az - bz;
     return (d0 * d0 + d1 * d1) + d2 * d2;
 }
 
+// (d, idx) lexicographic order.  Written with bitwise operators: a short-circuit || / &&
+// on per-lane values becomes divergent control flow (exec-mask branches) on the SIMD.
 __device__ __forceinline__ bool key_less(double da, int ia, double db, int ib) {
-    return da < db || (da == db && ia < ib);
+    return (bool)((int)(da < db) | ((int)(da == db) & (int)(ia < ib)));
+}
+__device__ __forceinline__ bool key_le(double da, int ia, double db, int ib) {
+    return (bool)((int)(da < db) | ((int)(da == db) & (int)(ia <= ib)));
 }
 
 __device__ __forceinline__ double wsum(double x) {
@@ -72,7 +86,9 @@ __device__ __forceinline__ void wave_bitonic(double* bd, int* bi, int lane, int 
                     const int pi = __shfl(ki[s], pl, 64);
                     const bool up = (e & k) == 0;
                     const bool lower = (e & jd) == 0;
-                    const bool take = (lower == up) ? key_less(pd, pi, kd[s], ki[s]) : key_less(kd[s], ki[s], pd, pi);
+                    // keys are distinct except identical padding, so "mine < partner" is
+                    // !(partner < mine): one comparison, no divergent select
+                    const bool take = key_less(pd, pi, kd[s], ki[s]) != (lower != up);
                     kd[s] = take ? pd : kd[s];
                     ki[s] = take ? pi : ki[s];
                 }
@@ -82,7 +98,7 @@ __device__ __forceinline__ void wave_bitonic(double* bd, int* bi, int lane, int 
                     if ((s & jd) == 0) {
                         const int t = s | jd;
                         const bool up = ((lane * PER + s) & k) == 0;
-                        const bool sw = up ? key_less(kd[t], ki[t], kd[s], ki[s]) : key_less(kd[s], ki[s], kd[t], ki[t]);
+                        const bool sw = key_less(kd[t], ki[t], kd[s], ki[s]) != !up;
                         const double ds = kd[s], dt = kd[t];
                         const int is = ki[s], it = ki[t];
                         kd[s] = sw ? dt : ds; kd[t] = sw ? ds : dt;
@@ -150,6 +166,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     int prev_c = -1, prev_K = 0;
     double prev_kth = 0.0, pqx = 0.0, pqy = 0.0, pqz = 0.0;
     unsigned n_queries = 0, n_leaves = 0, n_sel = 0, n_box = 0, n_cand = 0;
+#ifdef SE3ICP_PROF
+    unsigned long long c_knn = 0, c_sort = 0, c_sum = 0, c_fin = 0;
+#endif
 
     for (int j = 0; j < kQ; ++j) {
         const int w = w0 + j;
@@ -168,6 +187,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         const int Kw = min(K, n);
         const int own = first_leaf + tree_node_of(w - cl.off, n, T.L);
         ++n_queries;
+        PROF_NOW(t_q0);
 
         // ------------------------------------------------------------ kNN
         // Candidates accepted by the current bound are appended, unsorted, to the wave's
@@ -220,7 +240,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
             int base = 0;
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-                const bool keep = dk[s] < thr || (dk[s] == thr && ik[s] <= thr_i);
+                const bool keep = key_le(dk[s], ik[s], thr, thr_i);
                 const unsigned long long m = __ballot(keep);
                 if (keep) {
                     const int at = base + __popcll(m & ((1ull << lane) - 1ull));
@@ -253,7 +273,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
                 const int slot = cl.off + a + lane;
                 li = T.perm[slot];
                 d = l2_3(qx, qy, qz, TX[slot], TY[slot], TZ[slot]);
-                acc = !have_thr || d < thr || (d == thr && li <= thr_i);
+                acc = (bool)((int)!have_thr | (int)key_le(d, li, thr, thr_i));
             }
             const unsigned long long m = __ballot(acc);
             if (acc) {
@@ -295,6 +315,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
             }
         }
         // exact order of the survivors
+        PROF_NOW(t_q1);
+        PROF_ADD(c_knn, t_q0, t_q1);
         n_cand += nb;
         if (nb > 128) select_thr();
         __builtin_amdgcn_wave_barrier();
@@ -326,7 +348,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
             pj[PK_FLAGS] = (double)((st.k_lrf > 0 ? 1 : 0) | (st.k_nrm > 0 ? 2 : 0) | (write_knn ? 4 : 0));
         }
         __builtin_amdgcn_wave_barrier();
+        PROF_NOW(t_q2);
+        PROF_ADD(c_sort, t_q1, t_q2);
     }
+    PROF_NOW(t_s0);
 
     // ---------------------------------------------------------------- per-query sums
     // (a separate pass over the parked neighbour lists keeps the kNN loop's live state small)
@@ -418,8 +443,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         }
         __builtin_amdgcn_wave_barrier();
     }
+    PROF_NOW(t_s1);
+    PROF_ADD(c_sum, t_s0, t_s1);
+    unsigned long long* ctr = v.stats + kStatCols * ((w0 / kQ) & 63);
     if (lane == 0) {  // work counters (bench diagnostics)
-        unsigned long long* ctr = v.stats + kStatCols * ((w0 / kQ) & 63);
         atomicAdd(ctr + 0, (unsigned long long)n_queries);
         atomicAdd(ctr + 1, (unsigned long long)n_leaves);
         atomicAdd(ctr + 2, (unsigned long long)n_sel);
@@ -518,6 +545,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
             v.fr32[(size_t)r * v.ld + gp] = (float)f32v;
         }
     }
+#ifdef SE3ICP_PROF
+    PROF_NOW(t_f1);
+    PROF_ADD(c_fin, t_s1, t_f1);
+    if (lane == 0) {
+        atomicAdd(ctr + 8, c_knn);
+        atomicAdd(ctr + 9, c_sort);
+        atomicAdd(ctr + 10, c_sum);
+        atomicAdd(ctr + 11, c_fin);
+    }
+#endif
 }
 
 }  // namespace

@@ -41,6 +41,21 @@ __device__ __forceinline__ float box_lb(const float* lo, const float* hi, const 
     return s;
 }
 
+// 12-D: dimensions in pairs on the packed f32 path (v_pk_add_f32 with the box corners
+// read as scalar pairs), max(lo - q, q - hi, 0) per dimension (v_max3_f32), v_pk_fma_f32
+// chains: 5 instead of 7 VALU per two dimensions
+__device__ __forceinline__ float box_lb12(const float* lo, const float* hi, const f32x2* q2) {
+    f32x2 s2;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+        const f32x2 a = f32x2{lo[2 * r], lo[2 * r + 1]} - q2[r];
+        const f32x2 b = q2[r] - f32x2{hi[2 * r], hi[2 * r + 1]};
+        const f32x2 e = f32x2{fmaxf(fmaxf(a.x, b.x), 0.f), fmaxf(fmaxf(a.y, b.y), 0.f)};
+        s2 = (r == 0) ? e * e : __builtin_elementwise_fma(e, e, s2);
+    }
+    return s2.x + s2.y;
+}
+
 template <int D>
 __global__ __launch_bounds__(256) void k_nn_group(View v) {
     constexpr int NV = (D + 3) / 4;
@@ -107,6 +122,9 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
     int stk = 0;  // DFS stack in a VGPR: lane i holds entry i (depth <= 2L+1 < 64)
     int sp = 1;
     unsigned n_eval = 0, n_box = 0;  // wave-uniform work counters (roofline accounting)
+#ifdef SE3ICP_PROF
+    unsigned n_want = 0, n_leafv = 0, n_valid = __popcll(__ballot(valid));
+#endif
     while (sp > 0) {
         const int h = __builtin_amdgcn_readlane(stk, sp - 1);
         --sp;
@@ -115,6 +133,13 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
             const int ta = tree_first(ct.n, TR.L, li), tb = tree_first(ct.n, TR.L, li + 1);
             const int cnt = tb - ta;
             if (cnt <= 0) continue;
+#ifdef SE3ICP_PROF
+            if constexpr (D == 12) {  // lanes whose own bound admits this leaf (union inflation)
+                const float lb = box_lb12(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q2);
+                n_want += __popcll(__ballot(valid && lb * (1.f - 2e-6f) < thr));
+                ++n_leafv;
+            }
+#endif
             __builtin_amdgcn_wave_barrier();
             if (lane < cnt) {
                 float e[NV * 4];
@@ -156,8 +181,14 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
         }
         n_box += 2;
         const int hl = 2 * h + 1, hr = 2 * h + 2;
-        const float ll = box_lb<D>(box_lo + (size_t)hl * D, box_hi + (size_t)hl * D, q);
-        const float lr = box_lb<D>(box_lo + (size_t)hr * D, box_hi + (size_t)hr * D, q);
+        float ll, lr;
+        if constexpr (D == 12) {
+            ll = box_lb12(box_lo + (size_t)hl * D, box_hi + (size_t)hl * D, q2);
+            lr = box_lb12(box_lo + (size_t)hr * D, box_hi + (size_t)hr * D, q2);
+        } else {
+            ll = box_lb<D>(box_lo + (size_t)hl * D, box_hi + (size_t)hl * D, q);
+            lr = box_lb<D>(box_lo + (size_t)hr * D, box_hi + (size_t)hr * D, q);
+        }
         // the f32 bound is within (D+2) ulps of the exact distance to the (inflated) box
         const bool vl = __ballot(ll * (1.f - 2e-6f) < thr) != 0ull;
         const bool vr = __ballot(lr * (1.f - 2e-6f) < thr) != 0ull;
@@ -172,6 +203,13 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
         unsigned long long* st = v.stats + kStatCols * (gi & 63) + (D == 12 ? 0 : 2);
         atomicAdd(st, 64ull * n_eval);
         atomicAdd(st + 1, 64ull * n_box);
+#ifdef SE3ICP_PROF
+        if (D == 12) {
+            atomicAdd(v.stats + kStatCols * (gi & 63) + 8, (unsigned long long)n_want);
+            atomicAdd(v.stats + kStatCols * (gi & 63) + 9, (unsigned long long)n_leafv);
+            atomicAdd(v.stats + kStatCols * (gi & 63) + 10, (unsigned long long)n_leafv * n_valid);
+        }
+#endif
     }
     if (!valid) return;
     // certification (see the header) and the stored distance

@@ -10,7 +10,7 @@ import os
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 _ROOT = os.path.dirname(_PKG)  # se3-icp_amd/
-LIB_PATH = os.path.join(_ROOT, "lib", "libse3icp.so")
+LIB_PATH = os.environ.get("SE3ICP_LIB") or os.path.join(_ROOT, "lib", "libse3icp.so")
 
 OK = 0
 ERR_INVALID_ARG = -1
