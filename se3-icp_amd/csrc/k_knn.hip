@@ -5,9 +5,10 @@
 //   * Open3D EstimateNormals on the k_nrm nearest (ISR.cpp:643, :43) and the GICP
 //     covariance Rx diag(eps,1,1) Rx^T (ISR.cpp:33-52).
 // One wavefront per point, points taken in kd-tree order so that neighbouring waves
-// touch the same leaves.  The wave scans the point's own leaf, then climbs the tree
-// and descends into each sibling subtree whose box can still hold a point at or below
-// the current k-th distance (register stack, near child first).  Candidates are
+// touch the same leaves.  The wave scans the point's own leaf, then tests node boxes
+// lane-parallel (64 per instruction: the nodes of the level with <= 64 leaves below
+// each, then the leaves under each open one) and scans the leaves that can still hold
+// a point at or below the current k-th distance.  Candidates are
 // (d2, index) keys in f64 with nanoflann's arithmetic (ties -> lowest index), kept in
 // a 256-entry LDS buffer re-sorted by a register bitonic network.  The TOLDI and
 // normal sums over neighbour ranks are then wave reductions (the reference sums them
@@ -53,10 +54,126 @@ __device__ __forceinline__ bool key_le(double da, int ia, double db, int ib) {
     return (bool)((int)(da < db) | ((int)(da == db) & (int)(ia <= ib)));
 }
 
+#ifndef SE3ICP_LRF_ORDER
+#define SE3ICP_LRF_ORDER 2
+#endif
+#ifndef SE3ICP_LRF_TIGHT
+#define SE3ICP_LRF_TIGHT 0
+#endif
+#ifndef SE3ICP_LRF_FASTSORT
+#define SE3ICP_LRF_FASTSORT 1
+#endif
+
+// Set bits of a wave-uniform 64-bit mask in outward order from position p (p may lie
+// outside [0, 64)): p, p+1, p-1, p+2, p-2, ... (ORDER 2), or ascending (ORDER 0).
+// Neighbouring leaves in tree order are neighbours in space, so the bound tightens early.
+struct OutwardBits {
+    unsigned long long up, dn;
+    bool flip = false;
+    __device__ OutwardBits(unsigned long long m, int p) {
+#if SE3ICP_LRF_ORDER == 2
+        if (p < 0) { up = m; dn = 0ull; }
+        else if (p >= 64) { up = 0ull; dn = m; }
+        else { dn = m & ((1ull << p) - 1ull); up = m & ~((1ull << p) - 1ull); }
+#else
+        (void)p;
+        up = m;
+        dn = 0ull;
+#endif
+    }
+    __device__ int next() {
+        const bool use_up = up != 0ull && (dn == 0ull || !flip);
+        flip = !flip;
+        if (use_up) { const int t = __builtin_ctzll(up); up &= up - 1ull; return t; }
+        if (dn != 0ull) { const int t = 63 - __builtin_clzll(dn); dn &= ~(1ull << t); return t; }
+        return -1;
+    }
+};
+
+__device__ __forceinline__ float wave_minf(float x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x = fminf(x, __shfl_xor(x, o, 64));
+    return x;
+}
+
 __device__ __forceinline__ double wsum(double x) {
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
     return x;
+}
+
+// bits of the f32 value >= d (d >= 0): the f32 keys preserve <= of the f64 distances
+__device__ __forceinline__ unsigned f32_up_bits(double d) {
+    float f = (float)d;
+    if ((double)f < d) f = __uint_as_float(__float_as_uint(f) + 1u);
+    return __float_as_uint(f);
+}
+
+// Fast path of the final order: one 64-bit key per candidate, (f32 bits of d rounded
+// up) << 32 | idx.  Distinct f32 keys are in the f64 order (f32_up_bits is monotone), so
+// the order is the exact (f64 d, idx) order unless two of the first `lim` entries share
+// an f32 key; that is detected after the network and the caller falls back to the exact
+// (f64, idx) sort (bd / bi untouched).  On success bi[] holds the sorted indices and bd[]
+// the f32-rounded-up distances (upper bounds, used only to seed the next query's bound).
+template <int PER>
+__device__ __forceinline__ bool wave_sort_u64(double* bd, int* bi, int lane, int cnt, int lim) {
+    constexpr int N = 64 * PER;
+    unsigned long long k[PER];
+#pragma unroll
+    for (int s = 0; s < PER; ++s) {
+        const int e = lane * PER + s;
+        k[s] = e < cnt ? ((unsigned long long)f32_up_bits(bd[e]) << 32) | (unsigned)bi[e] : ~0ull;
+    }
+#pragma unroll
+    for (int kk = 2; kk <= N; kk <<= 1) {
+#pragma unroll
+        for (int jd = kk >> 1; jd > 0; jd >>= 1) {
+            if (jd >= PER) {
+                const int pl = lane ^ (jd / PER);
+#pragma unroll
+                for (int s = 0; s < PER; ++s) {
+                    const int e = lane * PER + s;
+                    const unsigned long long pk = __shfl(k[s], pl, 64);
+                    // keys are distinct except identical padding (see wave_bitonic)
+                    const bool take = (pk < k[s]) != (((e & jd) == 0) != ((e & kk) == 0));
+                    k[s] = take ? pk : k[s];
+                }
+            } else {
+#pragma unroll
+                for (int s = 0; s < PER; ++s) {
+                    if ((s & jd) == 0) {
+                        const int t = s | jd;
+                        const bool up = ((lane * PER + s) & kk) == 0;
+                        const bool sw = (k[t] < k[s]) != !up;
+                        const unsigned long long ks = k[s], kt = k[t];
+                        k[s] = sw ? kt : ks;
+                        k[t] = sw ? ks : kt;
+                    }
+                }
+            }
+        }
+    }
+    bool tie = false;
+#pragma unroll
+    for (int s = 0; s + 1 < PER; ++s) {
+        const int e = lane * PER + s;
+        tie |= (bool)((int)(e + 1 < lim) & (int)((unsigned)(k[s] >> 32) == (unsigned)(k[s + 1] >> 32)));
+    }
+    {
+        const unsigned nxt = __shfl_down((unsigned)(k[0] >> 32), 1, 64);
+        const int e = lane * PER + PER - 1;
+        tie |= (bool)((int)(e + 1 < lim) & (int)(lane < 63) & (int)((unsigned)(k[PER - 1] >> 32) == nxt));
+    }
+    if (__ballot(tie) != 0ull) return false;
+#pragma unroll
+    for (int s = 0; s < PER; ++s) {
+        const int e = lane * PER + s;
+        if (e < cnt) {
+            bi[e] = (int)(unsigned)k[s];
+            bd[e] = (double)__uint_as_float((unsigned)(k[s] >> 32));
+        }
+    }
+    return true;
 }
 
 // ascending sort of the wave's first 64*PER (d2, idx) keys (PER per lane, entry
@@ -113,13 +230,6 @@ __device__ __forceinline__ void wave_bitonic(double* bd, int* bi, int lane, int 
         bd[lane * PER + s] = kd[s];
         bi[lane * PER + s] = ki[s];
     }
-}
-
-// bits of the f32 value >= d (d >= 0): the f32 keys preserve <= of the f64 distances
-__device__ __forceinline__ unsigned f32_up_bits(double d) {
-    float f = (float)d;
-    if ((double)f < d) f = __uint_as_float(__float_as_uint(f) + 1u);
-    return __float_as_uint(f);
 }
 
 // squared distance from q to a 3-D box (f32; the boxes are inflated to bound the f64 points)
@@ -206,6 +316,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
             thr_f = __uint_as_float(f32_up_bits(thr * (1.0 + 2e-6)));
         };
         int thr_i = INT_MAX;  // < INT_MAX only after an exact truncation (ties resolved by index)
+        bool tight = false;   // a bound from this query's own candidates exists
         if (prev_c == c && prev_K == K) {
             const double dx = qx - pqx, dy = qy - pqy, dz = qz - pqz;
             const double r = sqrt(prev_kth) + sqrt(dx * dx + dy * dy + dz * dz);
@@ -251,6 +362,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
             }
             nb = base;
             have_thr = true;
+            tight = true;
             if (nb > kBuf - kLeafMax) {  // massive ties at the bound: exact sort and truncation
                 __builtin_amdgcn_wave_barrier();
                 wave_bitonic<4>(bd, bi, lane, nb);
@@ -282,36 +394,71 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
                 bi[at] = li;
             }
             nb += __popcll(m);
-            if ((!have_thr && nb >= Kw) || nb > kBuf - kLeafMax) select_thr();
+            // the first bound from Kw candidates (a seeded bound is loose), then whenever the buffer fills
+            if ((!tight && nb >= Kw && (SE3ICP_LRF_TIGHT || !have_thr)) || nb > kBuf - kLeafMax) select_thr();
         };
         auto open = [&](float lb) __attribute__((always_inline)) {  // may a box at lb hold a candidate?
             return !have_thr || lb <= thr_f;
         };
 
+        // Own leaf first.  Without a bound yet (first query of the wave or of a cloud) the
+        // leaves next to it in tree order follow until Kw candidates give one.  Then the
+        // boxes are tested lane-parallel, 64 nodes per VALU instruction: all nodes of the
+        // level A = L - 6 (<= 64 leaves below each), and the leaves of each level-A node
+        // that can still hold a point within the bound; open leaves are scanned in order,
+        // re-tested against the bound as it tightens.  Every leaf whose box lies within
+        // the bound is scanned, so no member of the exact top-Kw is missed.
         leaf(own);
-        for (int node = own; node > 0; node = (node - 1) >> 1) {
-            const int sib = (node & 1) ? node + 1 : node - 1;
-            ++n_box;
-            if (!open(box_lb3(box_lo + 3 * sib, box_hi + 3 * sib, fx, fy, fz))) continue;
-            int stk = 0, sp = 0;  // stack in a VGPR: lane i holds entry i
-            stk = (lane == sp) ? sib : stk;
-            ++sp;
-            while (sp > 0) {
-                const int h = __builtin_amdgcn_readlane(stk, sp - 1);
-                --sp;
-                if (h >= first_leaf) {
-                    leaf(h);
-                    continue;
+        const int nleaf = 1 << T.L;
+        const int own_i = own - first_leaf;
+        int s_lo = own_i, s_hi = own_i;  // leaves scanned so far: [s_lo, s_hi]
+        while (!have_thr && (s_lo > 0 || s_hi < nleaf - 1)) {
+            if (s_hi < nleaf - 1) leaf(first_leaf + (++s_hi));
+            if (!have_thr && s_lo > 0) leaf(first_leaf + (--s_lo));
+        }
+        {
+            const int sh = T.L > 6 ? 6 : T.L;  // leaves per level-A node: 2^sh <= 64
+            const int A = T.L - sh;
+            const int nA = 1 << A, firstA = nA - 1;
+            for (int c0 = 0; c0 < nA; c0 += 64) {
+                const int ai = c0 + lane;
+                float lbA = INFINITY;
+                if (ai < nA) lbA = box_lb3(box_lo + 3 * (firstA + ai), box_hi + 3 * (firstA + ai), fx, fy, fz);
+                ++n_box;
+#if SE3ICP_LRF_ORDER == 1
+                // nearest first: the bound tightens fastest and the rest fall to it
+                for (;;) {
+                    const float m = wave_minf(lbA);
+                    const unsigned long long mm = __ballot(lbA == m);
+                    if (mm == 0ull || !open(m)) break;
+                    const int j = __builtin_ctzll(mm);
+                    if (lane == j) lbA = INFINITY;
+#else
+                OutwardBits itA(__ballot((int)(ai < nA) & (int)open(lbA)), (own_i >> sh) - c0);
+                for (int j; (j = itA.next()) >= 0;) {
+                    if (!open(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbA), j)))) continue;
+#endif
+                    const int l0 = (c0 + j) << sh;  // first leaf of the level-A node
+                    const int li = l0 + lane;
+                    float lbL = INFINITY;
+                    if ((int)(lane < (1 << sh)) & ((int)(li < s_lo) | (int)(li > s_hi)))
+                        lbL = box_lb3(box_lo + 3 * (first_leaf + li), box_hi + 3 * (first_leaf + li), fx, fy, fz);
+                    ++n_box;
+#if SE3ICP_LRF_ORDER == 1
+                    for (;;) {
+                        const float ml = wave_minf(lbL);
+                        const unsigned long long ml_m = __ballot(lbL == ml);
+                        if (ml_m == 0ull || !open(ml)) break;
+                        const int t = __builtin_ctzll(ml_m);
+                        if (lane == t) lbL = INFINITY;
+#else
+                    OutwardBits itL(__ballot(open(lbL)), own_i - l0);
+                    for (int t; (t = itL.next()) >= 0;) {
+                        if (!open(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbL), t)))) continue;
+#endif
+                        leaf(first_leaf + l0 + t);
+                    }
                 }
-                const int hl = 2 * h + 1, hr = 2 * h + 2;
-                n_box += 2;
-                const float ll = box_lb3(box_lo + 3 * hl, box_hi + 3 * hl, fx, fy, fz);
-                const float lr = box_lb3(box_lo + 3 * hr, box_hi + 3 * hr, fx, fy, fz);
-                const bool vl = open(ll), vr = open(lr);
-                const bool lf = ll <= lr;
-                const int nearh = lf ? hl : hr, farh = lf ? hr : hl;
-                if (lf ? vr : vl) { stk = (lane == sp) ? farh : stk; ++sp; }
-                if (lf ? vl : vr) { stk = (lane == sp) ? nearh : stk; ++sp; }
             }
         }
         // exact order of the survivors
@@ -320,8 +467,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         n_cand += nb;
         if (nb > 128) select_thr();
         __builtin_amdgcn_wave_barrier();
-        if (nb <= 128) wave_bitonic<2>(bd, bi, lane, nb);
-        else wave_bitonic<4>(bd, bi, lane, nb);
+        {
+            const int lim = min(nb, Kw + 1);  // ranks whose order matters (top-Kw and its boundary)
+            bool done = false;
+#if SE3ICP_LRF_FASTSORT
+            done = nb <= 128 ? wave_sort_u64<2>(bd, bi, lane, nb, lim) : wave_sort_u64<4>(bd, bi, lane, nb, lim);
+            __builtin_amdgcn_wave_barrier();
+#endif
+            if (!done) {
+                if (nb <= 128) wave_bitonic<2>(bd, bi, lane, nb);
+                else wave_bitonic<4>(bd, bi, lane, nb);
+            }
+        }
         __builtin_amdgcn_wave_barrier();
         const int nTop = min(Kw, nb);
         if (nTop == Kw) {
