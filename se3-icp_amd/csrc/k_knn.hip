@@ -21,6 +21,7 @@
 #include "devmath.hpp"
 #include "tree.hpp"
 #include "view.hpp"
+#include "wave.hpp"
 
 namespace se3icp {
 
@@ -90,17 +91,7 @@ struct OutwardBits {
     }
 };
 
-__device__ __forceinline__ float wave_minf(float x) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) x = fminf(x, __shfl_xor(x, o, 64));
-    return x;
-}
-
-__device__ __forceinline__ double wsum(double x) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
-    return x;
-}
+__device__ __forceinline__ double wsum(double x) { return wave_sum(x); }
 
 // bits of the f32 value >= d (d >= 0): the f32 keys preserve <= of the f64 distances
 __device__ __forceinline__ unsigned f32_up_bits(double d) {
@@ -129,11 +120,10 @@ __device__ __forceinline__ bool wave_sort_u64(double* bd, int* bi, int lane, int
 #pragma unroll
         for (int jd = kk >> 1; jd > 0; jd >>= 1) {
             if (jd >= PER) {
-                const int pl = lane ^ (jd / PER);
 #pragma unroll
                 for (int s = 0; s < PER; ++s) {
                     const int e = lane * PER + s;
-                    const unsigned long long pk = __shfl(k[s], pl, 64);
+                    const unsigned long long pk = xor_lane(k[s], jd / PER);
                     // keys are distinct except identical padding (see wave_bitonic)
                     const bool take = (pk < k[s]) != (((e & jd) == 0) != ((e & kk) == 0));
                     k[s] = take ? pk : k[s];
@@ -195,12 +185,11 @@ __device__ __forceinline__ void wave_bitonic(double* bd, int* bi, int lane, int 
 #pragma unroll
         for (int jd = k >> 1; jd > 0; jd >>= 1) {
             if (jd >= PER) {
-                const int pl = lane ^ (jd / PER);
 #pragma unroll
                 for (int s = 0; s < PER; ++s) {
                     const int e = lane * PER + s;
-                    const double pd = __shfl(kd[s], pl, 64);
-                    const int pi = __shfl(ki[s], pl, 64);
+                    const double pd = xor_lane(kd[s], jd / PER);
+                    const int pi = xor_lane(ki[s], jd / PER);
                     const bool up = (e & k) == 0;
                     const bool lower = (e & jd) == 0;
                     // keys are distinct except identical padding, so "mine < partner" is
