@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include "loopdev.hpp"
+#include "wave.hpp"
 #include "tree.hpp"
 
 namespace se3icp {
@@ -25,6 +26,10 @@ namespace {
 using namespace loopdev;
 
 constexpr int kWaves = 4;
+// Leaves wanted by at most this many lanes take the compacted path (8 lanes per query)
+#ifndef SE3ICP_NN_COMPACT
+#define SE3ICP_NN_COMPACT 40
+#endif
 
 // packed f32 pairs: v_pk_add_f32 / v_pk_fma_f32 issue two lanes' worth of f32 math per
 // instruction (the f32 vector peak of gfx950 assumes them)
@@ -56,10 +61,31 @@ __device__ __forceinline__ float box_lb12(const float* lo, const float* hi, cons
     return s2.x + s2.y;
 }
 
+// f32 squared 12-D distance of a query (dimension pairs) to a staged target: two
+// interleaved FMA chains (even / odd dimensions) and one add, within the D-term chain
+// bound f32_err assumes
+__device__ __forceinline__ float dist12(const f32x2* q2, const float4* t) {
+    const float4 A = t[0], B = t[1], C = t[2];
+    f32x2 e, s2;
+    e = q2[0] - f32x2{A.x, A.y}; s2 = e * e;
+    e = q2[1] - f32x2{A.z, A.w}; s2 = __builtin_elementwise_fma(e, e, s2);
+    e = q2[2] - f32x2{B.x, B.y}; s2 = __builtin_elementwise_fma(e, e, s2);
+    e = q2[3] - f32x2{B.z, B.w}; s2 = __builtin_elementwise_fma(e, e, s2);
+    e = q2[4] - f32x2{C.x, C.y}; s2 = __builtin_elementwise_fma(e, e, s2);
+    e = q2[5] - f32x2{C.z, C.w}; s2 = __builtin_elementwise_fma(e, e, s2);
+    return s2.x + s2.y;
+}
+
 template <int D>
 __global__ __launch_bounds__(256) void k_nn_group(View v) {
     constexpr int NV = (D + 3) / 4;
     __shared__ float4 s_tile[kWaves][kLeafMax * NV];
+    // compacted leaf sweeps (12-D): the wave's query vectors, the list of lanes that want
+    // the current leaf, and the per-query top-2 of the leaf
+    __shared__ float4 s_q[D == 12 ? kWaves : 1][D == 12 ? 64 * 3 : 1];
+    __shared__ int s_wl[kWaves][64];
+    __shared__ float s_r1[kWaves][64], s_r2[kWaves][64];
+    __shared__ int s_rb[kWaves][64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     // wave-uniform work item: the pair record, node boxes and leaf ranges become scalar loads
     const int gi = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wid);
@@ -76,12 +102,12 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
     const int g = cs.off + (valid ? TR.perm[cs.off + a + lane] : TR.perm[cs.off + a]);
 
     // query: f64 pose applied to the source element, rounded to f32
-    double Tm[12], Q[D];
-    load_T(P, Tm);
-    query_f64<D>(v, Tm, g, Q);
     float q[D];
     float na;
-    {
+    {  // (the f64 query is recomputed at the end rather than held through the traversal)
+        double Tm[12], Q[D];
+        load_T(P, Tm);
+        query_f64<D>(v, Tm, g, Q);
         double n2 = 0;
 #pragma unroll
         for (int r = 0; r < D; ++r) {
@@ -97,6 +123,11 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
     for (int r = 0; r < D / 2; ++r) q2[r] = f32x2{q[2 * r], q[2 * r + 1]};
     const float* tv = TR.tvec + ct.off;
     const size_t ld = v.ld;
+    if constexpr (D == 12) {
+        s_q[wid][lane * 3 + 0] = make_float4(q[0], q[1], q[2], q[3]);
+        s_q[wid][lane * 3 + 1] = make_float4(q[4], q[5], q[6], q[7]);
+        s_q[wid][lane * 3 + 2] = make_float4(q[8], q[9], q[10], q[11]);
+    }
 
     float d1 = INFINITY, d2 = INFINITY;
     int i1 = -1;  // target tree position of the best candidate
@@ -133,12 +164,18 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
             const int ta = tree_first(ct.n, TR.L, li), tb = tree_first(ct.n, TR.L, li + 1);
             const int cnt = tb - ta;
             if (cnt <= 0) continue;
-#ifdef SE3ICP_PROF
-            if constexpr (D == 12) {  // lanes whose own bound admits this leaf (union inflation)
-                const float lb = box_lb12(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q2);
-                n_want += __popcll(__ballot(valid && lb * (1.f - 2e-6f) < thr));
-                ++n_leafv;
+            // lanes whose own bound admits this leaf (box re-tested: the bounds shrank since the push)
+            unsigned long long W = ~0ull;
+            int w = 64;
+            if constexpr (D == 12) {
+                const float lbh = box_lb12(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q2);
+                W = __ballot(lbh * (1.f - 2e-6f) < thr);
+                if (W == 0ull) continue;
+                w = __popcll(W);
             }
+#ifdef SE3ICP_PROF
+            n_want += __popcll(W & __ballot(valid));
+            ++n_leafv;
 #endif
             __builtin_amdgcn_wave_barrier();
             if (lane < cnt) {
@@ -149,34 +186,80 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
                 for (int k = 0; k < NV; ++k) tile[lane * NV + k] = make_float4(e[4 * k], e[4 * k + 1], e[4 * k + 2], e[4 * k + 3]);
             }
             __builtin_amdgcn_wave_barrier();
-            for (int j = 0; j < cnt; ++j) {
-                float acc;
-                if constexpr (D == 12) {
-                    // two interleaved FMA chains (even / odd dimensions) and one add: within
-                    // the D-term chain bound f32_err assumes
-                    const float4 A = tile[j * 3], B = tile[j * 3 + 1], C = tile[j * 3 + 2];
-                    f32x2 e, s2;
-                    e = q2[0] - f32x2{A.x, A.y}; s2 = e * e;
-                    e = q2[1] - f32x2{A.z, A.w}; s2 = __builtin_elementwise_fma(e, e, s2);
-                    e = q2[2] - f32x2{B.x, B.y}; s2 = __builtin_elementwise_fma(e, e, s2);
-                    e = q2[3] - f32x2{B.z, B.w}; s2 = __builtin_elementwise_fma(e, e, s2);
-                    e = q2[4] - f32x2{C.x, C.y}; s2 = __builtin_elementwise_fma(e, e, s2);
-                    e = q2[5] - f32x2{C.z, C.w}; s2 = __builtin_elementwise_fma(e, e, s2);
-                    acc = s2.x + s2.y;
-                } else {
-                    const float4 A = tile[j];
-                    float e;
-                    e = q[0] - A.x; acc = e * e;
-                    e = q[1] - A.y; acc = fmaf(e, e, acc);
-                    e = q[2] - A.z; acc = fmaf(e, e, acc);
+            if (D != 12 || w > SE3ICP_NN_COMPACT) {
+                // every lane sweeps every target (broadcast LDS reads)
+                for (int j = 0; j < cnt; ++j) {
+                    float acc;
+                    if constexpr (D == 12) {
+                        acc = dist12(q2, tile + j * 3);
+                    } else {
+                        const float4 A = tile[j];
+                        float e;
+                        e = q[0] - A.x; acc = e * e;
+                        e = q[1] - A.y; acc = fmaf(e, e, acc);
+                        e = q[2] - A.z; acc = fmaf(e, e, acc);
+                    }
+                    const bool lt = acc < d1;
+                    d2 = __builtin_amdgcn_fmed3f(d1, d2, acc);
+                    d1 = lt ? acc : d1;
+                    i1 = lt ? (ta + j) : i1;  // target tree position
                 }
-                const bool lt = acc < d1;
-                d2 = __builtin_amdgcn_fmed3f(d1, d2, acc);
-                d1 = lt ? acc : d1;
-                i1 = lt ? (ta + j) : i1;  // target tree position
+                n_eval += cnt;
+            } else if constexpr (D == 12) {
+                // compacted: 8 lanes per wanting query, 4 targets per lane, then a top-2
+                // merge over the 8 lanes and into the query's own lane
+                if ((W >> lane) & 1ull)
+                    s_wl[wid][__builtin_amdgcn_mbcnt_hi((unsigned)(W >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)W, 0u))] = lane;
+                __builtin_amdgcn_wave_barrier();
+                const int sub = lane & 7;
+                for (int it = 0; it < w; it += 8) {
+                    const int slot = it + (lane >> 3);
+                    const int qi = s_wl[wid][slot < w ? slot : it];
+                    const float4 QA = s_q[wid][qi * 3], QB = s_q[wid][qi * 3 + 1], QC = s_q[wid][qi * 3 + 2];
+                    const f32x2 qq[6] = {f32x2{QA.x, QA.y}, f32x2{QA.z, QA.w}, f32x2{QB.x, QB.y},
+                                         f32x2{QB.z, QB.w}, f32x2{QC.x, QC.y}, f32x2{QC.z, QC.w}};
+                    float a1 = INFINITY, a2 = INFINITY;
+                    int b1 = 0;
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        // (loop-invariant in `it`: the compiler keeps the lane's 4 targets in
+                        // registers across the wanting queries — 4 waves/SIMD, measured faster
+                        // than re-reading them at 5)
+                        const int j = sub + 8 * u;
+                        float acc = dist12(qq, tile + 3 * (j < cnt ? j : 0));
+                        acc = j < cnt ? acc : INFINITY;
+                        const bool lt = acc < a1;
+                        a2 = __builtin_amdgcn_fmed3f(a1, a2, acc);
+                        a1 = lt ? acc : a1;
+                        b1 = lt ? j : b1;
+                    }
+#pragma unroll
+                    for (int m = 1; m <= 4; m <<= 1) {
+                        const float p1 = xor_lane(a1, m), p2 = xor_lane(a2, m);
+                        const int pb = xor_lane(b1, m);
+                        const bool lt = (bool)((int)(p1 < a1) | ((int)(p1 == a1) & (int)(pb < b1)));
+                        a2 = fminf(fmaxf(a1, p1), fminf(a2, p2));
+                        b1 = lt ? pb : b1;
+                        a1 = fminf(a1, p1);
+                    }
+                    if ((int)(sub == 0) & (int)(slot < w)) {
+                        s_r1[wid][qi] = a1;
+                        s_r2[wid][qi] = a2;
+                        s_rb[wid][qi] = ta + b1;
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+                if ((W >> lane) & 1ull) {
+                    const float r1 = s_r1[wid][lane], r2 = s_r2[wid][lane];
+                    const int rb = s_rb[wid][lane];
+                    d2 = fminf(fmaxf(d1, r1), fminf(d2, r2));
+                    i1 = r1 < d1 ? rb : i1;
+                    d1 = fminf(d1, r1);
+                }
+                __builtin_amdgcn_wave_barrier();
+                n_eval += 4 * ((w + 7) >> 3);  // 64-lane evaluation slots issued
             }
-            if (valid && d1 < INFINITY) thr = fminf(thr, d1 + 3.f * f32_err(d1, na, nb, D));
-            n_eval += cnt;
+            if ((int)valid & (int)(d1 < INFINITY)) thr = fminf(thr, d1 + 3.f * f32_err(d1, na, nb, D));
             continue;
         }
         n_box += 2;
@@ -213,8 +296,8 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
     }
     if (!valid) return;
     // certification (see the header) and the stored distance
-    const bool flag = (i1 < 0) || !(d2 - d1 > 2.f * f32_err(d2, na, nb, D));
-    if (flag && ct.n > 1) {
+    const bool flag = (bool)((int)(i1 < 0) | (int)!(d2 - d1 > 2.f * f32_err(d2, na, nb, D)));
+    if ((int)flag & (int)(ct.n > 1)) {
         const int at = atomicAdd(v.flag_count, 1);
         v.flag_list[at] = g;
         atomicAdd(&v.pair_rechecked[w.pair], 1);
@@ -222,6 +305,9 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
     // tree position -> target index; a NaN query keeps the reference's zero-initialised index
     i1 = (i1 < 0) ? 0 : TR.perm[ct.off + i1];
     v.corr_idx[g] = i1;
+    double Tm[12], Q[D];
+    load_T(P, Tm);
+    query_f64<D>(v, Tm, g, Q);
     if constexpr (D == 12) {
         v.corr_dist[g] = stored_dist(v, PHASE_SE3, ct, Q, i1);
     } else {
