@@ -207,7 +207,10 @@ int Engine::build_tree(int D, const float* vec, hipStream_t s, const double* vec
     while ((1 << cbits) < nclouds_) ++cbits;
     const size_t need = tree_sort_temp_bytes((int)ntot_, 32 + tb.L + cbits);
     if (!ensure<char>(d_sort_tmp_, need)) return SE3ICP_ERR_OUT_OF_MEMORY;
+    std::vector<int32_t> host_n(nclouds_);
+    for (int c = 0; c < nclouds_; ++c) host_n[c] = h_clouds_[c].n;
     TreeView t{};
+    t.host_n = host_n.data();
     t.D = D;
     t.L = tb.L;
     t.nnodes = nnodes;

@@ -145,6 +145,142 @@ __global__ __launch_bounds__(256) void k_tree_keys32(TreeView t, int level, int 
     vals[g] = p;
 }
 
+// The levels below G in one workgroup per level-G node (<= kLocalMax points): the node's
+// permutation stays in LDS and every level is a bitonic sort of (sub-node, coordinate
+// along the sub-node's widest dimension) keys -- the same median splits as the global
+// levels, without a device-wide radix sort per level.
+constexpr int kLocalMax = 4096;
+#ifndef SE3ICP_TREE_SPLIT
+#define SE3ICP_TREE_SPLIT 1
+#endif
+constexpr int kLocalThreads = 512;
+
+template <int D>
+__global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G) {
+    __shared__ unsigned long long s_key[kLocalMax];
+    __shared__ int32_t s_val[kLocalMax];
+    __shared__ int s_best[128];
+    const int nG = 1 << G;
+    const int c = blockIdx.x / nG, i = blockIdx.x % nG;
+    const CloudDev cl = t.clouds[c];
+    const int n = cl.n;
+    const int A = tree_first(n, G, i), m = tree_first(n, G, i + 1) - A;
+    const int tid = threadIdx.x;
+    if (m <= 1) return;
+    for (int e = tid; e < kLocalMax; e += kLocalThreads) s_val[e] = e < m ? t.perm[cl.off + A + e] : -1;
+    int np2 = 2;
+    while (np2 < m) np2 <<= 1;
+    for (int l = G; l < t.L; ++l) {
+        const int r = l - G;
+        const int nsub = 1 << r;  // sub-nodes of this level under the WG's node (<= 128: see the host)
+        // split dimension of each sub-node: widest extent of the box of every
+        // kSplitSample-th point (the sample of the global levels), a wave per sub-node
+        {
+            const int lane = tid & 63, wv = tid >> 6;
+            for (int k = wv; k < nsub; k += kLocalThreads / 64) {
+                const int a0 = tree_first(n, l, (i << r) + k) - A, a1 = tree_first(n, l, (i << r) + k + 1) - A;
+#ifndef SE3ICP_TREE_STRIDE
+                const int stride = (a1 - a0 > 64 * kSplitSample) ? kSplitSample : 1;
+#else
+                const int stride = SE3ICP_TREE_STRIDE;
+#endif
+#if SE3ICP_TREE_SPLIT == 1
+                // widest spread: the dimension of largest sample variance
+                float s1[D], s2[D];
+#pragma unroll
+                for (int d = 0; d < D; ++d) { s1[d] = 0.f; s2[d] = 0.f; }
+                int cnt = 0;
+                for (int e = a0 + lane * stride; e < a1; e += 64 * stride) {
+                    const int p = s_val[e];
+                    ++cnt;
+#pragma unroll
+                    for (int d = 0; d < D; ++d) {
+                        const float x = t.vec[(size_t)d * t.ld + cl.off + p];
+                        s1[d] += x;
+                        s2[d] = fmaf(x, x, s2[d]);
+                    }
+                }
+                for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+                const float inv = cnt > 0 ? 1.f / (float)cnt : 0.f;
+                int best = 0;
+                float ext = -1.f;
+#pragma unroll 1  // (a full unroll here crashes amdgcn instruction selection in ROCm 7.2)
+                for (int d = 0; d < D; ++d) {
+                    float a = s1[d], b = s2[d];
+#pragma unroll
+                    for (int o = 32; o >= 1; o >>= 1) {
+                        a += __shfl_xor(a, o, 64);
+                        b += __shfl_xor(b, o, 64);
+                    }
+                    const float mu = a * inv;
+                    const float e = b * inv - mu * mu;
+                    if (e > ext) { ext = e; best = d; }
+                }
+#else
+                float lo[D], hi[D];
+#pragma unroll
+                for (int d = 0; d < D; ++d) { lo[d] = INFINITY; hi[d] = -INFINITY; }
+                for (int e = a0 + lane * stride; e < a1; e += 64 * stride) {
+                    const int p = s_val[e];
+#pragma unroll
+                    for (int d = 0; d < D; ++d) {
+                        const float x = t.vec[(size_t)d * t.ld + cl.off + p];
+                        lo[d] = fminf(lo[d], x);
+                        hi[d] = fmaxf(hi[d], x);
+                    }
+                }
+                int best = 0;
+                float ext = -1.f;
+#pragma unroll 1  // (a full unroll here crashes amdgcn instruction selection in ROCm 7.2)
+                for (int d = 0; d < D; ++d) {
+                    float l0 = lo[d], h0 = hi[d];
+#pragma unroll
+                    for (int o = 32; o >= 1; o >>= 1) {
+                        l0 = fminf(l0, __shfl_xor(l0, o, 64));
+                        h0 = fmaxf(h0, __shfl_xor(h0, o, 64));
+                    }
+                    const float e = h0 - l0;
+                    if (e > ext) { ext = e; best = d; }
+                }
+#endif
+                if (lane == 0) s_best[k] = best;
+            }
+        }
+        __syncthreads();
+        for (int e = tid; e < np2; e += kLocalThreads) {
+            unsigned long long key = ~0ull;
+            if (e < m) {
+                const int sub = tree_node_of(A + e, n, l) - (i << r);
+                const int p = s_val[e];
+                const float* row = t.vec + (size_t)s_best[sub] * t.ld;
+                const uint32_t u = ord_bits(row[cl.off + p]);
+                key = (unsigned long long)u | ((unsigned long long)(unsigned)sub << 32);
+            }
+            s_key[e] = key;
+        }
+        __syncthreads();
+        for (int kk = 2; kk <= np2; kk <<= 1) {
+            for (int jd = kk >> 1; jd > 0; jd >>= 1) {
+                for (int x = tid; x < (np2 >> 1); x += kLocalThreads) {
+                    const int a = ((x & ~(jd - 1)) << 1) | (x & (jd - 1));  // bit jd of a is clear
+                    const int b = a | jd;
+                    const unsigned long long ka = s_key[a], kb = s_key[b];
+                    const bool up = (a & kk) == 0;
+                    if ((ka > kb) == up) {
+                        s_key[a] = kb;
+                        s_key[b] = ka;
+                        const int va = s_val[a];
+                        s_val[a] = s_val[b];
+                        s_val[b] = va;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+    }
+    for (int e = tid; e < m; e += kLocalThreads) t.perm[cl.off + A + e] = s_val[e];
+}
+
 __global__ __launch_bounds__(256) void k_tree_finish(TreeView t) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g < t.npts) {
@@ -219,7 +355,14 @@ int build_trees(TreeView t, void* sort_tmp, size_t sort_tmp_bytes, unsigned long
     int cbits = 0;
     while ((1 << cbits) < t.nclouds) ++cbits;
     const int end_bit = 32 + t.L + cbits;
-    for (int l = 0; l < t.L; ++l) {
+    // global levels until every node fits one workgroup's LDS sort (and <= 128 sub-nodes below)
+    int max_n = 0;
+    for (int c = 0; c < t.nclouds; ++c) max_n = std::max(max_n, t.host_n ? t.host_n[c] : 0);
+    int G = 0;
+    while (G < t.L && (((long long)max_n + (1ll << G) - 1) >> G) > kLocalMax) ++G;
+    if (t.L - 1 - G > 7) G = t.L - 8;
+    if (!t.host_n) G = t.L;
+    for (int l = 0; l < G; ++l) {
         hipLaunchKernelGGL(bbox, dim3(nbs), dim3(256), 0, s, t, l);
         // 24-bit keys (3 passes) while >= 8 quantisation bits remain, then 32-bit keys,
         // then the exact 64-bit keys (very large batches only)
@@ -241,6 +384,9 @@ int build_trees(TreeView t, void* sort_tmp, size_t sort_tmp_bytes, unsigned long
                 return -1;
         }
     }
+    if (G < t.L)
+        hipLaunchKernelGGL(t.D == 12 ? k_tree_local<12> : k_tree_local<3>, dim3(t.nclouds << G), dim3(kLocalThreads), 0,
+                           s, t, G);
     hipLaunchKernelGGL(k_tree_finish, dim3(nb), dim3(256), 0, s, t);
     const int nleaves = t.nclouds << t.L;
     hipLaunchKernelGGL(t.D == 12 ? k_tree_leafbox<12> : k_tree_leafbox<3>, dim3((nleaves + 3) / 4), dim3(256), 0, s, t);

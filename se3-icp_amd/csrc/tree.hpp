@@ -33,6 +33,7 @@ struct TreeView {
     uint32_t* bhi;
     float* lo;         // [nclouds][nnodes][D] node boxes
     float* hi;
+    const int32_t* host_n;  // host copy of the clouds' point counts (level split of the build)
 };
 
 __host__ __device__ __forceinline__ int tree_first(int n, int level, int i) {
