@@ -61,6 +61,9 @@ __device__ __forceinline__ bool key_le(double da, int ia, double db, int ib) {
 #ifndef SE3ICP_LRF_TIGHT
 #define SE3ICP_LRF_TIGHT 0
 #endif
+#ifndef SE3ICP_LRF_XCD
+#define SE3ICP_LRF_XCD 1
+#endif
 #ifndef SE3ICP_LRF_FASTSORT
 #define SE3ICP_LRF_FASTSORT 1
 #endif
@@ -249,7 +252,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     // first global slot (3-D tree order) of the wave's kQ queries; wave-uniform so that
     // the per-cloud records and the node boxes are scalar loads
-    const int w0 = __builtin_amdgcn_readfirstlane((blockIdx.x * kWaves + wid) * kQ);
+#if SE3ICP_LRF_XCD
+    const int bid = xcd_block(blockIdx.x, gridDim.x);  // neighbouring blocks (tree order) share an XCD's L2
+#else
+    const int bid = blockIdx.x;
+#endif
+    const int w0 = __builtin_amdgcn_readfirstlane((bid * kWaves + wid) * kQ);
     if (w0 >= v.npts) return;
     const TreeRef T = v.t3;
     double* bd = s_d[wid];

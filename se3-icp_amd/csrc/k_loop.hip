@@ -17,6 +17,7 @@
 #include <cmath>
 
 #include "loopdev.hpp"
+#include "wave.hpp"
 #include "tree.hpp"
 
 namespace se3icp {
@@ -408,10 +409,12 @@ __global__ __launch_bounds__(256) void k_reduce(View v) {
         }
     }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    {  // the 28 sums over the wave by recursive halving (wave.hpp)
+        double x[32];
 #pragma unroll
-    for (int i = 0; i < kRedVals; ++i) {
-        const double s = wsum(acc[i]);
-        if (lane == 0) red[wid][i] = s;
+        for (int i = 0; i < 32; ++i) x[i] = i < kRedVals ? acc[i] : 0.0;
+        const double sv = wave_sum32(x);
+        if ((int)((lane & 1) == 0) & (int)((lane >> 1) < kRedVals)) red[wid][lane >> 1] = sv;
     }
     __syncthreads();
     if (threadIdx.x < kRedVals) {

@@ -49,4 +49,60 @@ __device__ __forceinline__ float wave_minf(float x) {
     return x;
 }
 
+// Sums of 32 values over the 64 lanes by recursive halving (each exchange step sends
+// half of the values still held): 32 f64 exchanges instead of 32 x 6 butterflies.
+// Returns the total of value (lane >> 1) in every lane.
+__device__ __forceinline__ double swap_add32(double a, double b) {
+    // v_permlane32_swap on both dwords: lanes 0-31 get (own a) + (partner's a),
+    // lanes 32-63 get (own b) + (partner's b)
+    const unsigned long long ua = (unsigned long long)__double_as_longlong(a), ub = (unsigned long long)__double_as_longlong(b);
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)ua, (unsigned)ub, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+    const double na = __longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0]));
+    const double nb = __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1]));
+    return na + nb;
+}
+__device__ __forceinline__ double swap_add16(double a, double b) {
+    // v_permlane16_swap: rows 0/2 keep a and receive the odd row's a, rows 1/3 keep b
+    // and receive the even row's b
+    const unsigned long long ua = (unsigned long long)__double_as_longlong(a), ub = (unsigned long long)__double_as_longlong(b);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)ua, (unsigned)ub, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+    const double na = __longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0]));
+    const double nb = __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1]));
+    return na + nb;
+}
+__device__ __forceinline__ double wave_sum32(const double (&x)[32]) {
+    const int lane = threadIdx.x & 63;
+    double y16[16], y8[8], y4[4], y2[2];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) y16[i] = swap_add32(x[i], x[i + 16]);  // value i + 16*bit5
+#pragma unroll
+    for (int i = 0; i < 8; ++i) y8[i] = swap_add16(y16[i], y16[i + 8]);  // + 8*bit4
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // lane ^ 8: keep the half of bit3, send the other
+        const bool b = (lane >> 3) & 1;
+        const double keep = b ? y8[i + 4] : y8[i], send = b ? y8[i] : y8[i + 4];
+        y4[i] = keep + xor_lane(send, 8);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const bool b = (lane >> 2) & 1;
+        const double keep = b ? y4[i + 2] : y4[i], send = b ? y4[i] : y4[i + 2];
+        y2[i] = keep + xor_lane(send, 4);
+    }
+    const bool b = (lane >> 1) & 1;
+    const double keep = b ? y2[1] : y2[0], send = b ? y2[0] : y2[1];
+    const double y = keep + xor_lane(send, 2);
+    return y + xor_lane(y, 1);
+}
+
+// Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, Workgroup
+// dispatch): relabel them so that each XCD runs one contiguous range of the grid and its
+// L2 keeps the data neighbouring blocks share (bijective for any grid size).
+__device__ __forceinline__ int xcd_block(int b, int nb) {
+    const int q = nb >> 3, r = nb & 7, x = b & 7, i = b >> 3;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
+}
+
 }  // namespace se3icp
