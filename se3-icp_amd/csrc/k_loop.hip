@@ -67,35 +67,46 @@ __device__ __forceinline__ void recheck_one(const View& v, const PairDev* P, con
     if (bi < 0 || bi >= ct.n) bi = 0;
     double bd = dist(bi);
     const int first_leaf = (1 << TR.L) - 1;
-    int stk = 0, sp = 1;  // register stack: lane i holds entry i
-    while (sp > 0) {
-        const int h = __builtin_amdgcn_readlane(stk, sp - 1);
-        --sp;
-        if (h >= first_leaf) {
-            const int li = h - first_leaf;
-            const int ta = tree_first(ct.n, TR.L, li), tb = tree_first(ct.n, TR.L, li + 1);
-            double d = DBL_MAX;
-            int j = INT_MAX;
-            if (lane < tb - ta) {
-                j = TR.perm[ct.off + ta + lane];
-                d = dist(j);
-            }
+    // Lane-parallel box tests (64 nodes per instruction): the nodes of level A = L - 6
+    // (<= 64 leaves below each), then the leaves under each node that can still hold a
+    // point at or below the best distance (<=: a lower index may tie); open leaves are
+    // swept a point per lane.  Seeded with the f32 winner, few boxes stay open.
+    const int sh = TR.L > 6 ? 6 : TR.L;
+    const int A = TR.L - sh, nA = 1 << A, firstA = nA - 1;
+    for (int c0 = 0; c0 < nA; c0 += 64) {
+        const int ai = c0 + lane;
+        const double lbA = ai < nA ? lbound(firstA + ai) : DBL_MAX;
+        unsigned long long mA = __ballot(lbA <= bd);
+        while (mA) {
+            const int j = __builtin_ctzll(mA);
+            mA &= mA - 1ull;
+            if (!(__shfl(lbA, j, 64) <= bd)) continue;
+            const int l0 = (c0 + j) << sh;
+            const int li = l0 + lane;
+            const double lbL = lane < (1 << sh) ? lbound(first_leaf + li) : DBL_MAX;
+            unsigned long long mL = __ballot(lbL <= bd);
+            while (mL) {
+                const int t = __builtin_ctzll(mL);
+                mL &= mL - 1ull;
+                if (!(__shfl(lbL, t, 64) <= bd)) continue;
+                const int ta = tree_first(ct.n, TR.L, l0 + t), tb = tree_first(ct.n, TR.L, l0 + t + 1);
+                double d = DBL_MAX;
+                int jj = INT_MAX;
+                if (lane < tb - ta) {
+                    jj = TR.perm[ct.off + ta + lane];
+                    d = dist(jj);
+                }
 #pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) {
-                const double od = __shfl_xor(d, o, 64);
-                const int oj = __shfl_xor(j, o, 64);
-                if (key_less(od, oj, d, j)) { d = od; j = oj; }
+                for (int o = 32; o >= 1; o >>= 1) {
+                    const double od = xor_lane(d, o);
+                    const int oj = xor_lane(jj, o);
+                    const bool tk = (bool)((int)(od < d) | ((int)(od == d) & (int)(oj < jj)));
+                    d = tk ? od : d;
+                    jj = tk ? oj : jj;
+                }
+                if ((int)(d < bd) | ((int)(d == bd) & (int)(jj < bi))) { bd = d; bi = jj; }
             }
-            if (key_less(d, j, bd, bi)) { bd = d; bi = j; }
-            continue;
         }
-        const int hl = 2 * h + 1, hr = 2 * h + 2;
-        const double ll = lbound(hl), lr = lbound(hr);
-        const bool vl = ll <= bd, vr = lr <= bd;
-        const bool lf = ll <= lr;
-        const int nearh = lf ? hl : hr, farh = lf ? hr : hl;
-        if (lf ? vr : vl) { stk = (lane == sp) ? farh : stk; ++sp; }
-        if (lf ? vl : vr) { stk = (lane == sp) ? nearh : stk; ++sp; }
     }
     if (lane == 0) {
         v.corr_idx[g] = bi;
