@@ -76,6 +76,50 @@ __device__ __forceinline__ float dist12(const f32x2* q2, const float4* t) {
     return s2.x + s2.y;
 }
 
+// One leaf against its w wanting queries (list wl): LPQ lanes per query, targets
+// sub, sub+LPQ, sub+2LPQ, sub+3LPQ per lane (LPQ * 4 >= cnt), the group's top-2 into
+// r1/r2/rb[query].  The lane's 4 targets are loop-invariant over the queries: the
+// compiler keeps them in registers (4 waves/SIMD; measured faster than re-reading at 5).
+template <int LPQ>
+__device__ __forceinline__ void compact_sweep(const float4* tile, const float4* sq, const int* wl, float* r1, float* r2,
+                                              int* rb, int w, int cnt, int ta, int lane) {
+    constexpr int QPI = 64 / LPQ;  // queries per pass
+    const int sub = lane & (LPQ - 1);
+    for (int it = 0; it < w; it += QPI) {
+        const int slot = it + lane / LPQ;
+        const int qi = wl[slot < w ? slot : it];
+        const float4 QA = sq[qi * 3], QB = sq[qi * 3 + 1], QC = sq[qi * 3 + 2];
+        const f32x2 qq[6] = {f32x2{QA.x, QA.y}, f32x2{QA.z, QA.w}, f32x2{QB.x, QB.y},
+                             f32x2{QB.z, QB.w}, f32x2{QC.x, QC.y}, f32x2{QC.z, QC.w}};
+        float a1 = INFINITY, a2 = INFINITY;
+        int b1 = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = sub + LPQ * u;
+            float acc = dist12(qq, tile + 3 * (j < cnt ? j : 0));
+            acc = j < cnt ? acc : INFINITY;
+            const bool lt = acc < a1;
+            a2 = __builtin_amdgcn_fmed3f(a1, a2, acc);
+            a1 = lt ? acc : a1;
+            b1 = lt ? j : b1;
+        }
+#pragma unroll
+        for (int m = 1; m < LPQ; m <<= 1) {
+            const float p1 = xor_lane(a1, m), p2 = xor_lane(a2, m);
+            const int pb = xor_lane(b1, m);
+            const bool lt = (bool)((int)(p1 < a1) | ((int)(p1 == a1) & (int)(pb < b1)));
+            a2 = fminf(fmaxf(a1, p1), fminf(a2, p2));
+            b1 = lt ? pb : b1;
+            a1 = fminf(a1, p1);
+        }
+        if ((int)(sub == 0) & (int)(slot < w)) {
+            r1[qi] = a1;
+            r2[qi] = a2;
+            rb[qi] = ta + b1;
+        }
+    }
+}
+
 template <int D>
 __global__ __launch_bounds__(256) void k_nn_group(View v) {
     constexpr int NV = (D + 3) / 4;
@@ -206,48 +250,14 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
                 }
                 n_eval += cnt;
             } else if constexpr (D == 12) {
-                // compacted: 8 lanes per wanting query, 4 targets per lane, then a top-2
-                // merge over the 8 lanes and into the query's own lane
+                // compacted: LPQ lanes per wanting query (8 for leaves of <= 32 targets, 16
+                // up to 64), 4 targets per lane, then a top-2 merge over the LPQ lanes and
+                // into the query's own lane
                 if ((W >> lane) & 1ull)
                     s_wl[wid][__builtin_amdgcn_mbcnt_hi((unsigned)(W >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)W, 0u))] = lane;
                 __builtin_amdgcn_wave_barrier();
-                const int sub = lane & 7;
-                for (int it = 0; it < w; it += 8) {
-                    const int slot = it + (lane >> 3);
-                    const int qi = s_wl[wid][slot < w ? slot : it];
-                    const float4 QA = s_q[wid][qi * 3], QB = s_q[wid][qi * 3 + 1], QC = s_q[wid][qi * 3 + 2];
-                    const f32x2 qq[6] = {f32x2{QA.x, QA.y}, f32x2{QA.z, QA.w}, f32x2{QB.x, QB.y},
-                                         f32x2{QB.z, QB.w}, f32x2{QC.x, QC.y}, f32x2{QC.z, QC.w}};
-                    float a1 = INFINITY, a2 = INFINITY;
-                    int b1 = 0;
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        // (loop-invariant in `it`: the compiler keeps the lane's 4 targets in
-                        // registers across the wanting queries — 4 waves/SIMD, measured faster
-                        // than re-reading them at 5)
-                        const int j = sub + 8 * u;
-                        float acc = dist12(qq, tile + 3 * (j < cnt ? j : 0));
-                        acc = j < cnt ? acc : INFINITY;
-                        const bool lt = acc < a1;
-                        a2 = __builtin_amdgcn_fmed3f(a1, a2, acc);
-                        a1 = lt ? acc : a1;
-                        b1 = lt ? j : b1;
-                    }
-#pragma unroll
-                    for (int m = 1; m <= 4; m <<= 1) {
-                        const float p1 = xor_lane(a1, m), p2 = xor_lane(a2, m);
-                        const int pb = xor_lane(b1, m);
-                        const bool lt = (bool)((int)(p1 < a1) | ((int)(p1 == a1) & (int)(pb < b1)));
-                        a2 = fminf(fmaxf(a1, p1), fminf(a2, p2));
-                        b1 = lt ? pb : b1;
-                        a1 = fminf(a1, p1);
-                    }
-                    if ((int)(sub == 0) & (int)(slot < w)) {
-                        s_r1[wid][qi] = a1;
-                        s_r2[wid][qi] = a2;
-                        s_rb[wid][qi] = ta + b1;
-                    }
-                }
+                if (cnt <= 32) compact_sweep<8>(tile, s_q[wid], s_wl[wid], s_r1[wid], s_r2[wid], s_rb[wid], w, cnt, ta, lane);
+                else compact_sweep<16>(tile, s_q[wid], s_wl[wid], s_r1[wid], s_r2[wid], s_rb[wid], w, cnt, ta, lane);
                 __builtin_amdgcn_wave_barrier();
                 if ((W >> lane) & 1ull) {
                     const float r1 = s_r1[wid][lane], r2 = s_r2[wid][lane];
@@ -257,7 +267,7 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
                     d1 = fminf(d1, r1);
                 }
                 __builtin_amdgcn_wave_barrier();
-                n_eval += 4 * ((w + 7) >> 3);  // 64-lane evaluation slots issued
+                n_eval += 4 * ((w + (cnt <= 32 ? 7 : 3)) >> (cnt <= 32 ? 3 : 2));  // 64-lane evaluation slots issued
             }
             if ((int)valid & (int)(d1 < INFINITY)) thr = fminf(thr, d1 + 3.f * f32_err(d1, na, nb, D));
             continue;
