@@ -372,9 +372,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
             __builtin_amdgcn_wave_barrier();
         };
         auto leaf = [&](int h) __attribute__((always_inline)) {
-            const int i = h - first_leaf;
+            // (wave-uniform: readfirstlane keeps the leaf range arithmetic on the scalar unit)
+            const int i = __builtin_amdgcn_readfirstlane(h - first_leaf);
             ++n_leaves;
-            const int a = tree_first(n, T.L, i), b = tree_first(n, T.L, i + 1);
+            const int a = __builtin_amdgcn_readfirstlane(tree_first(n, T.L, i));
+            const int b = __builtin_amdgcn_readfirstlane(tree_first(n, T.L, i + 1));
             bool acc = false;
             double d = DBL_MAX;
             int li = INT_MAX;
