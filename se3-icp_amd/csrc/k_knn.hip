@@ -234,7 +234,9 @@ __device__ __forceinline__ float box_lb3(const float* lo, const float* hi, float
 
 // Per-query state parked in LDS between the kNN pass and the batched eigen-solves
 // (slots of s_park[wave][query]).
-enum ParkSlot { PK_C = 0, PK_NC = 6, PK_R = 12, PK_KK = 13, PK_GP = 14, PK_FLAGS = 15, PK_K = 16, PK_NTOP = 17, PK_N = 18 };
+// PK_SUM: the 21 neighbour sums of a query (see the sums pass), later its 6 TOLDI axis sums.
+enum ParkSlot { PK_SUM = 0, PK_R = 21, PK_KK = 22, PK_GP = 23, PK_FLAGS = 24, PK_K = 25, PK_NTOP = 26, PK_N = 27 };
+constexpr int kSums = 21;
 
 // The per-cloud records and node boxes are also passed as restrict-qualified arguments:
 // with no possible aliasing store the compiler can serve their wave-uniform reads from
@@ -526,77 +528,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         const int nTop = (int)pj[PK_NTOP];
         const int* nbl = (s_nbw + j * v.kmax);
 
-        // ------------------------------------------------------------ TOLDI sums (ISR.cpp:241-281)
+        // All sums of the query in one recursive-halving reduction (wave.hpp), 21 values:
+        //   [0..2]  S' = sum of v over ranks 1 .. rz-1   (v = p - q, local coordinates)
+        //   [3..5]  S  = sum of v over ranks 1 .. rz
+        //   [6..11] M  = sum of v v^T over ranks 1 .. rz (xx xy xz yy yz zz)
+        //   [12..20] Open3D cumulants of the raw coordinates over ranks 0 .. kn-1
+        // The TOLDI covariance about the quirk centroid (ISR.cpp:259-272) is assembled from
+        // S', S, M in the eigen pass; the reference sums the products sequentially, so
+        // both differ from it by rounding only.
+        double x[32];
+#pragma unroll
+        for (int i = 0; i < 32; ++i) x[i] = 0.0;
         if (flags & 1) {
             const int kk = min(st.k_lrf, nTop);
             const int rz = kk / 3;
-            double ax[2], ay[2], az[2];
-            int rk[2];
 #pragma unroll
             for (int u = 0; u < 2; ++u) {  // neighbour ranks lane+1 and lane+65 (k <= 128)
-                rk[u] = 1 + lane + 64 * u;
-                ax[u] = ay[u] = az[u] = 0.0;
-                if (rk[u] <= rz && rk[u] < kk) {
-                    const int q = nbl[rk[u]];
-                    ax[u] = X[q]; ay[u] = Y[q]; az[u] = Z[q];
+                const int rk = 1 + lane + 64 * u;
+                if ((int)(rk <= rz) & (int)(rk < kk)) {
+                    const int q = nbl[rk];
+                    const double vx = X[q] - qx, vy = Y[q] - qy, vz = Z[q] - qz;
+                    if (rk < rz) { x[0] += vx; x[1] += vy; x[2] += vz; }
+                    x[3] += vx; x[4] += vy; x[5] += vz;
+                    x[6] += vx * vx; x[7] += vx * vy; x[8] += vx * vz;
+                    x[9] += vy * vy; x[10] += vy * vz; x[11] += vz * vz;
                 }
             }
-            const int far = nbl[kk - 1];
-            const double fdx = qx - X[far], fdy = qy - Y[far], fdz = qz - Z[far];
-            const double computed_radius = sqrt(fdx * fdx + fdy * fdy + fdz * fdz);  // ISR.cpp:256
-            // ISR.cpp:259-265 centroid quirk: ranks 1 .. rz-1 divided by rz
-            double sx = 0, sy = 0, sz = 0;
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-                if (rk[u] < rz) { sx += ax[u]; sy += ay[u]; sz += az[u]; }
-            const double cx = wsum(sx) / (double)rz, cy = wsum(sy) / (double)rz, cz = wsum(sz) / (double)rz;
-            // ISR.cpp:268-272 covariance over ranks 1 .. rz
-            double c6[6] = {0, 0, 0, 0, 0, 0};
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-                if (rk[u] <= rz && rk[u] < kk) {
-                    const double ex = ax[u] - cx, ey = ay[u] - cy, ez = az[u] - cz;
-                    c6[0] += ex * ex; c6[1] += ex * ey; c6[2] += ex * ez;
-                    c6[3] += ey * ey; c6[4] += ey * ez; c6[5] += ez * ez;
-                }
-#pragma unroll
-            for (int i = 0; i < 6; ++i) c6[i] = wsum(c6[i]);
             if (lane == 0) {
-#pragma unroll
-                for (int i = 0; i < 6; ++i) pj[PK_C + i] = c6[i];
-                pj[PK_R] = computed_radius;
+                const int far = nbl[kk - 1];
+                const double fdx = qx - X[far], fdy = qy - Y[far], fdz = qz - Z[far];
+                pj[PK_R] = sqrt(fdx * fdx + fdy * fdy + fdz * fdz);  // ISR.cpp:256
                 pj[PK_KK] = (double)kk;
             }
         }
-
-        // ------------------------------------------------------------ normals covariance
-        // EstimateNormals (ISR.cpp:643, :43): Open3D cumulants over ranks 0 .. kn-1, self included
-        if (flags & 2) {
+        if (flags & 2) {  // EstimateNormals (ISR.cpp:643, :43): ranks 0 .. kn-1, self included
             const int kn = min(st.k_nrm, nTop);
-            double cu[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
             for (int r = lane; r < kn; r += 64) {
                 const int q = nbl[r];
-                const double x = X[q], y = Y[q], z = Z[q];
-                cu[0] += x; cu[1] += y; cu[2] += z;
-                cu[3] += x * x; cu[4] += x * y; cu[5] += x * z;
-                cu[6] += y * y; cu[7] += y * z; cu[8] += z * z;
-            }
-#pragma unroll
-            for (int i = 0; i < 9; ++i) cu[i] = wsum(cu[i]) / (double)kn;
-            double n6[6] = {1, 0, 0, 1, 0, 1};
-            if (kn >= 3) {
-                n6[0] = cu[3] - cu[0] * cu[0];
-                n6[1] = cu[4] - cu[0] * cu[1];
-                n6[2] = cu[5] - cu[0] * cu[2];
-                n6[3] = cu[6] - cu[1] * cu[1];
-                n6[4] = cu[7] - cu[1] * cu[2];
-                n6[5] = cu[8] - cu[2] * cu[2];
-            }
-            if (lane == 0) {
-#pragma unroll
-                for (int i = 0; i < 6; ++i) pj[PK_NC + i] = n6[i];
+                const double px = X[q], py = Y[q], pz = Z[q];
+                x[12] += px; x[13] += py; x[14] += pz;
+                x[15] += px * px; x[16] += px * py; x[17] += px * pz;
+                x[18] += py * py; x[19] += py * pz; x[20] += pz * pz;
             }
         }
+        const double sv = wave_sum32(x);
+        if ((int)((lane & 1) == 0) & (int)((lane >> 1) < kSums)) pj[PK_SUM + (lane >> 1)] = sv;
         __builtin_amdgcn_wave_barrier();
     }
     PROF_NOW(t_s1);
@@ -627,10 +603,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     const int my_flags = lane < kQ ? (int)pl[PK_FLAGS] : 0;
     const int my_gp = (int)pl[PK_GP];
     d3 zn{0, 0, 0};
-    if (my_flags & 1) zn = jacobi_smallest_evec(pl[PK_C], pl[PK_C + 1], pl[PK_C + 2], pl[PK_C + 3], pl[PK_C + 4], pl[PK_C + 5]);
+    if (my_flags & 1) {
+        // C = sum over ranks 1..rz of (v - cl)(v - cl)^T with the quirk centroid
+        // cl = c - q = (S' - q) / rz  (c = (ranks 1..rz-1 summed) / rz, ISR.cpp:259-265)
+        const int w = w0 + lane;
+        const double rz = (double)((int)pl[PK_KK] / 3);
+        const double q3[3] = {TX[w], TY[w], TZ[w]};
+        double cl[3], S[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            cl[a] = (pl[PK_SUM + a] - q3[a]) / rz;
+            S[a] = pl[PK_SUM + 3 + a];
+        }
+        const double* M = pl + PK_SUM + 6;
+        const int ia[6] = {0, 0, 0, 1, 1, 2}, ib[6] = {0, 1, 2, 1, 2, 2};
+        double c6[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            c6[k] = M[k] - S[ia[k]] * cl[ib[k]] - cl[ia[k]] * S[ib[k]] + rz * cl[ia[k]] * cl[ib[k]];
+        zn = jacobi_smallest_evec(c6[0], c6[1], c6[2], c6[3], c6[4], c6[5]);
+    }
     if (my_flags & 2) {
         const int c = v.cloud_of[w0 + lane];
-        d3 nm = fast_eigen3x3(pl[PK_NC], pl[PK_NC + 1], pl[PK_NC + 2], pl[PK_NC + 3], pl[PK_NC + 4], pl[PK_NC + 5]);
+        const int kn = min(v.setup[c].k_nrm, (int)pl[PK_NTOP]);
+        double n6[6] = {1, 0, 0, 1, 0, 1};
+        if (kn >= 3) {
+            double cu[9];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) cu[i] = pl[PK_SUM + 12 + i] / (double)kn;
+            n6[0] = cu[3] - cu[0] * cu[0];
+            n6[1] = cu[4] - cu[0] * cu[1];
+            n6[2] = cu[5] - cu[0] * cu[2];
+            n6[3] = cu[6] - cu[1] * cu[1];
+            n6[4] = cu[7] - cu[1] * cu[2];
+            n6[5] = cu[8] - cu[2] * cu[2];
+        }
+        d3 nm = fast_eigen3x3(n6[0], n6[1], n6[2], n6[3], n6[4], n6[5]);
         if (sqrt(dot3(nm, nm)) == 0.0) nm = d3{0, 0, 1};
         const int gp = my_gp;
         v.nrm64[gp] = nm.x;
@@ -645,9 +653,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     }
 
     // ---------------------------------------------------------------- TOLDI axes (ISR.cpp:286-306)
-    double acc3[3] = {0, 0, 0}, accs3[3] = {0, 0, 0};
+    __builtin_amdgcn_wave_barrier();  // (the eigen pass has read PK_SUM; the axis sums reuse it)
     for (int j = 0; j < kQ; ++j) {
-        const double* pj = park + j * PK_N;
+        double* pj = park + j * PK_N;
         if (!((int)pj[PK_FLAGS] & 1)) continue;
         const int w = w0 + j;
         const int c = v.cloud_of[w];
@@ -670,11 +678,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
             const double wgt = (rr * rr) * (an * an);
             s0 += wgt * vx; s1 += wgt * vy; s2 += wgt * vz;
         }
-        a0 = wsum(a0); a1 = wsum(a1); a2 = wsum(a2);
-        s0 = wsum(s0); s1 = wsum(s1); s2 = wsum(s2);
-        if (lane == j) {
-            acc3[0] = a0; acc3[1] = a1; acc3[2] = a2;
-            accs3[0] = s0; accs3[1] = s1; accs3[2] = s2;
+        const double x8[8] = {a0, a1, a2, s0, s1, s2, 0.0, 0.0};
+        const double sv = wave_sum_pow2<8>(x8);  // value lane >> 3
+        if ((int)((lane & 7) == 0) & (int)((lane >> 3) < 6)) pj[PK_SUM + (lane >> 3)] = sv;
+    }
+    __builtin_amdgcn_wave_barrier();
+    double acc3[3] = {0, 0, 0}, accs3[3] = {0, 0, 0};
+    if (my_flags & 1) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            acc3[a] = pl[PK_SUM + a];
+            accs3[a] = pl[PK_SUM + 3 + a];
         }
     }
     if (my_flags & 1) {

@@ -97,6 +97,43 @@ __device__ __forceinline__ double wave_sum32(const double (&x)[32]) {
     return y + xor_lane(y, 1);
 }
 
+// Sums of P (a power of two <= 32) values over the 64 lanes by recursive halving, the
+// largest lane strides first.  Returns the total of value (lane >> (6 - log2 P)) in
+// every lane.
+template <int P>
+__device__ __forceinline__ double wave_sum_pow2(const double (&x)[P]) {
+    static_assert(P >= 1 && P <= 32 && (P & (P - 1)) == 0, "P: power of two <= 32");
+    const int lane = threadIdx.x & 63;
+    if constexpr (P == 32) {
+        return wave_sum32(x);
+    } else {
+        double y[P];
+#pragma unroll
+        for (int i = 0; i < P; ++i) y[i] = x[i];
+        int n = P, m = 32;
+        // halving steps: stride m keeps the half of the values selected by lane bit m
+#pragma unroll
+        for (; n > 1; n >>= 1, m >>= 1) {
+#pragma unroll
+            for (int i = 0; i < n / 2; ++i) {
+                if (m == 32) {
+                    y[i] = swap_add32(y[i], y[i + n / 2]);
+                } else if (m == 16) {
+                    y[i] = swap_add16(y[i], y[i + n / 2]);
+                } else {
+                    const bool b = (lane & m) != 0;
+                    const double keep = b ? y[i + n / 2] : y[i], send = b ? y[i] : y[i + n / 2];
+                    y[i] = keep + xor_lane(send, m);
+                }
+            }
+        }
+        double r = y[0];
+#pragma unroll
+        for (; m >= 1; m >>= 1) r += xor_lane(r, m);
+        return r;
+    }
+}
+
 // Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, Workgroup
 // dispatch): relabel them so that each XCD runs one contiguous range of the grid and its
 // L2 keeps the data neighbouring blocks share (bijective for any grid size).
