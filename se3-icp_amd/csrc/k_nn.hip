@@ -27,6 +27,9 @@ using namespace loopdev;
 
 constexpr int kWaves = 4;
 // Leaves wanted by at most this many lanes take the compacted path (8 lanes per query)
+#ifndef SE3ICP_NN_COMPACT3
+#define SE3ICP_NN_COMPACT3 40  // R3 phase (0: broadcast sweeps only)
+#endif
 #ifndef SE3ICP_NN_COMPACT
 #define SE3ICP_NN_COMPACT 40
 #endif
@@ -80,23 +83,39 @@ __device__ __forceinline__ float dist12(const f32x2* q2, const float4* t) {
 // sub, sub+LPQ, sub+2LPQ, sub+3LPQ per lane (LPQ * 4 >= cnt), the group's top-2 into
 // r1/r2/rb[query].  The lane's 4 targets are loop-invariant over the queries: the
 // compiler keeps them in registers (4 waves/SIMD; measured faster than re-reading at 5).
-template <int LPQ>
+template <int D, int LPQ>
 __device__ __forceinline__ void compact_sweep(const float4* tile, const float4* sq, const int* wl, float* r1, float* r2,
                                               int* rb, int w, int cnt, int ta, int lane) {
+    constexpr int NV = (D + 3) / 4;
     constexpr int QPI = 64 / LPQ;  // queries per pass
     const int sub = lane & (LPQ - 1);
     for (int it = 0; it < w; it += QPI) {
         const int slot = it + lane / LPQ;
         const int qi = wl[slot < w ? slot : it];
-        const float4 QA = sq[qi * 3], QB = sq[qi * 3 + 1], QC = sq[qi * 3 + 2];
-        const f32x2 qq[6] = {f32x2{QA.x, QA.y}, f32x2{QA.z, QA.w}, f32x2{QB.x, QB.y},
-                             f32x2{QB.z, QB.w}, f32x2{QC.x, QC.y}, f32x2{QC.z, QC.w}};
+        f32x2 qq[6];
+        float4 Q3;
+        if constexpr (D == 12) {
+            const float4 QA = sq[qi * 3], QB = sq[qi * 3 + 1], QC = sq[qi * 3 + 2];
+            qq[0] = f32x2{QA.x, QA.y}; qq[1] = f32x2{QA.z, QA.w}; qq[2] = f32x2{QB.x, QB.y};
+            qq[3] = f32x2{QB.z, QB.w}; qq[4] = f32x2{QC.x, QC.y}; qq[5] = f32x2{QC.z, QC.w};
+        } else {
+            Q3 = sq[qi];
+        }
         float a1 = INFINITY, a2 = INFINITY;
         int b1 = 0;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int j = sub + LPQ * u;
-            float acc = dist12(qq, tile + 3 * (j < cnt ? j : 0));
+            float acc;
+            if constexpr (D == 12) {
+                acc = dist12(qq, tile + NV * (j < cnt ? j : 0));
+            } else {  // the broadcast sweep's arithmetic (f32_err bound)
+                const float4 A = tile[j < cnt ? j : 0];
+                float e;
+                e = Q3.x - A.x; acc = e * e;
+                e = Q3.y - A.y; acc = fmaf(e, e, acc);
+                e = Q3.z - A.z; acc = fmaf(e, e, acc);
+            }
             acc = j < cnt ? acc : INFINITY;
             const bool lt = acc < a1;
             a2 = __builtin_amdgcn_fmed3f(a1, a2, acc);
@@ -126,7 +145,7 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
     __shared__ float4 s_tile[kWaves][kLeafMax * NV];
     // compacted leaf sweeps (12-D): the wave's query vectors, the list of lanes that want
     // the current leaf, and the per-query top-2 of the leaf
-    __shared__ float4 s_q[D == 12 ? kWaves : 1][D == 12 ? 64 * 3 : 1];
+    __shared__ float4 s_q[kWaves][64 * NV];
     __shared__ int s_wl[kWaves][64];
     __shared__ float s_r1[kWaves][64], s_r2[kWaves][64];
     __shared__ int s_rb[kWaves][64];
@@ -171,6 +190,8 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
         s_q[wid][lane * 3 + 0] = make_float4(q[0], q[1], q[2], q[3]);
         s_q[wid][lane * 3 + 1] = make_float4(q[4], q[5], q[6], q[7]);
         s_q[wid][lane * 3 + 2] = make_float4(q[8], q[9], q[10], q[11]);
+    } else {
+        s_q[wid][lane] = make_float4(q[0], q[1], q[2], 0.f);
     }
 
     float d1 = INFINITY, d2 = INFINITY;
@@ -211,8 +232,10 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
             // lanes whose own bound admits this leaf (box re-tested: the bounds shrank since the push)
             unsigned long long W = ~0ull;
             int w = 64;
-            if constexpr (D == 12) {
-                const float lbh = box_lb12(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q2);
+            if (D == 12 || SE3ICP_NN_COMPACT3) {
+                float lbh;
+                if constexpr (D == 12) lbh = box_lb12(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q2);
+                else lbh = box_lb<D>(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q);
                 W = __ballot(lbh * (1.f - 2e-6f) < thr);
                 if (W == 0ull) continue;
                 w = __popcll(W);
@@ -230,7 +253,7 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
                 for (int k = 0; k < NV; ++k) tile[lane * NV + k] = make_float4(e[4 * k], e[4 * k + 1], e[4 * k + 2], e[4 * k + 3]);
             }
             __builtin_amdgcn_wave_barrier();
-            if (D != 12 || w > SE3ICP_NN_COMPACT) {
+            if (w > (D == 12 ? SE3ICP_NN_COMPACT : SE3ICP_NN_COMPACT3)) {
                 // every lane sweeps every target (broadcast LDS reads)
                 for (int j = 0; j < cnt; ++j) {
                     float acc;
@@ -249,15 +272,15 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
                     i1 = lt ? (ta + j) : i1;  // target tree position
                 }
                 n_eval += cnt;
-            } else if constexpr (D == 12) {
+            } else {
                 // compacted: LPQ lanes per wanting query (8 for leaves of <= 32 targets, 16
                 // up to 64), 4 targets per lane, then a top-2 merge over the LPQ lanes and
                 // into the query's own lane
                 if ((W >> lane) & 1ull)
                     s_wl[wid][__builtin_amdgcn_mbcnt_hi((unsigned)(W >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)W, 0u))] = lane;
                 __builtin_amdgcn_wave_barrier();
-                if (cnt <= 32) compact_sweep<8>(tile, s_q[wid], s_wl[wid], s_r1[wid], s_r2[wid], s_rb[wid], w, cnt, ta, lane);
-                else compact_sweep<16>(tile, s_q[wid], s_wl[wid], s_r1[wid], s_r2[wid], s_rb[wid], w, cnt, ta, lane);
+                if (cnt <= 32) compact_sweep<D, 8>(tile, s_q[wid], s_wl[wid], s_r1[wid], s_r2[wid], s_rb[wid], w, cnt, ta, lane);
+                else compact_sweep<D, 16>(tile, s_q[wid], s_wl[wid], s_r1[wid], s_r2[wid], s_rb[wid], w, cnt, ta, lane);
                 __builtin_amdgcn_wave_barrier();
                 if ((W >> lane) & 1ull) {
                     const float r1 = s_r1[wid][lane], r2 = s_r2[wid][lane];
