@@ -17,6 +17,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "tree.hpp"
+#include "wave.hpp"
 
 namespace se3icp {
 
@@ -150,6 +151,7 @@ __global__ __launch_bounds__(256) void k_tree_keys32(TreeView t, int level, int 
 // along the sub-node's widest dimension) keys -- the same median splits as the global
 // levels, without a device-wide radix sort per level.
 constexpr int kLocalMax = 4096;
+constexpr int kWaveSortPer = 8;  // sub-nodes of <= 512 points: register sort by one wave
 #ifndef SE3ICP_TREE_SPLIT
 #define SE3ICP_TREE_SPLIT 1
 #endif
@@ -168,8 +170,6 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
     const int tid = threadIdx.x;
     if (m <= 1) return;
     for (int e = tid; e < kLocalMax; e += kLocalThreads) s_val[e] = e < m ? t.perm[cl.off + A + e] : -1;
-    int np2 = 2;
-    while (np2 < m) np2 <<= 1;
     for (int l = G; l < t.L; ++l) {
         const int r = l - G;
         const int nsub = 1 << r;  // sub-nodes of this level under the WG's node (<= 128: see the host)
@@ -247,35 +247,69 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
             }
         }
         __syncthreads();
-        for (int e = tid; e < np2; e += kLocalThreads) {
-            unsigned long long key = ~0ull;
-            if (e < m) {
-                const int sub = tree_node_of(A + e, n, l) - (i << r);
-                const int p = s_val[e];
-                const float* row = t.vec + (size_t)s_best[sub] * t.ld;
-                const uint32_t u = ord_bits(row[cl.off + p]);
-                key = (unsigned long long)u | ((unsigned long long)(unsigned)sub << 32);
-            }
-            s_key[e] = key;
-        }
-        __syncthreads();
-        for (int kk = 2; kk <= np2; kk <<= 1) {
-            for (int jd = kk >> 1; jd > 0; jd >>= 1) {
-                for (int x = tid; x < (np2 >> 1); x += kLocalThreads) {
-                    const int a = ((x & ~(jd - 1)) << 1) | (x & (jd - 1));  // bit jd of a is clear
-                    const int b = a | jd;
-                    const unsigned long long ka = s_key[a], kb = s_key[b];
-                    const bool up = (a & kk) == 0;
-                    if ((ka > kb) == up) {
-                        s_key[a] = kb;
-                        s_key[b] = ka;
-                        const int va = s_val[a];
-                        s_val[a] = s_val[b];
-                        s_val[b] = va;
+        const int max_sub = (m + nsub - 1) / nsub + 1;  // sub-node sizes differ by <= 1
+        if (max_sub <= 64 * kWaveSortPer) {
+            // small sub-nodes: one wave sorts each in registers, (coordinate, point) keys
+            const int lane = tid & 63, wv = tid >> 6;
+            for (int k = wv; k < nsub; k += kLocalThreads / 64) {
+                const int a0 = tree_first(n, l, (i << r) + k) - A, a1 = tree_first(n, l, (i << r) + k + 1) - A;
+                const float* row = t.vec + (size_t)s_best[k] * t.ld + cl.off;
+                unsigned long long key[kWaveSortPer];
+#pragma unroll
+                for (int u = 0; u < kWaveSortPer; ++u) {
+                    const int e = a0 + lane * kWaveSortPer + u;
+                    key[u] = ~0ull;
+                    if (e < a1) {
+                        const int p = s_val[e];
+                        key[u] = ((unsigned long long)ord_bits(row[p]) << 32) | (unsigned)p;
                     }
                 }
-                __syncthreads();
+                wave_sort_keys<kWaveSortPer>(key);
+#pragma unroll
+                for (int u = 0; u < kWaveSortPer; ++u) {
+                    const int e = a0 + lane * kWaveSortPer + u;
+                    if (e < a1) s_val[e] = (int32_t)(unsigned)key[u];
+                }
             }
+            __syncthreads();
+            continue;
+        }
+        // large sub-nodes: block-wide bitonic sort of (sub-node, coordinate, element) keys
+        // (7 + 32 + 12 bits), 8 per thread in registers; only the 6 stages with partners
+        // in another wave go through LDS
+        {
+            constexpr int PER = kLocalMax / kLocalThreads;
+            unsigned long long k[PER];
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const int e = tid * PER + u;
+                k[u] = ~0ull;
+                if (e < m) {
+                    const int sub = tree_node_of(A + e, n, l) - (i << r);
+                    const float* row = t.vec + (size_t)s_best[sub] * t.ld;
+                    const uint32_t c = ord_bits(row[cl.off + s_val[e]]);
+                    k[u] = ((unsigned long long)(unsigned)sub << 44) | ((unsigned long long)c << 12) | (unsigned)e;
+                }
+            }
+            bitonic_net<PER, kLocalMax, 64 * PER>(k, tid, s_key);
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < PER; ++u) s_key[tid * PER + u] = k[u];
+            __syncthreads();
+            // gather the permutation through the element field
+            int nv[PER];
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const int e = tid * PER + u;
+                nv[u] = e < m ? s_val[(int)(s_key[e] & 0xfffu)] : 0;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const int e = tid * PER + u;
+                if (e < m) s_val[e] = nv[u];
+            }
+            __syncthreads();
         }
     }
     for (int e = tid; e < m; e += kLocalThreads) t.perm[cl.off + A + e] = s_val[e];

@@ -134,6 +134,60 @@ __device__ __forceinline__ double wave_sum_pow2(const double (&x)[P]) {
     }
 }
 
+// One compare-exchange stage (block KK, distance JD) of an ascending bitonic network
+// over distinct 64-bit keys (identical padding keys are interchangeable); entry
+// e = tid*PER + s sits in k[s] of thread tid.  Partners in the same thread swap in
+// registers, in the same wave through lane exchanges, in another wave through LDS
+// (s_key: NT*PER entries; XW: partner distance in entries from which that is needed).
+template <int PER, int KK, int JD, int XW>
+__device__ __forceinline__ void bitonic_stage(unsigned long long (&k)[PER], int tid, unsigned long long* s_key) {
+    if constexpr (JD < PER) {
+#pragma unroll
+        for (int s = 0; s < PER; ++s) {
+            if ((s & JD) == 0) {
+                const int t = s | JD;
+                const bool up = ((tid * PER + s) & KK) == 0;
+                const bool sw = (k[t] < k[s]) != !up;
+                const unsigned long long ks = k[s], kt = k[t];
+                k[s] = sw ? kt : ks;
+                k[t] = sw ? ks : kt;
+            }
+        }
+    } else if constexpr (JD < XW) {
+#pragma unroll
+        for (int s = 0; s < PER; ++s) {
+            const int e = tid * PER + s;
+            const unsigned long long pk = xor_lane(k[s], JD / PER);
+            const bool take = (pk < k[s]) != (((e & JD) == 0) != ((e & KK) == 0));
+            k[s] = take ? pk : k[s];
+        }
+    } else {
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < PER; ++s) s_key[tid * PER + s] = k[s];
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < PER; ++s) {
+            const int e = tid * PER + s;
+            const unsigned long long pk = s_key[e ^ JD];
+            const bool take = (pk < k[s]) != (((e & JD) == 0) != ((e & KK) == 0));
+            k[s] = take ? pk : k[s];
+        }
+    }
+}
+// the whole network over N entries, stage by stage at compile time
+template <int PER, int N, int XW, int KK = 2, int JD = 1>
+__device__ __forceinline__ void bitonic_net(unsigned long long (&k)[PER], int tid, unsigned long long* s_key) {
+    bitonic_stage<PER, KK, JD, XW>(k, tid, s_key);
+    if constexpr (JD > 1) bitonic_net<PER, N, XW, KK, JD / 2>(k, tid, s_key);
+    else if constexpr (KK < N) bitonic_net<PER, N, XW, KK * 2, KK>(k, tid, s_key);
+}
+// ascending register sort of the 64*PER keys of one wave
+template <int PER>
+__device__ __forceinline__ void wave_sort_keys(unsigned long long (&k)[PER]) {
+    bitonic_net<PER, 64 * PER, 64 * PER>(k, threadIdx.x & 63, nullptr);
+}
+
 // Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, Workgroup
 // dispatch): relabel them so that each XCD runs one contiguous range of the grid and its
 // L2 keeps the data neighbouring blocks share (bijective for any grid size).
