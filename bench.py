@@ -146,7 +146,8 @@ def main():
         rot_errs = [rot_err_deg(r.T, g) for r, g in zip(last, gts)]
         tr_errs = [float(np.linalg.norm(r.T[:3, 3] - g[:3, 3])) for r, g in zip(last, gts)]
         # dominant kernel + roofline (HIP events around every launch, on the engine's stream)
-        kms = {k: ktot.get(k, 0.0) for k in ["nn_se3_ms", "nn_r3_ms", "recheck_ms", "trim_ms", "reduce_ms", "lrf_ms"]}
+        kms = {k: ktot.get(k, 0.0) for k in ["nn_prep_ms", "nn_se3_ms", "nn_r3_ms", "recheck_ms", "trim_ms", "reduce_ms",
+                                            "lrf_ms"]}
         nq = max(1.0, ktot.get("lrf_queries", 0.0))
         lrf_work = {"queries_per_step": ktot.get("lrf_queries", 0.0) / args.steps,
                     "leaves_per_query": round(ktot.get("lrf_leaves", 0.0) / nq, 2),
@@ -195,6 +196,9 @@ def main():
             "kernel_ms_per_step": {k: round(v / args.steps, 3) for k, v in kms.items()},
             "lrf_work": lrf_work,
             "rechecked_queries_per_step": rechecked / args.steps,
+            # NN certificates (k_nn_prep): share of the loop's queries that still needed a search
+            "nn_searched_frac": {"se3": round(ktot.get("se3_searched", 0.0) / max(1.0, ktot.get("se3_queries", 0.0)), 4),
+                                 "r3": round(ktot.get("r3_searched", 0.0) / max(1.0, ktot.get("r3_queries", 0.0)), 4)},
             "phase_ms_per_step": {"setup": round(setup_ms / args.steps, 3), "loop": round(loop_ms / args.steps, 3)},
             "roofline": {
                 "kernel": kname,

@@ -165,11 +165,13 @@ int se3icp_nn(int device, const double* query, int64_t nq, const double* data, i
 /* ------------------------------------------------------------- diagnostics
  * Not part of the reference boundary: per-kernel GPU times (HIP events) of the
  * last batch on `device`, used by bench.py for the roofline figures.
- * out[18] = {nn_se3_ms, nn_r3_ms, recheck_ms, trim_ms, reduce_ms, setup_ms,
+ * out[23] = {nn_se3_ms, nn_r3_ms, recheck_ms, trim_ms, reduce_ms, setup_ms,
  *            nn_se3_launches, nn_r3_launches, se3_dist_evals, se3_box_tests,
  *            r3_dist_evals, r3_box_tests,   (evals/tests counted per lane)
  *            lrf_ms, lrf_queries, lrf_leaves, lrf_merges, lrf_box_tests,
- *            lrf_candidates}  (kNN/TOLDI/normals kernel) */
+ *            lrf_candidates,   (kNN/TOLDI/normals kernel)
+ *            nn_prep_ms, se3_queries, se3_searched, r3_queries, r3_searched}
+ *            (NN certificates: queries of all iterations / those searched) */
 int se3icp_set_profiling(int device, int on);
 int se3icp_last_kernel_times(int device, double* out);
 

@@ -273,7 +273,7 @@ int se3icp_set_profiling(int device, int on) {
     return 0;
 }
 
-int se3icp_last_kernel_times(int device, double* out /* [18] */) {
+int se3icp_last_kernel_times(int device, double* out /* [23] */) {
     Engine* e = usable_engine(device);
     if (!e || !out) return SE3ICP_ERR_NO_DEVICE;
     const auto& k = e->kernel_times();
@@ -295,6 +295,11 @@ int se3icp_last_kernel_times(int device, double* out /* [18] */) {
     out[15] = k.lrf_merges;
     out[16] = k.lrf_box_tests;
     out[17] = k.lrf_candidates;
+    out[18] = k.nn_prep_ms;
+    out[19] = k.se3_queries;
+    out[20] = k.se3_searched;
+    out[21] = k.r3_queries;
+    out[22] = k.r3_searched;
     return 0;
 }
 

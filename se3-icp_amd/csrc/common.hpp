@@ -21,6 +21,8 @@ constexpr int kMaxKnn = 128;      // SE3ICP_MAX_KNN
 constexpr int kBlock = 256;       // threads per block of the streaming/sweep kernels
 constexpr int kRedVals = 28;      // 21 JTJ upper + 6 JTr + 1 mse-sum (pt2pt reuses the slots)
 constexpr int kStatCols = 12;     // columns of the device work-counter table (View::stats); 8..11: SE3ICP_PROF section cycles
+constexpr int kHist = 256;        // pose history ring of the loop (View::hist), iterations
+constexpr int kChunkQ = 1024;     // source tree positions per NN work chunk (16 query groups)
 
 enum Phase : int32_t { PHASE_IDLE = 0, PHASE_SE3 = 1, PHASE_R3 = 2 };
 enum Estimator : int32_t { EST_PT2PT = 0, EST_PT2PL = 1, EST_GICP = 2 };
@@ -40,9 +42,11 @@ struct PairDev {
     int32_t cf;            // run_se3_icp_with_cf weighting / mse
     int32_t trim;          // 1 if ratio < 1 (threshold key valid)
     int32_t nkeep;         // floor(float(ratio) * float(ns))
-    int32_t _pad;
+    int32_t iter;          // 1-based iteration number (num_iterations_ after this iteration)
     float tgt_norm12;      // max |target 12-vector| (f32 sweep error bound)
     float tgt_norm3;       // max |centered target xyz| (f32 R3 error bound)
+    int32_t phase_start;   // first iteration of the current phase (older NN certificates are void)
+    int32_t _pad;
 };
 
 // Static work table: one entry per 256-query block of every pair.

@@ -83,6 +83,7 @@ int Engine::init() {
     HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     for (auto& e : ev_) HIPCHK(hipEventCreate(&e));
     if (const char* e = std::getenv("SE3ICP_L12_EXTRA")) l12_extra_ = std::max(0, std::min(2, std::atoi(e)));
+    if (const char* e = std::getenv("SE3ICP_NN_TRACE")) nn_trace_ = std::atoi(e) != 0;
     return 0;
 }
 
@@ -92,8 +93,9 @@ Engine::~Engine() {
     DevBuf* all[] = {&d_clouds_, &d_setup_, &d_pairs_, &d_cloud_of_, &d_inptr_, &d_in_, &d_xyz64_, &d_xyz32_,
                      &d_fr64_, &d_fr32_, &d_nrm64_, &d_cov64_, &d_conf64_, &d_knn_,
                      &d_corr_idx_, &d_corr_dist_, &d_flag_list_, &d_flag_count_, &d_trim_key_, &d_red_partial_,
-                     &d_red_out_, &d_work_, &d_gwork_, &d_wb_, &d_wn_, &d_chunks_, &d_partial_, &d_centers_,
+                     &d_red_out_, &d_work_, &d_wb_, &d_wn_, &d_chunks_, &d_partial_, &d_centers_,
                      &d_rechecked_, &d_keys0_, &d_keys1_, &d_vals1_, &d_sort_tmp_, &d_stats_,
+                     &d_qlist_, &d_qcount_, &d_hist_, &d_cert_d1_, &d_cert_l2_, &d_cert_it_, &d_margin_, &d_sqlist_,
                      &t3_.perm, &t3_.pos, &t3_.vec, &t3_.blo, &t3_.bhi, &t3_.lo, &t3_.hi,
                      &t12_.perm, &t12_.pos, &t12_.vec, &t12_.blo, &t12_.bhi, &t12_.lo, &t12_.hi};
     for (DevBuf* b : all)
@@ -102,6 +104,7 @@ Engine::~Engine() {
     if (h_red_) (void)hipHostFree(h_red_);
     if (h_partial_) (void)hipHostFree(h_partial_);
     if (h_rechecked_) (void)hipHostFree(h_rechecked_);
+    if (h_hist_) (void)hipHostFree(h_hist_);
     for (auto& e : ev_)
         if (e) (void)hipEventDestroy(e);
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -136,7 +139,9 @@ int Engine::alloc_points(int64_t ntot, int kmax, bool knn_list) {
               (!knn_list || ensure<int32_t>(d_knn_, L * kmax_)) && ensure<int32_t>(d_corr_idx_, L) && ensure<float>(d_corr_dist_, L) &&
               ensure<int32_t>(d_flag_list_, L) && ensure<int32_t>(d_flag_count_, 4) &&
               ensure<unsigned long long>(d_keys0_, L) && ensure<unsigned long long>(d_keys1_, L) &&
-              ensure<int32_t>(d_vals1_, L) && ensure<unsigned long long>(d_stats_, kStatCols * kStatSlots);
+              ensure<int32_t>(d_vals1_, L) && ensure<unsigned long long>(d_stats_, kStatCols * kStatSlots) &&
+              ensure<float>(d_cert_d1_, L) && ensure<float>(d_cert_l2_, L) && ensure<int32_t>(d_cert_it_, L) &&
+              ensure<float>(d_margin_, L) && ensure<int32_t>(d_sqlist_, L);
     for (TreeBufs* t : {&t3_, &t12_})
         ok = ok && ensure<int32_t>(t->perm, L) && ensure<int32_t>(t->pos, L);
     ok = ok && ensure<float>(t3_.vec, 3 * L) && ensure<float>(t12_.vec, 12 * L);
@@ -189,8 +194,16 @@ View Engine::view() const {
     };
     v.t3 = ref(t3_);
     v.t12 = ref(t12_);
-    v.gwork = (const GroupWork*)d_gwork_.p;
-    v.ngwork = ngwork_;
+    v.chunk_level = chunk_level_;
+    v.nchunks = nchunks_;
+    v.qlist = (int32_t*)d_qlist_.p;
+    v.qcount = (int32_t*)d_qcount_.p;
+    v.sq_list = (int32_t*)d_sqlist_.p;
+    v.hist = (const double*)d_hist_.p;
+    v.cert_d1 = (float*)d_cert_d1_.p;
+    v.cert_l2 = (float*)d_cert_l2_.p;
+    v.cert_it = (int32_t*)d_cert_it_.p;
+    v.nn_margin = (float*)d_margin_.p;
     return v;
 }
 
@@ -225,6 +238,7 @@ int Engine::build_tree(int D, const float* vec, hipStream_t s, const double* vec
     t.tvec = (float*)tb.vec.p;
     t.vec64 = vec64;
     t.tvec64 = vec64 ? (double*)tb.vec64.p : nullptr;
+    t.vec64_sources_only = D == 12;  // the loop reads f64 12-D vectors of source clouds (even ids) only
     t.blo = (uint32_t*)tb.blo.p;
     t.bhi = (uint32_t*)tb.bhi.p;
     t.lo = (float*)tb.lo.p;
@@ -390,9 +404,22 @@ int Engine::setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool nor
     // 5) 12-D kd-trees over the alpha/beta-weighted SE(3) elements
     have12_ = build12;
     if (build12) {
-        rc = build_tree(12, (const float*)d_fr32_.p, s);
+        rc = build_tree(12, (const float*)d_fr32_.p, s, (const double*)d_fr64_.p);  // f64 source elements in tree order
         if (rc) return rc;
     }
+    return 0;
+}
+
+// loop NN work chunks: nodes of level tree_L_ - 4 of every source tree (<= kChunkQ
+// positions each), their query lists, the pose history and void NN certificates
+int Engine::setup_chunks(int npairs, hipStream_t s) {
+    chunk_level_ = std::max(0, tree_L_ - 4);
+    nchunks_ = npairs << chunk_level_;
+    if (!ensure<int32_t>(d_qlist_, (size_t)nchunks_ * kChunkQ) || !ensure<int32_t>(d_qcount_, (size_t)nchunks_ * (kChunkQ / 64)) ||
+        !ensure<double>(d_hist_, (size_t)kHist * npairs * 12))
+        return SE3ICP_ERR_OUT_OF_MEMORY;
+    if (pinned(h_hist_, h_hist_cap_, (size_t)npairs * 12)) return SE3ICP_ERR_OUT_OF_MEMORY;
+    HIPCHK(hipMemsetAsync(d_cert_it_.p, 0xff, sizeof(int32_t) * ld_, s));
     return 0;
 }
 
@@ -473,15 +500,11 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     std::vector<double> centers, scales;
     rc = setup_clouds(clouds, on_device, se3, prm.scale_preprocessing, se3, &centers, &scales, s);
     if (rc) return rc;
-    // loop NN work: one wavefront per leaf of every source tree
-    h_gwork_.clear();
-    for (int p = 0; p < npairs; ++p)
-        for (int l = 0; l < (1 << tree_L_); ++l) h_gwork_.push_back(GroupWork{p, l});
-    ngwork_ = (int)h_gwork_.size();
-    if (!ensure<GroupWork>(d_gwork_, ngwork_)) return SE3ICP_ERR_OUT_OF_MEMORY;
-    HIPCHK(hipMemcpyAsync(d_gwork_.p, h_gwork_.data(), sizeof(GroupWork) * ngwork_, hipMemcpyHostToDevice, s));
+    rc = setup_chunks(npairs, s);
+    if (rc) return rc;
     HIPCHK(hipMemsetAsync(d_corr_idx_.p, 0xff, sizeof(int32_t) * ld_, s));  // no previous match yet
     HIPCHK(hipMemsetAsync(d_stats_.p, 0, sizeof(unsigned long long) * kStatCols * kStatSlots, s));
+    for (double& t : trace_prev_) t = 0;
     // norm bounds of the target search vectors (f32 error certificate) from the root boxes
     std::vector<float> n12, n3;
     rc = root_norms(t3_, 3, &n3, s);
@@ -499,6 +522,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         double sf = 1.0;
         int nkeep = 0;
         bool trim = false;
+        int phase = PHASE_IDLE, phase_start = 1;
     };
     std::vector<St> st(npairs);
     const float ratio = std::min(1.0f, std::max(0.0f, (float)prm.estimated_overlap));  // PCL setOverlapRatio(float)
@@ -525,6 +549,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     int active = npairs;
     while (active > 0) {
         bool any_se3 = false, any_r3 = false, any_trim = false;
+        int hist_row = 0;
         for (int p = 0; p < npairs; ++p) {
             PairDev& P = h_pairs_[p];
             St& S = st[p];
@@ -533,15 +558,27 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
             const bool se3_nn = (mi.kind == KIND_PURE) || (se3 && !S.sw);
             if (se3_nn) S.pure++;                                     // ISR.cpp:660
             P.phase = se3_nn ? PHASE_SE3 : PHASE_R3;
+            if (P.phase != S.phase) {  // NN certificates of the other metric are void
+                S.phase = P.phase;
+                S.phase_start = S.iter;
+            }
+            P.iter = S.iter;
+            P.phase_start = S.phase_start;
             for (int r = 0; r < 3; ++r)
                 for (int c = 0; c < 4; ++c) P.T[r * 4 + c] = S.T.m[r][c];
+            std::memcpy(h_hist_ + 12 * (size_t)p, P.T, sizeof(P.T));
+            hist_row = S.iter;  // equal for every active pair (lockstep)
             any_se3 |= se3_nn;
             any_r3 |= !se3_nn;
             any_trim |= S.trim;
         }
         HIPCHK(hipMemcpyAsync(d_pairs_.p, h_pairs_, sizeof(PairDev) * npairs, hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemsetAsync(d_flag_count_.p, 0, sizeof(int32_t), s));
+        HIPCHK(hipMemcpyAsync((double*)d_hist_.p + (size_t)(hist_row % kHist) * npairs * 12, h_hist_,
+                              sizeof(double) * 12 * npairs, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemsetAsync(d_flag_count_.p, 0, 3 * sizeof(int32_t), s));
         HIPCHK(hipEventRecord(ev_[0], s));
+        launch_nn_prep(v, s);
+        HIPCHK(hipEventRecord(ev_[8], s));
         if (any_se3) launch_nn_se3(v, s);
         HIPCHK(hipEventRecord(ev_[1], s));
         if (any_r3) launch_nn_r3(v, s);
@@ -558,12 +595,30 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         {
             float ms[5];
             for (int k = 0; k < 5; ++k) HIPCHK(hipEventElapsedTime(&ms[k], ev_[k], ev_[k + 1]));
+            float prep_ms = 0;
+            HIPCHK(hipEventElapsedTime(&prep_ms, ev_[0], ev_[8]));
+            ms[0] -= prep_ms;
+            ktimes_.nn_prep_ms += prep_ms;
             ktimes_.nn_se3_ms += ms[0];
             ktimes_.nn_r3_ms += ms[1];
             ktimes_.recheck_ms += ms[2];
             ktimes_.trim_ms += ms[3];
             ktimes_.reduce_ms += ms[4];
-            nn_ms += ms[0] + ms[1] + ms[2];
+            nn_ms += prep_ms + ms[0] + ms[1] + ms[2];
+            if (nn_trace_) {  // per-iteration NN work (diagnostics): diffs of the device counters
+                unsigned long long stats[kStatCols * kStatSlots];
+                HIPCHK(hipMemcpy(stats, d_stats_.p, sizeof(stats), hipMemcpyDeviceToHost));
+                double sum[kStatCols] = {};
+                for (int i = 0; i < kStatSlots; ++i)
+                    for (int k = 0; k < kStatCols; ++k) sum[k] += (double)stats[kStatCols * i + k];
+                std::fprintf(stderr,
+                             "[nn] iter %d: se3 %.0f/%.0f searched, evals %.3g boxes %.3g | r3 %.0f/%.0f, evals %.3g "
+                             "boxes %.3g | prep %.3f nn12 %.3f nn3 %.3f recheck %.3f ms\n",
+                             hist_row, sum[5] - trace_prev_[5], sum[4] - trace_prev_[4], sum[0] - trace_prev_[0],
+                             sum[1] - trace_prev_[1], sum[7] - trace_prev_[7], sum[6] - trace_prev_[6],
+                             sum[2] - trace_prev_[2], sum[3] - trace_prev_[3], prep_ms, ms[0], ms[1], ms[2]);
+                for (int k = 0; k < kStatCols; ++k) trace_prev_[k] = sum[k];
+            }
             if (any_se3) ktimes_.nn_se3_launches++;
             if (any_r3) ktimes_.nn_r3_launches++;
         }
@@ -610,6 +665,10 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         ktimes_.se3_box_tests = sum[1];
         ktimes_.r3_dist_evals = sum[2];
         ktimes_.r3_box_tests = sum[3];
+        ktimes_.se3_queries = sum[4];
+        ktimes_.se3_searched = sum[5];
+        ktimes_.r3_queries = sum[6];
+        ktimes_.r3_searched = sum[7];
 #ifdef SE3ICP_PROF
         std::fprintf(stderr, "[prof] nn12: leaf visits %.0f, lanes wanting a visited leaf %.1f%% of valid lanes\n",
                      sum[9], 100.0 * sum[8] / std::max(1.0, sum[10]));
@@ -786,27 +845,27 @@ int Engine::nn(const double* query, int64_t nq, const double* data, int64_t nd, 
     HIPCHK(hipMemcpyAsync(dst32, m32.data(), sizeof(float) * m32.size(), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(d_cloud_of_.p, cof.data(), sizeof(int32_t) * L, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(d_clouds_.p, h_clouds_.data(), sizeof(CloudDev) * 2, hipMemcpyHostToDevice, s));
-    rc = build_tree(dim, dst32, s);
+    rc = build_tree(dim, dst32, s, dst64);
     if (rc) return rc;
-    h_gwork_.clear();
-    for (int l = 0; l < (1 << tree_L_); ++l) h_gwork_.push_back(GroupWork{0, l});
-    ngwork_ = (int)h_gwork_.size();
-    if (!ensure<GroupWork>(d_gwork_, ngwork_)) return SE3ICP_ERR_OUT_OF_MEMORY;
-    HIPCHK(hipMemcpyAsync(d_gwork_.p, h_gwork_.data(), sizeof(GroupWork) * ngwork_, hipMemcpyHostToDevice, s));
+    rc = setup_chunks(1, s);
+    if (rc) return rc;
     PairDev P;
     std::memset(&P, 0, sizeof(P));
     P.T[0] = P.T[5] = P.T[10] = 1.0;
     P.src = 0;
     P.tgt = 1;
     P.phase = dim == 12 ? PHASE_SE3 : PHASE_R3;
+    P.iter = 1;
+    P.phase_start = 1;
     P.tgt_norm12 = (float)(nb * (1 + 1e-6));
     P.tgt_norm3 = (float)(nb * (1 + 1e-6));
     for (int a = 0; a < 3; ++a) P.f32_center[a] = cen[a];
     HIPCHK(hipMemcpyAsync(d_pairs_.p, &P, sizeof(P), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemsetAsync(d_flag_count_.p, 0, sizeof(int32_t), s));
+    HIPCHK(hipMemsetAsync(d_flag_count_.p, 0, 3 * sizeof(int32_t), s));
     HIPCHK(hipMemsetAsync(d_rechecked_.p, 0, sizeof(int32_t), s));
     HIPCHK(hipMemsetAsync(d_corr_idx_.p, 0xff, sizeof(int32_t) * L, s));
     View v = view();
+    launch_nn_prep(v, s);
     if (dim == 12) launch_nn_se3(v, s);
     else launch_nn_r3(v, s);
     launch_recheck(v, 512, s);

@@ -33,6 +33,9 @@ struct KernelTimes {
     double se3_dist_evals = 0, se3_box_tests = 0, r3_dist_evals = 0, r3_box_tests = 0;
     // fused kNN/TOLDI/normals kernel of the setup: time, queries, leaves scanned, sorts
     double lrf_ms = 0, lrf_queries = 0, lrf_leaves = 0, lrf_merges = 0, lrf_box_tests = 0, lrf_candidates = 0;
+    // NN certificates (k_nn_prep): its time, and per phase the queries of all iterations
+    // and those that had to be searched
+    double nn_prep_ms = 0, se3_queries = 0, se3_searched = 0, r3_queries = 0, r3_searched = 0;
 };
 
 class Engine {
@@ -80,6 +83,7 @@ class Engine {
     // together with the reference's preprocessing and scale[p] receives the factor.
     int setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool normalize_pairs, double scale_pre,
                      bool build12, std::vector<double>* centers, std::vector<double>* scales, hipStream_t s);
+    int setup_chunks(int npairs, hipStream_t s);
     View view() const;
 
     int dev_;
@@ -92,13 +96,15 @@ class Engine {
     // geometry of the current batch
     int nclouds_ = 0, npairs_ = 0;
     int64_t ntot_ = 0;
-    int ld_ = 0, kmax_ = 1, nwork_ = 0, ngwork_ = 0, tree_L_ = 0;
+    int ld_ = 0, kmax_ = 1, nwork_ = 0, tree_L_ = 0;
+    int chunk_level_ = 0, nchunks_ = 0;  // loop NN work chunks (View::chunk_level)
     bool have12_ = false, knn_list_ = false;
+    bool nn_trace_ = false;              // SE3ICP_NN_TRACE=1: per-iteration NN work on stderr
+    double trace_prev_[kStatCols] = {};
     int l12_extra_ = 0;  // extra levels of the 12-D trees (0: leaves of <= 64 targets, measured fastest with compacted sweeps)
     std::vector<CloudDev> h_clouds_;
     std::vector<CloudSetup> h_setup_;
     std::vector<BlockWork> h_work_;
-    std::vector<GroupWork> h_gwork_;
     std::vector<int32_t> h_wb_, h_wn_;
     std::vector<ChunkWork> h_chunks_;
     std::vector<const double*> h_inptr_;
@@ -106,15 +112,17 @@ class Engine {
     // device buffers
     DevBuf d_clouds_, d_setup_, d_pairs_, d_cloud_of_, d_inptr_, d_in_, d_xyz64_, d_xyz32_, d_fr64_, d_fr32_, d_nrm64_,
         d_cov64_, d_conf64_, d_knn_, d_corr_idx_, d_corr_dist_, d_flag_list_, d_flag_count_,
-        d_trim_key_, d_red_partial_, d_red_out_, d_work_, d_gwork_, d_wb_, d_wn_, d_chunks_, d_partial_, d_centers_,
-        d_rechecked_, d_keys0_, d_keys1_, d_vals1_, d_sort_tmp_, d_stats_;
+        d_trim_key_, d_red_partial_, d_red_out_, d_work_, d_wb_, d_wn_, d_chunks_, d_partial_, d_centers_,
+        d_rechecked_, d_keys0_, d_keys1_, d_vals1_, d_sort_tmp_, d_stats_, d_qlist_, d_qcount_, d_hist_, d_cert_d1_,
+        d_cert_l2_, d_cert_it_, d_margin_, d_sqlist_;
     TreeBufs t3_, t12_;
     // pinned host mirrors
     PairDev* h_pairs_ = nullptr;
     double* h_red_ = nullptr;
     double* h_partial_ = nullptr;
     int32_t* h_rechecked_ = nullptr;
-    size_t h_pairs_cap_ = 0, h_red_cap_ = 0, h_partial_cap_ = 0, h_rechecked_cap_ = 0;
+    double* h_hist_ = nullptr;  // one pose-history row (npairs x 12)
+    size_t h_pairs_cap_ = 0, h_red_cap_ = 0, h_partial_cap_ = 0, h_rechecked_cap_ = 0, h_hist_cap_ = 0;
     hipEvent_t ev_[16];
 };
 

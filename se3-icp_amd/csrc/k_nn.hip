@@ -4,14 +4,26 @@
 //                (12-D L2), update_correspondences_raw_flann_SE3 ISR.cpp:444-470;
 //   R3 phase:    exact 3-D 1-NN, update_correspondences_kd_tree_XYZ ISR.cpp:402-416.
 //
-// One wavefront = one leaf (<= 64 points) of the SOURCE kd-tree, i.e. 64 queries close
-// together in the search space (the pose acts on the 12-D/3-D vectors as an isometry, so
-// a leaf stays compact as the source moves).  The wave walks the TARGET kd-tree depth
-// first; a node is entered when some lane's f32 box bound is below that lane's pruning
-// threshold, and a leaf's <= 64 targets are staged through LDS and swept with broadcast
-// ds_read_b128 while each lane keeps (d1, i1, d2).  The previous iteration's match seeds
-// the threshold.  The f32 arg-min is then certified (k_loop.hip recheck handles the rest):
-//   thr = d1 + 3 err(d1)  => every unvisited target is > 2 err farther than the winner,
+// Certificates (k_nn_prep).  A search leaves each query a certificate: the exact distance
+// to its match is <= D1 and to every other target >= L2.  The query moves with the pose
+// only (q = T M0), so at a later iteration of the same phase, with delta = |q_now - q_then|
+// computed in f64 from the two poses, D1 + delta < L2 - delta proves the match unchanged
+// (triangle inequality) and the query is settled without a search.  As ICP converges the
+// per-iteration displacement shrinks geometrically and most queries settle this way.
+// To make certificates useful the search widens its radius to the smaller of
+// (sqrt(d1) + 2m)^2 and the second-best distance d2, m = the query's displacement in
+// this iteration (so the extra work is at most that of an exact 2-NN search).
+//
+// Search (k_nn_group).  The queries k_nn_prep could not settle are compacted per chunk
+// (<= 1024 consecutive source tree positions, i.e. close together in the search space;
+// the pose acts on the vectors as an isometry, so they stay close as the source moves)
+// and swept 64 per wavefront.  The wave walks the TARGET kd-tree depth first; a node is
+// entered when some lane's f32 box bound is below that lane's pruning threshold, and a
+// leaf's <= 64 targets are staged through LDS and swept with broadcast ds_read_b128 (or
+// by compacted lane groups) while each lane keeps (d1, i1, d2).  The previous
+// iteration's match seeds the threshold.  The f32 arg-min is then certified
+// (k_loop.hip recheck handles the rest):
+//   thr >= d1 + 3 err(d1)  => every unvisited target is > 2 err farther than the winner,
 //   and among the visited ones the gap d2 - d1 must exceed 2 err(d2).
 #include <hip/hip_runtime.h>
 
@@ -139,6 +151,212 @@ __device__ __forceinline__ void compact_sweep(const float4* tile, const float4* 
     }
 }
 
+// chunks with at least this many searched queries use k_nn_group, sparser ones k_nn_single
+// (measured: a 12-D wave-per-query search costs ~5x the lanes' share of a group's, a 3-D
+// one far more, but a group's latency bounds an iteration with few groups)
+#ifndef SE3ICP_NN_DENSE
+#define SE3ICP_NN_DENSE 128
+#endif
+#ifndef SE3ICP_NN_DENSE3
+#define SE3ICP_NN_DENSE3 256
+#endif
+#ifndef SE3ICP_NN_EXPAND
+#define SE3ICP_NN_EXPAND 1.0  // search widening, in units of the query's displacement this iteration
+#endif
+
+template <int D>
+__device__ __forceinline__ double dist_f64(const double* a, const double* b) {
+    double s = 0.0;
+#pragma unroll
+    for (int r = 0; r < D; ++r) s += (a[r] - b[r]) * (a[r] - b[r]);
+    return sqrt(s);
+}
+template <int D>
+__device__ __forceinline__ double norm_f64(const double* a) {
+    double s = 0.0;
+#pragma unroll
+    for (int r = 0; r < D; ++r) s += a[r] * a[r];
+    return sqrt(s);
+}
+__device__ __forceinline__ void load_hist(const View& v, int iter, int pair, double* T) {
+    const double* h = v.hist + ((size_t)(iter % kHist) * v.npairs + pair) * 12;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) T[i] = h[i];
+}
+
+// f64 source element / point at global tree slot gx (the tree-ordered f64 copy: queries of
+// a chunk read contiguous memory)
+template <int D>
+__device__ __forceinline__ void load_m0(const View& v, const TreeRef& TR, int gx, double* m) {
+#pragma unroll
+    for (int r = 0; r < D; ++r) m[r] = TR.tvec64[(size_t)r * v.ld + gx];
+}
+template <int D>
+__device__ __forceinline__ void pose_m0(const double* T, const double* m, double* q) {
+    if constexpr (D == 12) pose_frame(T, m, q);
+    else pose_point(T, m[0], m[1], m[2], q);
+}
+
+// Settle the query at source tree slot gx (point g) from its certificate (true: corr_idx
+// stays, corr_dist refreshed for the moved query) or prepare its search (false: nn_margin).
+template <int D>
+__device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, const PairDev* P, int pair,
+                                            const CloudDev& ct, int gx, int g) {
+    double m0[D], T[12], Q[D];
+    load_m0<D>(v, TR, gx, m0);
+    load_T(P, T);
+    pose_m0<D>(T, m0, Q);
+    const int it = P->iter;
+    const int ci = v.cert_it[g];
+    const double qn = norm_f64<D>(Q);
+    if ((int)(ci >= P->phase_start) & (int)(ci < it) & (int)(it - ci < kHist)) {
+        double Tr[12], Qr[D];
+        load_hist(v, ci, pair, Tr);
+        pose_m0<D>(Tr, m0, Qr);
+        // |q_now - q_then|, padded for the rounding of the two f64 queries
+        const double dl = dist_f64<D>(Q, Qr) * (1.0 + 1e-12) + 4e-16 * (qn + norm_f64<D>(Qr));
+        const double a = (double)v.cert_l2[g] - dl, b = (double)v.cert_d1[g] + dl;
+        // margin for the f64 rounding of the reference's own squared distances (|q| + |target| <= M)
+        const double M = 2.0 * qn + b;
+        if ((int)(a > b) & (int)((a - b) * (a + b) > 1e-14 * M * M)) {
+            const int j = v.corr_idx[g];
+            if constexpr (D == 12) {
+                v.corr_dist[g] = stored_dist(v, PHASE_SE3, ct, Q, j);
+            } else {
+                double Q12[12];
+                Q12[0] = Q[0]; Q12[1] = Q[1]; Q12[2] = Q[2];
+                v.corr_dist[g] = stored_dist(v, PHASE_R3, ct, Q12, j);
+            }
+            return true;
+        }
+    }
+    float m = 0.f;
+    if (it >= 2) {
+        double Tp[12], Qp[D];
+        load_hist(v, it - 1, pair, Tp);
+        pose_m0<D>(Tp, m0, Qp);
+        m = (float)(SE3ICP_NN_EXPAND * dist_f64<D>(Q, Qp));
+    }
+    v.nn_margin[g] = m;
+    return false;
+}
+
+// One 1024-thread block per chunk (a node of level CL = GL - 4 of the source tree: 16
+// query leaves of level GL).  Settles what the certificates allow and packs the rest
+// for k_nn_group: consecutive leaves' remaining queries share a 64-lane group as long as
+// they fit, a leaf is never split (with every query searched, a group is one leaf).
+// qlist[c][j][lane] = local tree position, qcount[c][j] = lanes of group j.
+__global__ __launch_bounds__(1024) void k_nn_prep(View v) {
+    constexpr int NL = kChunkQ / 64;  // leaves (groups) per chunk
+    __shared__ int s_cnt[NL], s_slot[NL], s_base[NL], s_wc[NL], s_single;
+    const int c = blockIdx.x;
+    const int pair = c >> v.chunk_level;
+    const PairDev* P = v.pairs + pair;
+    const int phase = P->phase;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (threadIdx.x < NL) s_cnt[threadIdx.x] = 0;
+    __syncthreads();
+    bool active = false;
+    int x = 0, l = 0;
+    if (phase != PHASE_IDLE) {
+        const CloudDev cs = v.clouds[P->src], ct = v.clouds[P->tgt];
+        const TreeRef TR = (phase == PHASE_SE3) ? v.t12 : v.t3;
+        const int ci = c & ((1 << v.chunk_level) - 1);
+        const int a = tree_first(cs.n, v.chunk_level, ci), b = tree_first(cs.n, v.chunk_level, ci + 1);
+        x = a + (int)threadIdx.x;
+        if (x < b) {
+            const int gx = cs.off + x, g = cs.off + TR.perm[gx];
+            active = (phase == PHASE_SE3) ? !prep_settle<12>(v, TR, P, pair, ct, gx, g)
+                                          : !prep_settle<3>(v, TR, P, pair, ct, gx, g);
+            l = tree_node_of(x, cs.n, TR.GL) - (ci << (TR.GL - v.chunk_level));
+            if (active) atomicAdd(&s_cnt[l], 1);
+        }
+    }
+    const unsigned long long m = __ballot(active);
+    if (lane == 0) s_wc[wid] = __popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {  // greedy packing of whole leaves into groups of <= 64
+        int cur = 0, grp = 0, base = 0, total = 0;
+        int gcnt[NL];
+#pragma unroll
+        for (int j = 0; j < NL; ++j) gcnt[j] = 0;
+        for (int j = 0; j < NL; ++j) {
+            const int n = s_cnt[j];
+            if (cur + n > 64) { ++grp; cur = 0; }
+            s_slot[j] = 64 * grp + cur;
+            s_base[j] = base;
+            gcnt[grp] += n;
+            cur += n;
+            base += n;
+        }
+        total = base;
+        // a sparse chunk goes to the one-query-per-wave kernel instead (SE(3) list from the
+        // front of sq_list, R3 from the back)
+        const bool dense = total >= (phase == PHASE_SE3 ? SE3ICP_NN_DENSE : SE3ICP_NN_DENSE3);
+        s_single = -1;
+        if ((int)!dense & (int)(total > 0)) s_single = atomicAdd(&v.flag_count[phase == PHASE_SE3 ? 1 : 2], total);
+        for (int j = 0; j < NL; ++j) v.qcount[c * NL + j] = dense ? gcnt[j] : 0;
+        if (phase != PHASE_IDLE) {  // work counters: queries / searched queries per phase
+            unsigned long long* st = v.stats + kStatCols * (c & 63) + (phase == PHASE_SE3 ? 4 : 6);
+            const CloudDev cs = v.clouds[P->src];
+            const int ci = c & ((1 << v.chunk_level) - 1);
+            atomicAdd(st, (unsigned long long)(tree_first(cs.n, v.chunk_level, ci + 1) - tree_first(cs.n, v.chunk_level, ci)));
+            atomicAdd(st + 1, (unsigned long long)total);
+        }
+    }
+    __syncthreads();
+    if (active) {
+        int r = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+        for (int w = 0; w < wid; ++w) r += s_wc[w];
+        const int sb = s_single;
+        if (sb < 0) {
+            v.qlist[(size_t)c * kChunkQ + s_slot[l] + (r - s_base[l])] = x;
+        } else {
+            const int gxs = v.clouds[P->src].off + x;
+            if (phase == PHASE_SE3) v.sq_list[sb + r] = gxs;
+            else v.sq_list[v.ld - 1 - (sb + r)] = gxs;
+        }
+    }
+}
+
+// Results of a searched query (one lane): the recheck flag, the certificate, the
+// correspondence and its stored distance.
+template <int D>
+__device__ __forceinline__ void nn_finish(const View& v, const PairDev* P, int pair, const TreeRef& TR,
+                                          const CloudDev& ct, int gx, int g, bool flag, float d1, float d2, int i1,
+                                          float thr, float na, float nb) {
+    if ((int)flag & (int)(ct.n > 1)) {
+        const int at = atomicAdd(v.flag_count, 1);
+        v.flag_list[at] = g;
+        atomicAdd(&v.pair_rechecked[pair], 1);
+    }
+    // certificate for the next iterations (k_nn_prep): exact match distance <= sqrt(d1 + err),
+    // every other target >= min(d2 - err(d2), thr): visited ones by the top-2, unvisited
+    // ones because every box skipped had a bound >= thr at the time (thr only decreases)
+    if ((int)flag | (int)(i1 < 0)) {
+        v.cert_it[g] = -1;
+    } else {
+        const float l2 = fminf(d2 - f32_err(d2, na, nb, D), thr * (1.f - 4e-6f));
+        v.cert_d1[g] = sqrtf(d1 + f32_err(d1, na, nb, D)) * (1.f + 1e-6f);
+        v.cert_l2[g] = sqrtf(fmaxf(l2, 0.f)) * (1.f - 1e-6f);
+        v.cert_it[g] = P->iter;
+    }
+    // tree position -> target index; a NaN query keeps the reference's zero-initialised index
+    i1 = (i1 < 0) ? 0 : TR.perm[ct.off + i1];
+    v.corr_idx[g] = i1;
+    double Tm[12], Q[D], m0[D];
+    load_T(P, Tm);
+    load_m0<D>(v, TR, gx, m0);
+    pose_m0<D>(Tm, m0, Q);
+    if constexpr (D == 12) {
+        v.corr_dist[g] = stored_dist(v, PHASE_SE3, ct, Q, i1);
+    } else {
+        double Q12[12];
+        Q12[0] = Q[0]; Q12[1] = Q[1]; Q12[2] = Q[2];
+        v.corr_dist[g] = stored_dist(v, PHASE_R3, ct, Q12, i1);
+    }
+}
+
 template <int D>
 __global__ __launch_bounds__(256) void k_nn_group(View v) {
     constexpr int NV = (D + 3) / 4;
@@ -150,19 +368,23 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
     __shared__ float s_r1[kWaves][64], s_r2[kWaves][64];
     __shared__ int s_rb[kWaves][64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    // wave-uniform work item: the pair record, node boxes and leaf ranges become scalar loads
+    // wave-uniform work item: group jg (64 listed queries) of chunk c; the pair record,
+    // node boxes and leaf ranges become scalar loads
     const int gi = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wid);
-    if (gi >= v.ngwork) return;
-    const GroupWork w = v.gwork[gi];
-    const PairDev* P = v.pairs + w.pair;
+    const int c = gi >> 4;
+    if (c >= v.nchunks) return;
+    const int pair = c >> v.chunk_level;
+    const PairDev* P = v.pairs + pair;
     const int phase = P->phase;
     if (phase != (D == 12 ? PHASE_SE3 : PHASE_R3)) return;
+    const int cnt_q = __builtin_amdgcn_readfirstlane(v.qcount[gi]);
+    if (cnt_q == 0) return;
     const CloudDev cs = v.clouds[P->src], ct = v.clouds[P->tgt];
     const TreeRef TR = (D == 12) ? v.t12 : v.t3;
-    const int a = tree_first(cs.n, TR.GL, w.leaf), b = tree_first(cs.n, TR.GL, w.leaf + 1);
-    if (b <= a) return;
-    const bool valid = lane < b - a;
-    const int g = cs.off + (valid ? TR.perm[cs.off + a + lane] : TR.perm[cs.off + a]);
+    const bool valid = lane < cnt_q;
+    const int gx = cs.off + v.qlist[(size_t)gi * 64 + (valid ? lane : 0)];  // source tree slot
+    const int g = cs.off + TR.perm[gx];
+    const float mrg = valid ? v.nn_margin[g] : 0.f;
 
     // query: f64 pose applied to the source element, rounded to f32
     float q[D];
@@ -170,7 +392,9 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
     {  // (the f64 query is recomputed at the end rather than held through the traversal)
         double Tm[12], Q[D];
         load_T(P, Tm);
-        query_f64<D>(v, Tm, g, Q);
+        double m0[D];
+        load_m0<D>(v, TR, gx, m0);
+        pose_m0<D>(Tm, m0, Q);
         double n2 = 0;
 #pragma unroll
         for (int r = 0; r < D; ++r) {
@@ -194,6 +418,13 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
         s_q[wid][lane] = make_float4(q[0], q[1], q[2], 0.f);
     }
 
+    // pruning threshold for the best / second-best f32 distances a1 <= a2: the certified
+    // radius a1 + 3 err, widened by the margin up to (sqrt(a1) + 2 mrg)^2 but never past a2
+    auto widen = [&](float a1, float a2) __attribute__((always_inline)) {
+        const float e = sqrtf(a1) + 2.f * mrg;
+        const float t = fmaxf(a1, fminf(e * e, a2));
+        return t + 3.f * f32_err(t, na, nb, D);
+    };
     float d1 = INFINITY, d2 = INFINITY;
     int i1 = -1;  // target tree position of the best candidate
     float thr = valid ? INFINITY : -1.f;
@@ -207,7 +438,7 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
                 const float e = q[r] - tv[(size_t)r * ld + tp];
                 s = fmaf(e, e, s);
             }
-            thr = s + 3.f * f32_err(s, na, nb, D);
+            thr = widen(s, INFINITY);
         }
     }
 
@@ -292,7 +523,7 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
                 __builtin_amdgcn_wave_barrier();
                 n_eval += 4 * ((w + (cnt <= 32 ? 7 : 3)) >> (cnt <= 32 ? 3 : 2));  // 64-lane evaluation slots issued
             }
-            if ((int)valid & (int)(d1 < INFINITY)) thr = fminf(thr, d1 + 3.f * f32_err(d1, na, nb, D));
+            if ((int)valid & (int)(d1 < INFINITY)) thr = fminf(thr, widen(d1, d2));
             continue;
         }
         n_box += 2;
@@ -330,33 +561,172 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
     if (!valid) return;
     // certification (see the header) and the stored distance
     const bool flag = (bool)((int)(i1 < 0) | (int)!(d2 - d1 > 2.f * f32_err(d2, na, nb, D)));
-    if ((int)flag & (int)(ct.n > 1)) {
-        const int at = atomicAdd(v.flag_count, 1);
-        v.flag_list[at] = g;
-        atomicAdd(&v.pair_rechecked[w.pair], 1);
+    nn_finish<D>(v, P, pair, TR, ct, gx, g, flag, d1, d2, i1, thr, na, nb);
+}
+
+// ------------------------------------------------------------------ one wavefront per query
+// For the queries of sparse chunks (k_nn_prep): a wave's latency, not its lanes, bounds
+// the group kernel when few queries remain, so here the 64 lanes work on ONE query:
+// lane-parallel box tests (the nodes of level A = L - 6, then the 64 leaves under each
+// open one) and a target per lane in the leaf sweeps; each lane keeps the top-2 of the
+// targets it evaluated, the wave's (d1, d2) are two wave minima per leaf.
+template <int D>
+__device__ __forceinline__ void single_one(const View& v, const PairDev* P, int pair, const TreeRef& TR,
+                                           const CloudDev& ct, int gx, int g, int lane, unsigned* n_eval,
+                                           unsigned* n_box) {
+    float q[D];
+    float na;
+    {
+        double Tm[12], m0[D], Q[D];
+        load_T(P, Tm);
+        load_m0<D>(v, TR, gx, m0);
+        pose_m0<D>(Tm, m0, Q);
+        double n2 = 0;
+#pragma unroll
+        for (int r = 0; r < D; ++r) {
+            const double c = (D == 3) ? Q[r] - P->f32_center[r] : Q[r];
+            q[r] = (float)c;
+            n2 += c * c;
+        }
+        na = (float)sqrt(n2) * 1.000001f;
     }
-    // tree position -> target index; a NaN query keeps the reference's zero-initialised index
-    i1 = (i1 < 0) ? 0 : TR.perm[ct.off + i1];
-    v.corr_idx[g] = i1;
-    double Tm[12], Q[D];
-    load_T(P, Tm);
-    query_f64<D>(v, Tm, g, Q);
-    if constexpr (D == 12) {
-        v.corr_dist[g] = stored_dist(v, PHASE_SE3, ct, Q, i1);
-    } else {
-        double Q12[12];
-        Q12[0] = Q[0]; Q12[1] = Q[1]; Q12[2] = Q[2];
-        v.corr_dist[g] = stored_dist(v, PHASE_R3, ct, Q12, i1);
+    const float nb = (D == 12) ? P->tgt_norm12 : P->tgt_norm3;
+    f32x2 q2[(D + 1) / 2];
+#pragma unroll
+    for (int r = 0; r < D / 2; ++r) q2[r] = f32x2{q[2 * r], q[2 * r + 1]};
+    const float mrg = v.nn_margin[g];
+    auto widen = [&](float a1, float a2) __attribute__((always_inline)) {
+        const float e = sqrtf(a1) + 2.f * mrg;
+        const float t = fmaxf(a1, fminf(e * e, a2));
+        return t + 3.f * f32_err(t, na, nb, D);
+    };
+    const float* tv = TR.tvec + ct.off;
+    const size_t ld = v.ld;
+    float thr = INFINITY;
+    {  // seed with the previous match
+        const int prev = v.corr_idx[g];
+        if (prev >= 0 && prev < ct.n) {
+            const int tp = TR.pos[ct.off + prev];
+            float s = 0.f;
+#pragma unroll
+            for (int r = 0; r < D; ++r) {
+                const float e = q[r] - tv[(size_t)r * ld + tp];
+                s = fmaf(e, e, s);
+            }
+            thr = widen(s, INFINITY);
+        }
+    }
+    const float* box_lo = TR.lo + (size_t)P->tgt * TR.nnodes * D;
+    const float* box_hi = TR.hi + (size_t)P->tgt * TR.nnodes * D;
+    auto lbound = [&](int h) __attribute__((always_inline)) {
+        if constexpr (D == 12) return box_lb12(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q2);
+        else return box_lb<D>(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q);
+    };
+    const int L = TR.L;
+    const int sh = L > 6 ? 6 : L;
+    const int A = L - sh, nA = 1 << A, firstA = nA - 1, first_leaf = (1 << L) - 1;
+    float a1 = INFINITY, a2 = INFINITY, d1 = INFINITY, d2 = INFINITY;
+    int b1 = -1;
+    for (int c0 = 0; c0 < nA; c0 += 64) {
+        const int ai = c0 + lane;
+        const float lbA = ai < nA ? lbound(firstA + ai) : INFINITY;
+        *n_box += 1;
+        unsigned long long mA = __ballot(lbA * (1.f - 2e-6f) < thr);
+        while (mA) {
+            const int j = __builtin_ctzll(mA);
+            mA &= mA - 1ull;
+            if (!(__shfl(lbA, j, 64) * (1.f - 2e-6f) < thr)) continue;
+            const int l0 = (c0 + j) << sh;
+            const float lbL = lane < (1 << sh) ? lbound(first_leaf + l0 + lane) : INFINITY;
+            *n_box += 1;
+            unsigned long long mL = __ballot(lbL * (1.f - 2e-6f) < thr);
+            while (mL) {
+                const int t = __builtin_ctzll(mL);
+                mL &= mL - 1ull;
+                if (!(__shfl(lbL, t, 64) * (1.f - 2e-6f) < thr)) continue;
+                const int ta = tree_first(ct.n, L, l0 + t), tb = tree_first(ct.n, L, l0 + t + 1);
+                float d = INFINITY;
+                if (lane < tb - ta) {
+                    const int x = ta + lane;
+                    if constexpr (D == 12) {
+                        f32x2 e, s2;
+#pragma unroll
+                        for (int r = 0; r < 6; ++r) {
+                            e = q2[r] - f32x2{tv[(size_t)(2 * r) * ld + x], tv[(size_t)(2 * r + 1) * ld + x]};
+                            s2 = (r == 0) ? e * e : __builtin_elementwise_fma(e, e, s2);
+                        }
+                        d = s2.x + s2.y;
+                    } else {
+                        float e, acc;
+                        e = q[0] - tv[x]; acc = e * e;
+                        e = q[1] - tv[ld + x]; acc = fmaf(e, e, acc);
+                        e = q[2] - tv[2 * ld + x]; acc = fmaf(e, e, acc);
+                        d = acc;
+                    }
+                }
+                *n_eval += 1;
+                const bool lt = d < a1;
+                a2 = __builtin_amdgcn_fmed3f(a1, a2, d);
+                b1 = lt ? ta + lane : b1;
+                a1 = lt ? d : a1;
+                // wave top-2: the smallest lane best, then the smallest of the other lanes'
+                // bests and the winner's second (ties between lanes: d2 = d1)
+                d1 = wave_minf(a1);
+                const unsigned long long win = __ballot(a1 == d1);
+                const float other = wave_minf(a1 == d1 ? a2 : a1);
+                d2 = __popcll(win) > 1 ? d1 : other;
+                if (d1 < INFINITY) thr = fminf(thr, widen(d1, d2));
+            }
+        }
+    }
+    int i1 = -1;
+    {
+        const unsigned long long win = __ballot((int)(a1 == d1) & (int)(b1 >= 0));
+        if (win) i1 = __shfl(b1, __builtin_ctzll(win), 64);
+    }
+    if (lane != 0) return;
+    const bool flag = (bool)((int)(i1 < 0) | (int)!(d2 - d1 > 2.f * f32_err(d2, na, nb, D)));
+    nn_finish<D>(v, P, pair, TR, ct, gx, g, flag, d1, d2, i1, thr, na, nb);
+}
+
+// grid-stride over the single-query list of the phase: SE(3) entries from the front,
+// R3 entries from the back (counters flag_count[1], [2])
+template <int D>
+__global__ __launch_bounds__(256) void k_nn_single(View v) {
+    const int lane = threadIdx.x & 63;
+    const int w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int nq = __builtin_amdgcn_readfirstlane(v.flag_count[D == 12 ? 1 : 2]);
+    unsigned n_eval = 0, n_box = 0;
+    for (int f = w0; f < nq; f += gridDim.x * 4) {
+        const int gx = __builtin_amdgcn_readfirstlane(D == 12 ? v.sq_list[f] : v.sq_list[v.ld - 1 - f]);
+        const int pair = v.cloud_of[gx] >> 1;
+        const PairDev* P = v.pairs + pair;
+        const CloudDev cs = v.clouds[P->src], ct = v.clouds[P->tgt];
+        const TreeRef TR = (D == 12) ? v.t12 : v.t3;
+        const int g = cs.off + TR.perm[gx];
+        single_one<D>(v, P, pair, TR, ct, gx, g, lane, &n_eval, &n_box);
+    }
+    if ((int)(lane == 0) & (int)(n_eval + n_box > 0)) {
+        unsigned long long* st = v.stats + kStatCols * (w0 & 63) + (D == 12 ? 0 : 2);
+        atomicAdd(st, 64ull * n_eval);
+        atomicAdd(st + 1, 64ull * n_box);
     }
 }
 
 }  // namespace
 
+void launch_nn_prep(const View& v, hipStream_t s) {
+    hipLaunchKernelGGL(k_nn_prep, dim3(v.nchunks), dim3(kChunkQ), 0, s, v);
+}
+// 16 groups of 64 per chunk, kWaves groups per block
+// and the single-query kernel over a fixed grid (8192 waves)
 void launch_nn_se3(const View& v, hipStream_t s) {
-    hipLaunchKernelGGL(k_nn_group<12>, dim3((v.ngwork + kWaves - 1) / kWaves), dim3(64 * kWaves), 0, s, v);
+    hipLaunchKernelGGL(k_nn_group<12>, dim3(v.nchunks * (kChunkQ / 64) / kWaves), dim3(64 * kWaves), 0, s, v);
+    hipLaunchKernelGGL(k_nn_single<12>, dim3(2048), dim3(256), 0, s, v);
 }
 void launch_nn_r3(const View& v, hipStream_t s) {
-    hipLaunchKernelGGL(k_nn_group<3>, dim3((v.ngwork + kWaves - 1) / kWaves), dim3(64 * kWaves), 0, s, v);
+    hipLaunchKernelGGL(k_nn_group<3>, dim3(v.nchunks * (kChunkQ / 64) / kWaves), dim3(64 * kWaves), 0, s, v);
+    hipLaunchKernelGGL(k_nn_single<3>, dim3(2048), dim3(256), 0, s, v);
 }
 
 }  // namespace se3icp

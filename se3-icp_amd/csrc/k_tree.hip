@@ -324,7 +324,7 @@ __global__ __launch_bounds__(256) void k_tree_finish(TreeView t) {
         const int p = t.perm[g];
         t.pos[cl.off + p] = g - cl.off;
         for (int d = 0; d < t.D; ++d) t.tvec[(size_t)d * t.ld + g] = t.vec[(size_t)d * t.ld + cl.off + p];
-        if (t.tvec64)
+        if ((t.tvec64 != nullptr) & !((t.vec64_sources_only != 0) & ((t.cloud_of[g] & 1) != 0)))
             for (int d = 0; d < t.D; ++d) t.tvec64[(size_t)d * t.ld + g] = t.vec64[(size_t)d * t.ld + cl.off + p];
     }
 }

@@ -28,7 +28,8 @@ struct TreeView {
     int32_t* pos;      // [ld] point (global slot) -> local tree position
     float* tvec;       // [D][ld] vectors in tree order
     const double* vec64;  // optional [D][ld] f64 vectors (original order) ...
-    double* tvec64;       // ... copied into tree order (3-D trees: coalesced leaf loads)
+    double* tvec64;       // ... copied into tree order (coalesced leaf / query-chunk loads)
+    int32_t vec64_sources_only;  // copy the f64 vectors of even (source) clouds only
     uint32_t* blo;     // [nclouds][nnodes][D] build scratch (orderable bits)
     uint32_t* bhi;
     float* lo;         // [nclouds][nnodes][D] node boxes

@@ -37,12 +37,6 @@ struct TreeRef {
     const float* hi;
 };
 
-// One wavefront of the loop's NN kernel = one leaf (<= 64 queries) of a source tree.
-struct GroupWork {
-    int32_t pair;
-    int32_t leaf;
-};
-
 struct View {
     int32_t ld;        // SoA row stride (total points of the batch, padded to 64)
     int32_t npts;      // real points of the batch (per-point kernels stop here)
@@ -68,7 +62,7 @@ struct View {
     float* corr_dist;
     unsigned long long* stats;  // [4] NN work counters: se3 dist evals, se3 box tests, r3 dist evals, r3 box tests
     int32_t* flag_list;
-    int32_t* flag_count;  // [1]
+    int32_t* flag_count;  // [3] recheck list, single-query lists (SE(3), R3)
     uint64_t* trim_key;   // [npairs]
     double* red_partial;  // [nwork * kRedVals]
     double* red_out;      // [npairs * kRedVals]
@@ -77,8 +71,23 @@ struct View {
     int32_t* pair_rechecked;  // [npairs]
     // kd-trees (k_tree.hip) over the f32 vectors: 3-D points (xyz32) and 12-D SE(3) elements (fr32)
     TreeRef t3, t12;
-    const GroupWork* gwork;   // [ngwork] source leaves of every pair
-    int32_t ngwork;
+    // loop NN work (k_nn.hip): chunk c = node (c mod 2^CL) of level CL of pair (c >> CL)'s
+    // source tree (<= kChunkQ positions); k_nn_prep compacts the chunk's queries that its
+    // certificate cannot settle into qlist, k_nn_group sweeps them 64 per wavefront
+    int32_t chunk_level;  // CL
+    int32_t nchunks;      // npairs << CL
+    int32_t* qlist;       // [nchunks * kChunkQ] global slots of the searched queries, tree order
+    int32_t* qcount;      // [nchunks][16] lanes of each group (0: none)
+    int32_t* sq_list;     // [ld] queries of sparse chunks (global source tree slots) for k_nn_single:
+                          // SE(3) phase from the front (count flag_count[1]), R3 from the back ([2])
+    const double* hist;   // [kHist][npairs][12] pose T used at iteration k, row k % kHist
+    // NN certificate of each source point from its last search (iteration cert_it):
+    // every target other than the match is at least cert_l2 away from that query, the
+    // match at most cert_d1 (exact distances, conservatively rounded)
+    float* cert_d1;
+    float* cert_l2;
+    int32_t* cert_it;     // -1: none
+    float* nn_margin;     // [ld] search-radius expansion of the searched queries
 };
 
 // ---- k_setup.hip
@@ -95,8 +104,10 @@ void launch_normalize(const View& v, const ChunkWork* chunks, int nchunks, doubl
 void launch_lrf(const View& v, int write_knn, hipStream_t s);
 
 // ---- k_loop.hip
-// exact 1-NN of every active pair's source points, one wavefront per source leaf,
-// traversing the target kd-tree (12-D in the SE(3) phase, 3-D in the R3 phase)
+// exact 1-NN of every active pair's source points: k_nn_prep settles the queries whose
+// certificate still holds and lists the rest, k_nn_group sweeps those 64 per wavefront
+// through the target kd-tree (12-D in the SE(3) phase, 3-D in the R3 phase)
+void launch_nn_prep(const View& v, hipStream_t s);
 void launch_nn_se3(const View& v, hipStream_t s);
 void launch_nn_r3(const View& v, hipStream_t s);
 void launch_recheck(const View& v, int nblocks, hipStream_t s);

@@ -276,9 +276,10 @@ def nearest_neighbors(query, data, device: int = 0):
 
 
 def last_kernel_times(device: int = 0) -> dict:
-    out = (C.c_double * 18)()
+    out = (C.c_double * 23)()
     _lib.check(_lib.load().se3icp_last_kernel_times(device, out))
     keys = ["nn_se3_ms", "nn_r3_ms", "recheck_ms", "trim_ms", "reduce_ms", "setup_ms", "nn_se3_launches",
             "nn_r3_launches", "se3_dist_evals", "se3_box_tests", "r3_dist_evals", "r3_box_tests",
-            "lrf_ms", "lrf_queries", "lrf_leaves", "lrf_merges", "lrf_box_tests", "lrf_candidates"]
+            "lrf_ms", "lrf_queries", "lrf_leaves", "lrf_merges", "lrf_box_tests", "lrf_candidates",
+            "nn_prep_ms", "se3_queries", "se3_searched", "r3_queries", "r3_searched"]
     return dict(zip(keys, list(out)))
