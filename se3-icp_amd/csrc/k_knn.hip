@@ -513,39 +513,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
 
     // ---------------------------------------------------------------- per-query sums
     // (a separate pass over the parked neighbour lists keeps the kNN loop's live state small)
-    for (int j = 0; j < kQ; ++j) {
-        double* pj = park + j * PK_N;
+    // Eight lanes per query, the wave's kQ = 8 queries at once: lane qs of group qj takes the
+    // neighbour ranks = qs (mod 8), and the group's partial sums are combined by a three-stage
+    // butterfly (DPP / swizzle exchanges).  21 values per query:
+    //   [0..2]  S' = sum of v over ranks 1 .. rz-1   (v = p - q, local coordinates)
+    //   [3..5]  S  = sum of v over ranks 1 .. rz
+    //   [6..11] M  = sum of v v^T over ranks 1 .. rz (xx xy xz yy yz zz)
+    //   [12..20] Open3D cumulants of the raw coordinates over ranks 0 .. kn-1
+    // The TOLDI covariance about the quirk centroid (ISR.cpp:259-272) is assembled from
+    // S', S, M in the eigen pass; the reference sums the products sequentially, so
+    // both differ from it by rounding only.
+    static_assert(kQ * 8 == 64, "eight lanes per query");
+    const int qj = lane >> 3, qs = lane & 7;
+    {
+        double* pj = park + qj * PK_N;
         const int flags = (int)pj[PK_FLAGS];
-        if (!(flags & 3)) continue;
-        const int w = w0 + j;
-        const int c = cloud_of[w];
-        const CloudSetup st = setup[c];
-        const CloudDev cl = clouds[c];
-        const double* X = v.xyz64 + cl.off;
-        const double* Y = v.xyz64 + v.ld + cl.off;
-        const double* Z = v.xyz64 + 2 * (size_t)v.ld + cl.off;
-        const double qx = TX[w], qy = TY[w], qz = TZ[w];
-        const int nTop = (int)pj[PK_NTOP];
-        const int* nbl = (s_nbw + j * v.kmax);
-
-        // All sums of the query in one recursive-halving reduction (wave.hpp), 21 values:
-        //   [0..2]  S' = sum of v over ranks 1 .. rz-1   (v = p - q, local coordinates)
-        //   [3..5]  S  = sum of v over ranks 1 .. rz
-        //   [6..11] M  = sum of v v^T over ranks 1 .. rz (xx xy xz yy yz zz)
-        //   [12..20] Open3D cumulants of the raw coordinates over ranks 0 .. kn-1
-        // The TOLDI covariance about the quirk centroid (ISR.cpp:259-272) is assembled from
-        // S', S, M in the eigen pass; the reference sums the products sequentially, so
-        // both differ from it by rounding only.
-        double x[32];
+        double x[kSums];
 #pragma unroll
-        for (int i = 0; i < 32; ++i) x[i] = 0.0;
-        if (flags & 1) {
-            const int kk = min(st.k_lrf, nTop);
-            const int rz = kk / 3;
-#pragma unroll
-            for (int u = 0; u < 2; ++u) {  // neighbour ranks lane+1 and lane+65 (k <= 128)
-                const int rk = 1 + lane + 64 * u;
-                if ((int)(rk <= rz) & (int)(rk < kk)) {
+        for (int i = 0; i < kSums; ++i) x[i] = 0.0;
+        if (flags & 3) {
+            const int w = w0 + qj;
+            const int c = cloud_of[w];
+            const int off = clouds[c].off;
+            const double* X = v.xyz64 + off;
+            const double* Y = v.xyz64 + v.ld + off;
+            const double* Z = v.xyz64 + 2 * (size_t)v.ld + off;
+            const double qx = TX[w], qy = TY[w], qz = TZ[w];
+            const int nTop = (int)pj[PK_NTOP];
+            const int* nbl = s_nbw + qj * v.kmax;
+            if (flags & 1) {
+                const int kk = min(setup[c].k_lrf, nTop);
+                const int rz = kk / 3;
+                const int hi = min(rz, kk - 1);
+                for (int rk = 1 + qs; rk <= hi; rk += 8) {
                     const int q = nbl[rk];
                     const double vx = X[q] - qx, vy = Y[q] - qy, vz = Z[q] - qz;
                     if (rk < rz) { x[0] += vx; x[1] += vy; x[2] += vz; }
@@ -553,26 +553,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
                     x[6] += vx * vx; x[7] += vx * vy; x[8] += vx * vz;
                     x[9] += vy * vy; x[10] += vy * vz; x[11] += vz * vz;
                 }
+                if (qs == 0) {
+                    const int far = nbl[kk - 1];
+                    const double fdx = qx - X[far], fdy = qy - Y[far], fdz = qz - Z[far];
+                    pj[PK_R] = sqrt(fdx * fdx + fdy * fdy + fdz * fdz);  // ISR.cpp:256
+                    pj[PK_KK] = (double)kk;
+                }
             }
-            if (lane == 0) {
-                const int far = nbl[kk - 1];
-                const double fdx = qx - X[far], fdy = qy - Y[far], fdz = qz - Z[far];
-                pj[PK_R] = sqrt(fdx * fdx + fdy * fdy + fdz * fdz);  // ISR.cpp:256
-                pj[PK_KK] = (double)kk;
+            if (flags & 2) {  // EstimateNormals (ISR.cpp:643, :43): ranks 0 .. kn-1, self included
+                const int kn = min(setup[c].k_nrm, nTop);
+                for (int r = qs; r < kn; r += 8) {
+                    const int q = nbl[r];
+                    const double px = X[q], py = Y[q], pz = Z[q];
+                    x[12] += px; x[13] += py; x[14] += pz;
+                    x[15] += px * px; x[16] += px * py; x[17] += px * pz;
+                    x[18] += py * py; x[19] += py * pz; x[20] += pz * pz;
+                }
             }
         }
-        if (flags & 2) {  // EstimateNormals (ISR.cpp:643, :43): ranks 0 .. kn-1, self included
-            const int kn = min(st.k_nrm, nTop);
-            for (int r = lane; r < kn; r += 64) {
-                const int q = nbl[r];
-                const double px = X[q], py = Y[q], pz = Z[q];
-                x[12] += px; x[13] += py; x[14] += pz;
-                x[15] += px * px; x[16] += px * py; x[17] += px * pz;
-                x[18] += py * py; x[19] += py * pz; x[20] += pz * pz;
-            }
+#pragma unroll
+        for (int i = 0; i < kSums; ++i) {
+            x[i] += xor_lane(x[i], 1);
+            x[i] += xor_lane(x[i], 2);
+            x[i] += xor_lane(x[i], 4);
         }
-        const double sv = wave_sum32(x);
-        if ((int)((lane & 1) == 0) & (int)((lane >> 1) < kSums)) pj[PK_SUM + (lane >> 1)] = sv;
+        __builtin_amdgcn_wave_barrier();
+        if ((int)(qs == 0) & (int)((flags & 3) != 0)) {
+#pragma unroll
+            for (int i = 0; i < kSums; ++i) pj[PK_SUM + i] = x[i];
+        }
         __builtin_amdgcn_wave_barrier();
     }
     PROF_NOW(t_s1);
@@ -654,33 +663,42 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
 
     // ---------------------------------------------------------------- TOLDI axes (ISR.cpp:286-306)
     __builtin_amdgcn_wave_barrier();  // (the eigen pass has read PK_SUM; the axis sums reuse it)
-    for (int j = 0; j < kQ; ++j) {
-        double* pj = park + j * PK_N;
-        if (!((int)pj[PK_FLAGS] & 1)) continue;
-        const int w = w0 + j;
-        const int c = v.cloud_of[w];
-        const CloudDev cl = v.clouds[c];
-        const double* X = v.xyz64 + cl.off;
-        const double* Y = v.xyz64 + v.ld + cl.off;
-        const double* Z = v.xyz64 + 2 * (size_t)v.ld + cl.off;
-        const double qx = TX[w], qy = TY[w], qz = TZ[w];
-        const double nx = __shfl(zn.x, j, 64), ny = __shfl(zn.y, j, 64), nz = __shfl(zn.z, j, 64);
-        const double R = pj[PK_R];
-        const int kk = (int)pj[PK_KK];
-        const int* nbl = (s_nbw + j * v.kmax);
-        double a0 = 0, a1 = 0, a2 = 0, s0 = 0, s1 = 0, s2 = 0;
-        for (int r = 1 + lane; r < kk; r += 64) {
-            const int q = nbl[r];
-            const double vx = X[q] - qx, vy = Y[q] - qy, vz = Z[q] - qz;
-            a0 += vx; a1 += vy; a2 += vz;
-            const double an = nx * vx + ny * vy + nz * vz;
-            const double rr = R - sqrt(vx * vx + vy * vy + vz * vz);
-            const double wgt = (rr * rr) * (an * an);
-            s0 += wgt * vx; s1 += wgt * vy; s2 += wgt * vz;
+    {  // eight lanes per query again (see the sums pass)
+        double* pj = park + qj * PK_N;
+        const int flags = (int)pj[PK_FLAGS];
+        const double nx = __shfl(zn.x, qj, 64), ny = __shfl(zn.y, qj, 64), nz = __shfl(zn.z, qj, 64);
+        double x6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        if (flags & 1) {
+            const int w = w0 + qj;
+            const int off = v.clouds[v.cloud_of[w]].off;
+            const double* X = v.xyz64 + off;
+            const double* Y = v.xyz64 + v.ld + off;
+            const double* Z = v.xyz64 + 2 * (size_t)v.ld + off;
+            const double qx = TX[w], qy = TY[w], qz = TZ[w];
+            const double R = pj[PK_R];
+            const int kk = (int)pj[PK_KK];
+            const int* nbl = s_nbw + qj * v.kmax;
+            for (int r = 1 + qs; r < kk; r += 8) {
+                const int q = nbl[r];
+                const double vx = X[q] - qx, vy = Y[q] - qy, vz = Z[q] - qz;
+                x6[0] += vx; x6[1] += vy; x6[2] += vz;
+                const double an = nx * vx + ny * vy + nz * vz;
+                const double rr = R - sqrt(vx * vx + vy * vy + vz * vz);
+                const double wgt = (rr * rr) * (an * an);
+                x6[3] += wgt * vx; x6[4] += wgt * vy; x6[5] += wgt * vz;
+            }
         }
-        const double x8[8] = {a0, a1, a2, s0, s1, s2, 0.0, 0.0};
-        const double sv = wave_sum_pow2<8>(x8);  // value lane >> 3
-        if ((int)((lane & 7) == 0) & (int)((lane >> 3) < 6)) pj[PK_SUM + (lane >> 3)] = sv;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            x6[i] += xor_lane(x6[i], 1);
+            x6[i] += xor_lane(x6[i], 2);
+            x6[i] += xor_lane(x6[i], 4);
+        }
+        __builtin_amdgcn_wave_barrier();
+        if ((int)(qs == 0) & (int)((flags & 1) != 0)) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) pj[PK_SUM + i] = x6[i];
+        }
     }
     __builtin_amdgcn_wave_barrier();
     double acc3[3] = {0, 0, 0}, accs3[3] = {0, 0, 0};

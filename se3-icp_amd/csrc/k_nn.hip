@@ -197,45 +197,65 @@ __device__ __forceinline__ void pose_m0(const double* T, const double* m, double
     else pose_point(T, m[0], m[1], m[2], q);
 }
 
+// Only the translation rows of a source element are loaded here.  Its rotation columns are
+// alpha times an orthonormal TOLDI frame X, so for two poses T, T':
+//   |T M0 - T' M0|^2 = alpha^2 |(R - R') X|_F^2 + |(R - R') m_t + t - t'|^2
+//                    = alpha^2 |R - R'|_F^2     + |(R - R') m_t + t - t'|^2
+// and |T M0|^2 = 3 alpha^2 + |R m_t + t|^2 (X orthonormal to f64 rounding; padded below).
+// The 3-D phase is the translation part alone (alpha = 0).
+__device__ __forceinline__ double rot_frob2(const double* A, const double* B) {
+    double s = 0.0;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) s += (A[r * 4 + c] - B[r * 4 + c]) * (A[r * 4 + c] - B[r * 4 + c]);
+    return s;
+}
+__device__ __forceinline__ double dist3_f64(const double* a, const double* b) {
+    return sqrt((a[0] - b[0]) * (a[0] - b[0]) + (a[1] - b[1]) * (a[1] - b[1]) + (a[2] - b[2]) * (a[2] - b[2]));
+}
+
 // Settle the query at source tree slot gx (point g) from its certificate (true: corr_idx
 // stays, corr_dist refreshed for the moved query) or prepare its search (false: nn_margin).
 template <int D>
 __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, const PairDev* P, int pair,
-                                            const CloudDev& ct, int gx, int g) {
-    double m0[D], T[12], Q[D];
-    load_m0<D>(v, TR, gx, m0);
+                                            const CloudDev& ct, int gx, int g, double a2) {
+    double mt[3], T[12], Qt[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) mt[r] = TR.tvec64[(size_t)(D - 3 + r) * v.ld + gx];
     load_T(P, T);
-    pose_m0<D>(T, m0, Q);
+    pose_point(T, mt[0], mt[1], mt[2], Qt);
+    const double rot2 = 3.0 * a2 * (1.0 + 1e-12);  // |rotation columns|^2 (12-D), 0 (3-D)
     const int it = P->iter;
     const int ci = v.cert_it[g];
-    const double qn = norm_f64<D>(Q);
+    const double qn = sqrt(rot2 + Qt[0] * Qt[0] + Qt[1] * Qt[1] + Qt[2] * Qt[2]);
     if ((int)(ci >= P->phase_start) & (int)(ci < it) & (int)(it - ci < kHist)) {
-        double Tr[12], Qr[D];
+        double Tr[12], Qr[3];
         load_hist(v, ci, pair, Tr);
-        pose_m0<D>(Tr, m0, Qr);
-        // |q_now - q_then|, padded for the rounding of the two f64 queries
-        const double dl = dist_f64<D>(Q, Qr) * (1.0 + 1e-12) + 4e-16 * (qn + norm_f64<D>(Qr));
+        pose_point(Tr, mt[0], mt[1], mt[2], Qr);
+        const double qr = sqrt(rot2 + Qr[0] * Qr[0] + Qr[1] * Qr[1] + Qr[2] * Qr[2]);
+        const double dt = dist3_f64(Qt, Qr);
+        // |q_now - q_then|, padded for the frame's orthonormality and the rounding of the
+        // two f64 queries the searches used
+        const double dl = sqrt(a2 * rot_frob2(T, Tr) * (1.0 + 1e-12) + dt * dt) * (1.0 + 1e-12) + 2e-15 * (qn + qr);
         const double a = (double)v.cert_l2[g] - dl, b = (double)v.cert_d1[g] + dl;
         // margin for the f64 rounding of the reference's own squared distances (|q| + |target| <= M)
         const double M = 2.0 * qn + b;
         if ((int)(a > b) & (int)((a - b) * (a + b) > 1e-14 * M * M)) {
             const int j = v.corr_idx[g];
-            if constexpr (D == 12) {
-                v.corr_dist[g] = stored_dist(v, PHASE_SE3, ct, Q, j);
-            } else {
-                double Q12[12];
-                Q12[0] = Q[0]; Q12[1] = Q[1]; Q12[2] = Q[2];
-                v.corr_dist[g] = stored_dist(v, PHASE_R3, ct, Q12, j);
-            }
+            double Q12[12];
+            Q12[D - 3] = Qt[0]; Q12[D - 2] = Qt[1]; Q12[D - 1] = Qt[2];
+            v.corr_dist[g] = stored_dist(v, D == 12 ? PHASE_SE3 : PHASE_R3, ct, Q12, j);
             return true;
         }
     }
     float m = 0.f;
     if (it >= 2) {
-        double Tp[12], Qp[D];
+        double Tp[12], Qp[3];
         load_hist(v, it - 1, pair, Tp);
-        pose_m0<D>(Tp, m0, Qp);
-        m = (float)(SE3ICP_NN_EXPAND * dist_f64<D>(Q, Qp));
+        pose_point(Tp, mt[0], mt[1], mt[2], Qp);
+        const double dt = dist3_f64(Qt, Qp);
+        m = (float)(SE3ICP_NN_EXPAND * sqrt(a2 * rot_frob2(T, Tp) + dt * dt));
     }
     v.nn_margin[g] = m;
     return false;
@@ -266,8 +286,9 @@ __global__ __launch_bounds__(1024) void k_nn_prep(View v) {
         x = a + (int)threadIdx.x;
         if (x < b) {
             const int gx = cs.off + x, g = cs.off + TR.perm[gx];
-            active = (phase == PHASE_SE3) ? !prep_settle<12>(v, TR, P, pair, ct, gx, g)
-                                          : !prep_settle<3>(v, TR, P, pair, ct, gx, g);
+            const double al = v.setup[P->src].alpha;
+            active = (phase == PHASE_SE3) ? !prep_settle<12>(v, TR, P, pair, ct, gx, g, al * al)
+                                          : !prep_settle<3>(v, TR, P, pair, ct, gx, g, 0.0);
             l = tree_node_of(x, cs.n, TR.GL) - (ci << (TR.GL - v.chunk_level));
             if (active) atomicAdd(&s_cnt[l], 1);
         }
@@ -344,17 +365,12 @@ __device__ __forceinline__ void nn_finish(const View& v, const PairDev* P, int p
     // tree position -> target index; a NaN query keeps the reference's zero-initialised index
     i1 = (i1 < 0) ? 0 : TR.perm[ct.off + i1];
     v.corr_idx[g] = i1;
-    double Tm[12], Q[D], m0[D];
+    // the stored distance needs the translation part of the query only (ISR.cpp:465-468)
+    double Tm[12], Q12[12];
     load_T(P, Tm);
-    load_m0<D>(v, TR, gx, m0);
-    pose_m0<D>(Tm, m0, Q);
-    if constexpr (D == 12) {
-        v.corr_dist[g] = stored_dist(v, PHASE_SE3, ct, Q, i1);
-    } else {
-        double Q12[12];
-        Q12[0] = Q[0]; Q12[1] = Q[1]; Q12[2] = Q[2];
-        v.corr_dist[g] = stored_dist(v, PHASE_R3, ct, Q12, i1);
-    }
+    const double* m = TR.tvec64 + gx;
+    pose_point(Tm, m[(size_t)(D - 3) * v.ld], m[(size_t)(D - 2) * v.ld], m[(size_t)(D - 1) * v.ld], Q12 + D - 3);
+    v.corr_dist[g] = stored_dist(v, D == 12 ? PHASE_SE3 : PHASE_R3, ct, Q12, i1);
 }
 
 template <int D>
