@@ -235,13 +235,17 @@ __device__ __forceinline__ float box_lb3(const float* lo, const float* hi, float
 // Per-query state parked in LDS between the kNN pass and the batched eigen-solves
 // (slots of s_park[wave][query]).
 // PK_SUM: the 21 neighbour sums of a query (see the sums pass), later its 6 TOLDI axis sums.
-enum ParkSlot { PK_SUM = 0, PK_R = 21, PK_KK = 22, PK_GP = 23, PK_FLAGS = 24, PK_K = 25, PK_NTOP = 26, PK_N = 27 };
+// PK_ZN: the TOLDI z axis (smallest-eigenvalue eigenvector) from the batched solve.
+enum ParkSlot { PK_SUM = 0, PK_R = 21, PK_KK = 22, PK_GP = 23, PK_FLAGS = 24, PK_K = 25, PK_NTOP = 26, PK_ZN = 27, PK_N = 30 };
 constexpr int kSums = 21;
 
 // The per-cloud records and node boxes are also passed as restrict-qualified arguments:
 // with no possible aliasing store the compiler can serve their wave-uniform reads from
 // the scalar cache (s_load) instead of vector loads.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_lrf(View v, int write_knn, const int32_t* __restrict__ cloud_of,
+#ifndef SE3ICP_LRF_WPE
+#define SE3ICP_LRF_WPE 5
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_WPE))) void k_lrf(View v, int write_knn, const int32_t* __restrict__ cloud_of,
                                              const CloudSetup* __restrict__ setup,
                                              const CloudDev* __restrict__ clouds, const float* __restrict__ tlo,
                                              const float* __restrict__ thi) {
@@ -252,6 +256,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     extern __shared__ int s_dyn[];
     __shared__ double s_park[kWaves][kQ][PK_N];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#ifdef SE3ICP_LRF_LDSPAD  // occupancy experiment: unused LDS
+    __shared__ int s_pad[SE3ICP_LRF_LDSPAD / 4];
+    if (v.npts < 0) s_pad[threadIdx.x] = 0;
+#endif
     // first global slot (3-D tree order) of the wave's kQ queries; wave-uniform so that
     // the per-cloud records and the node boxes are scalar loads
 #if SE3ICP_LRF_XCD
@@ -260,7 +268,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     const int bid = blockIdx.x;
 #endif
     const int w0 = __builtin_amdgcn_readfirstlane((bid * kWaves + wid) * kQ);
-    if (w0 >= v.npts) return;
+    if (bid * kWaves * kQ >= v.npts) return;  // (block-uniform: the block synchronises later)
     const TreeRef T = v.t3;
     double* bd = s_d[wid];
     int* bi = s_i[wid];
@@ -275,6 +283,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     int prev_c = -1, prev_K = 0;
     double prev_kth = 0.0, pqx = 0.0, pqy = 0.0, pqz = 0.0;
     unsigned n_queries = 0, n_leaves = 0, n_sel = 0, n_box = 0, n_cand = 0;
+#ifdef SE3ICP_LRF_NOCOUNT  // work counters off (SGPR pressure experiment)
+#define LRF_COUNT(x) do {} while (0)
+#else
+#define LRF_COUNT(x) x
+#endif
 #ifdef SE3ICP_PROF
     unsigned long long c_knn = 0, c_sort = 0, c_sum = 0, c_fin = 0;
 #endif
@@ -325,7 +338,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         }
         auto select_thr = [&]() __attribute__((always_inline)) {
             __builtin_amdgcn_wave_barrier();
-            ++n_sel;
+            LRF_COUNT(++n_sel);
             double dk[4];
             int ik[4];
             unsigned u[4];
@@ -376,7 +389,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         auto leaf = [&](int h) __attribute__((always_inline)) {
             // (wave-uniform: readfirstlane keeps the leaf range arithmetic on the scalar unit)
             const int i = __builtin_amdgcn_readfirstlane(h - first_leaf);
-            ++n_leaves;
+            LRF_COUNT(++n_leaves);
             const int a = __builtin_amdgcn_readfirstlane(tree_first(n, T.L, i));
             const int b = __builtin_amdgcn_readfirstlane(tree_first(n, T.L, i + 1));
             bool acc = false;
@@ -425,7 +438,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
                 const int ai = c0 + lane;
                 float lbA = INFINITY;
                 if (ai < nA) lbA = box_lb3(box_lo + 3 * (firstA + ai), box_hi + 3 * (firstA + ai), fx, fy, fz);
-                ++n_box;
+                LRF_COUNT(++n_box);
 #if SE3ICP_LRF_ORDER == 1
                 // nearest first: the bound tightens fastest and the rest fall to it
                 for (;;) {
@@ -444,7 +457,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
                     float lbL = INFINITY;
                     if ((int)(lane < (1 << sh)) & ((int)(li < s_lo) | (int)(li > s_hi)))
                         lbL = box_lb3(box_lo + 3 * (first_leaf + li), box_hi + 3 * (first_leaf + li), fx, fy, fz);
-                    ++n_box;
+                    LRF_COUNT(++n_box);
 #if SE3ICP_LRF_ORDER == 1
                     for (;;) {
                         const float ml = wave_minf(lbL);
@@ -465,7 +478,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
         // exact order of the survivors
         PROF_NOW(t_q1);
         PROF_ADD(c_knn, t_q0, t_q1);
-        n_cand += nb;
+        LRF_COUNT(n_cand += nb);
         if (nb > 128) select_thr();
         __builtin_amdgcn_wave_barrier();
         {
@@ -596,8 +609,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
     }
 
     // ---------------------------------------------------------------- batched eigen-solves
-    // lane j < kQ solves query j's 3x3 problems: one solve per kQ queries instead of one
-    // per query on a whole wave
+    // Wave 0 solves the 3x3 problems of the block's kWaves * kQ = 32 queries, lane
+    // wq * kQ + j for query j of wave wq: one solve per 32 queries instead of one per
+    // kQ queries on each wave (the other waves' SIMD slots go to other blocks meanwhile).
     __builtin_amdgcn_wave_barrier();
     if (write_knn) {  // se3icp_knn_self: the sorted lists
         for (int j = 0; j < kQ; ++j) {
@@ -608,65 +622,74 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
             for (int r = lane; r < K; r += 64) out[r] = s_nbw[j * v.kmax + r];
         }
     }
-    const double* pl = park + (lane < kQ ? lane : 0) * PK_N;
-    const int my_flags = lane < kQ ? (int)pl[PK_FLAGS] : 0;
-    const int my_gp = (int)pl[PK_GP];
-    d3 zn{0, 0, 0};
-    if (my_flags & 1) {
-        // C = sum over ranks 1..rz of (v - cl)(v - cl)^T with the quirk centroid
-        // cl = c - q = (S' - q) / rz  (c = (ranks 1..rz-1 summed) / rz, ISR.cpp:259-265)
-        const int w = w0 + lane;
-        const double rz = (double)((int)pl[PK_KK] / 3);
-        const double q3[3] = {TX[w], TY[w], TZ[w]};
-        double cl[3], S[3];
+    __syncthreads();
+    if (wid == 0) {
+        static_assert(kWaves * kQ <= 64, "one lane per query of the block");
+        double* pb = &s_park[lane < kWaves * kQ ? lane / kQ : 0][lane % kQ][0];
+        const int b_flags = lane < kWaves * kQ ? (int)pb[PK_FLAGS] : 0;
+        const int wb = bid * kWaves * kQ + lane;  // the query's tree slot
+        d3 zn{0, 0, 0};
+        if (b_flags & 1) {
+            // C = sum over ranks 1..rz of (v - cl)(v - cl)^T with the quirk centroid
+            // cl = c - q = (S' - q) / rz  (c = (ranks 1..rz-1 summed) / rz, ISR.cpp:259-265)
+            const double rz = (double)((int)pb[PK_KK] / 3);
+            const double q3[3] = {TX[wb], TY[wb], TZ[wb]};
+            double cl[3], S[3];
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            cl[a] = (pl[PK_SUM + a] - q3[a]) / rz;
-            S[a] = pl[PK_SUM + 3 + a];
+            for (int a = 0; a < 3; ++a) {
+                cl[a] = (pb[PK_SUM + a] - q3[a]) / rz;
+                S[a] = pb[PK_SUM + 3 + a];
+            }
+            const double* M = pb + PK_SUM + 6;
+            const int ia[6] = {0, 0, 0, 1, 1, 2}, ib[6] = {0, 1, 2, 1, 2, 2};
+            double c6[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k)
+                c6[k] = M[k] - S[ia[k]] * cl[ib[k]] - cl[ia[k]] * S[ib[k]] + rz * cl[ia[k]] * cl[ib[k]];
+            zn = jacobi_smallest_evec(c6[0], c6[1], c6[2], c6[3], c6[4], c6[5]);
         }
-        const double* M = pl + PK_SUM + 6;
-        const int ia[6] = {0, 0, 0, 1, 1, 2}, ib[6] = {0, 1, 2, 1, 2, 2};
-        double c6[6];
+        if (b_flags & 2) {
+            const int c = v.cloud_of[wb];
+            const int kn = min(v.setup[c].k_nrm, (int)pb[PK_NTOP]);
+            double n6[6] = {1, 0, 0, 1, 0, 1};
+            if (kn >= 3) {
+                double cu[9];
 #pragma unroll
-        for (int k = 0; k < 6; ++k)
-            c6[k] = M[k] - S[ia[k]] * cl[ib[k]] - cl[ia[k]] * S[ib[k]] + rz * cl[ia[k]] * cl[ib[k]];
-        zn = jacobi_smallest_evec(c6[0], c6[1], c6[2], c6[3], c6[4], c6[5]);
+                for (int i = 0; i < 9; ++i) cu[i] = pb[PK_SUM + 12 + i] / (double)kn;
+                n6[0] = cu[3] - cu[0] * cu[0];
+                n6[1] = cu[4] - cu[0] * cu[1];
+                n6[2] = cu[5] - cu[0] * cu[2];
+                n6[3] = cu[6] - cu[1] * cu[1];
+                n6[4] = cu[7] - cu[1] * cu[2];
+                n6[5] = cu[8] - cu[2] * cu[2];
+            }
+            d3 nm = fast_eigen3x3(n6[0], n6[1], n6[2], n6[3], n6[4], n6[5]);
+            if (sqrt(dot3(nm, nm)) == 0.0) nm = d3{0, 0, 1};
+            const int gp = (int)pb[PK_GP];
+            v.nrm64[gp] = nm.x;
+            v.nrm64[v.ld + gp] = nm.y;
+            v.nrm64[2 * (size_t)v.ld + gp] = nm.z;
+            if (v.setup[c].want_cov) {
+                double cv[6];
+                gicp_cov_from_normal(nm, 1e-3, cv);
+#pragma unroll
+                for (int r = 0; r < 6; ++r) v.cov64[(size_t)r * v.ld + gp] = cv[r];
+            }
+        }
+        if (b_flags & 1) {
+            pb[PK_ZN] = zn.x;
+            pb[PK_ZN + 1] = zn.y;
+            pb[PK_ZN + 2] = zn.z;
+        }
     }
-    if (my_flags & 2) {
-        const int c = v.cloud_of[w0 + lane];
-        const int kn = min(v.setup[c].k_nrm, (int)pl[PK_NTOP]);
-        double n6[6] = {1, 0, 0, 1, 0, 1};
-        if (kn >= 3) {
-            double cu[9];
-#pragma unroll
-            for (int i = 0; i < 9; ++i) cu[i] = pl[PK_SUM + 12 + i] / (double)kn;
-            n6[0] = cu[3] - cu[0] * cu[0];
-            n6[1] = cu[4] - cu[0] * cu[1];
-            n6[2] = cu[5] - cu[0] * cu[2];
-            n6[3] = cu[6] - cu[1] * cu[1];
-            n6[4] = cu[7] - cu[1] * cu[2];
-            n6[5] = cu[8] - cu[2] * cu[2];
-        }
-        d3 nm = fast_eigen3x3(n6[0], n6[1], n6[2], n6[3], n6[4], n6[5]);
-        if (sqrt(dot3(nm, nm)) == 0.0) nm = d3{0, 0, 1};
-        const int gp = my_gp;
-        v.nrm64[gp] = nm.x;
-        v.nrm64[v.ld + gp] = nm.y;
-        v.nrm64[2 * (size_t)v.ld + gp] = nm.z;
-        if (v.setup[c].want_cov) {
-            double cv[6];
-            gicp_cov_from_normal(nm, 1e-3, cv);
-#pragma unroll
-            for (int r = 0; r < 6; ++r) v.cov64[(size_t)r * v.ld + gp] = cv[r];
-        }
-    }
+    __syncthreads();
 
     // ---------------------------------------------------------------- TOLDI axes (ISR.cpp:286-306)
     __builtin_amdgcn_wave_barrier();  // (the eigen pass has read PK_SUM; the axis sums reuse it)
     {  // eight lanes per query again (see the sums pass)
         double* pj = park + qj * PK_N;
         const int flags = (int)pj[PK_FLAGS];
-        const double nx = __shfl(zn.x, qj, 64), ny = __shfl(zn.y, qj, 64), nz = __shfl(zn.z, qj, 64);
+        const double nx = pj[PK_ZN], ny = pj[PK_ZN + 1], nz = pj[PK_ZN + 2];
         double x6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         if (flags & 1) {
             const int w = w0 + qj;
@@ -700,37 +723,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
             for (int i = 0; i < 6; ++i) pj[PK_SUM + i] = x6[i];
         }
     }
-    __builtin_amdgcn_wave_barrier();
-    double acc3[3] = {0, 0, 0}, accs3[3] = {0, 0, 0};
-    if (my_flags & 1) {
+    // the frames, again on wave 0 for the block's 32 queries
+    __syncthreads();
+    if (wid == 0) {
+        const double* pb = &s_park[lane < kWaves * kQ ? lane / kQ : 0][lane % kQ][0];
+        const int b_flags = lane < kWaves * kQ ? (int)pb[PK_FLAGS] : 0;
+        if (b_flags & 1) {
+            const int w = bid * kWaves * kQ + lane;
+            const CloudSetup st = v.setup[v.cloud_of[w]];
+            const double qx = TX[w], qy = TY[w], qz = TZ[w];
+            d3 nrm{pb[PK_ZN], pb[PK_ZN + 1], pb[PK_ZN + 2]};
+            if (nrm.x * pb[PK_SUM] + nrm.y * pb[PK_SUM + 1] + nrm.z * pb[PK_SUM + 2] < 0.0)
+                nrm = d3{-nrm.x, -nrm.y, -nrm.z};  // ISR.cpp:298
+            const d3 zax = nrm;
+            const d3 accs{pb[PK_SUM + 3], pb[PK_SUM + 4], pb[PK_SUM + 5]};
+            d3 xax = accs - dot3(accs, zax) * zax;  // ISR.cpp:302-303 (no |x| = 0 guard, as the reference)
+            xax = (1.0 / sqrt(dot3(xax, xax))) * xax;
+            const d3 yax = cross3(zax, xax);  // ISR.cpp:306
+            const double al = st.alpha, be = st.beta;
+            const double f12[12] = {al * xax.x, al * xax.y, al * xax.z, al * yax.x, al * yax.y, al * yax.z,
+                                    al * zax.x, al * zax.y, al * zax.z, be * qx, be * qy, be * qz};
+            const int gp = (int)pb[PK_GP];
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            acc3[a] = pl[PK_SUM + a];
-            accs3[a] = pl[PK_SUM + 3 + a];
-        }
-    }
-    if (my_flags & 1) {
-        const int w = w0 + lane;
-        const CloudSetup st = v.setup[v.cloud_of[w]];
-        const double qx = TX[w], qy = TY[w], qz = TZ[w];
-        d3 nrm = zn;
-        if (nrm.x * acc3[0] + nrm.y * acc3[1] + nrm.z * acc3[2] < 0.0) nrm = d3{-nrm.x, -nrm.y, -nrm.z};  // ISR.cpp:298
-        const d3 zax = nrm;
-        const d3 accs{accs3[0], accs3[1], accs3[2]};
-        d3 xax = accs - dot3(accs, zax) * zax;  // ISR.cpp:302-303 (no |x| = 0 guard, as the reference)
-        xax = (1.0 / sqrt(dot3(xax, xax))) * xax;
-        const d3 yax = cross3(zax, xax);  // ISR.cpp:306
-        const double al = st.alpha, be = st.beta;
-        const double f12[12] = {al * xax.x, al * xax.y, al * xax.z, al * yax.x, al * yax.y, al * yax.z,
-                                al * zax.x, al * zax.y, al * zax.z, be * qx, be * qy, be * qz};
-        const int gp = my_gp;
-#pragma unroll
-        for (int r = 0; r < 12; ++r) {
-            v.fr64[(size_t)r * v.ld + gp] = f12[r];
-            // f32 copy: 12-D search vectors of targets (cf: translation rows = points,
-            // ISR.cpp:834-836) and the kd-tree grouping of sources
-            const double f32v = (st.cf_target && r >= 9) ? (r == 9 ? qx : (r == 10 ? qy : qz)) : f12[r];
-            v.fr32[(size_t)r * v.ld + gp] = (float)f32v;
+            for (int r = 0; r < 12; ++r) {
+                v.fr64[(size_t)r * v.ld + gp] = f12[r];
+                // f32 copy: 12-D search vectors of targets (cf: translation rows = points,
+                // ISR.cpp:834-836) and the kd-tree grouping of sources
+                const double f32v = (st.cf_target && r >= 9) ? (r == 9 ? qx : (r == 10 ? qy : qz)) : f12[r];
+                v.fr32[(size_t)r * v.ld + gp] = (float)f32v;
+            }
         }
     }
 #ifdef SE3ICP_PROF
