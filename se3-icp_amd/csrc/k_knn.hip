@@ -363,7 +363,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
             int base = 0;
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-                const bool keep = key_le(dk[s], ik[s], thr, thr_i);
+                // (d, point index) <= (thr, thr_i); the buffer holds tree slots, so the point
+                // index is looked up only after an exact truncation (thr_i set, rare)
+                bool keep = dk[s] < thr;
+                if (thr_i != INT_MAX) {
+                    const int li = (s * 64 + lane < nb) ? T.perm[ik[s]] : INT_MAX;
+                    keep |= (bool)((int)(dk[s] == thr) & (int)(li <= thr_i));
+                } else {
+                    keep |= dk[s] == thr;
+                }
                 const unsigned long long m = __ballot(keep);
                 if (keep) {
                     const int at = base + __popcll(m & ((1ull << lane) - 1ull));
@@ -377,11 +385,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
             tight = true;
             if (nb > kBuf - kLeafMax) {  // massive ties at the bound: exact sort and truncation
                 __builtin_amdgcn_wave_barrier();
+                for (int e = lane; e < nb; e += 64) bi[e] = T.perm[bi[e]];  // slots -> point indices
+                __builtin_amdgcn_wave_barrier();
                 wave_bitonic<4>(bd, bi, lane, nb);
                 __builtin_amdgcn_wave_barrier();
                 nb = Kw;
                 thr = bd[Kw - 1];
                 thr_i = bi[Kw - 1];
+                for (int e = lane; e < nb; e += 64) bi[e] = cl.off + T.pos[cl.off + bi[e]];  // and back
                 set_thr_f();
             }
             __builtin_amdgcn_wave_barrier();
@@ -394,18 +405,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
             const int b = __builtin_amdgcn_readfirstlane(tree_first(n, T.L, i + 1));
             bool acc = false;
             double d = DBL_MAX;
-            int li = INT_MAX;
+            const int slot = cl.off + a + lane;
             if (lane < b - a) {
-                const int slot = cl.off + a + lane;
-                li = T.perm[slot];
                 d = l2_3(qx, qy, qz, TX[slot], TY[slot], TZ[slot]);
-                acc = (bool)((int)!have_thr | (int)key_le(d, li, thr, thr_i));
+                // (d, point index) <= (thr, thr_i): the index matters only at d == thr after an
+                // exact truncation (rare), so the candidate is kept as its tree slot
+                bool eq = d == thr;
+                if (thr_i != INT_MAX) eq = (bool)((int)eq & (int)(T.perm[slot] <= thr_i));
+                acc = (bool)((int)!have_thr | (int)(d < thr) | (int)eq);
             }
             const unsigned long long m = __ballot(acc);
             if (acc) {
                 const int at = nb + __popcll(m & ((1ull << lane) - 1ull));
                 bd[at] = d;
-                bi[at] = li;
+                bi[at] = slot;
             }
             nb += __popcll(m);
             // the first bound from Kw candidates (a seeded bound is loose), then whenever the buffer fills
@@ -488,9 +501,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
             done = nb <= 128 ? wave_sort_u64<2>(bd, bi, lane, nb, lim) : wave_sort_u64<4>(bd, bi, lane, nb, lim);
             __builtin_amdgcn_wave_barrier();
 #endif
-            if (!done) {
+            if (!done) {  // exact (f64 d, point index) order; the lists keep tree slots
+                for (int e = lane; e < nb; e += 64) bi[e] = T.perm[bi[e]];
+                __builtin_amdgcn_wave_barrier();
                 if (nb <= 128) wave_bitonic<2>(bd, bi, lane, nb);
                 else wave_bitonic<4>(bd, bi, lane, nb);
+                __builtin_amdgcn_wave_barrier();
+                for (int e = lane; e < nb; e += 64) bi[e] = cl.off + T.pos[cl.off + bi[e]];
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -547,10 +564,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
         if (flags & 3) {
             const int w = w0 + qj;
             const int c = cloud_of[w];
-            const int off = clouds[c].off;
-            const double* X = v.xyz64 + off;
-            const double* Y = v.xyz64 + v.ld + off;
-            const double* Z = v.xyz64 + 2 * (size_t)v.ld + off;
+            const double* X = TX;  // the lists hold tree slots: tree-ordered coordinates
+            const double* Y = TY;
+            const double* Z = TZ;
             const double qx = TX[w], qy = TY[w], qz = TZ[w];
             const int nTop = (int)pj[PK_NTOP];
             const int* nbl = s_nbw + qj * v.kmax;
@@ -619,7 +635,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
             if (!((int)pj[PK_FLAGS] & 4)) continue;
             const int K = (int)pj[PK_K];
             int* out = v.knn + (size_t)(int)pj[PK_GP] * v.kmax;
-            for (int r = lane; r < K; r += 64) out[r] = s_nbw[j * v.kmax + r];
+            for (int r = lane; r < K; r += 64) {
+                const int sl = s_nbw[j * v.kmax + r];
+                out[r] = sl >= 0 ? T.perm[sl] : -1;
+            }
         }
     }
     __syncthreads();
@@ -693,10 +712,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
         double x6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         if (flags & 1) {
             const int w = w0 + qj;
-            const int off = v.clouds[v.cloud_of[w]].off;
-            const double* X = v.xyz64 + off;
-            const double* Y = v.xyz64 + v.ld + off;
-            const double* Z = v.xyz64 + 2 * (size_t)v.ld + off;
+            const double* X = TX;  // (tree slots, see the sums pass)
+            const double* Y = TY;
+            const double* Z = TZ;
             const double qx = TX[w], qy = TY[w], qz = TZ[w];
             const double R = pj[PK_R];
             const int kk = (int)pj[PK_KK];
