@@ -25,12 +25,17 @@ namespace {
             return SE3ICP_ERR_HIP;                                                                  \
         }                                                                                           \
     } while (0)
+#define SYNC_STREAM(st)                   \
+    do {                                  \
+        const int rc_ = sync_stream(st);  \
+        if (rc_) return rc_;              \
+    } while (0)
 
 double wall_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-enum Kind { KIND_ICP, KIND_SE3, KIND_CF, KIND_PURE };
+// Kind (KIND_ICP / SE3 / CF / PURE): pairmath.hpp
 
 struct MethodInfo {
     Kind kind;
@@ -67,12 +72,22 @@ int pinned(T*& p, size_t& cap, size_t count) {
     return 0;
 }
 
+// Wait for an event by polling: the loop's host side has nothing else to do, and a
+// blocking wait adds the thread's wake-up latency to every step.
+hipError_t spin_wait(hipEvent_t e) {
+    for (;;) {
+        const hipError_t r = hipEventQuery(e);
+        if (r != hipErrorNotReady) return r;
+    }
+}
+
 constexpr int kStatSlots = 64;  // work counters: [64][kStatCols] u64 (spread against atomic contention)
 
 }  // namespace
 
 Engine::Engine(int device) : dev_(device) {
     for (auto& e : ev_) e = nullptr;
+    for (auto& e : loop_ev_) e = nullptr;
     ok_ = init() == 0;
 }
 
@@ -82,6 +97,7 @@ int Engine::init() {
     HIPCHK(hipSetDevice(dev_));
     HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     for (auto& e : ev_) HIPCHK(hipEventCreate(&e));
+    for (auto& e : loop_ev_) HIPCHK(hipEventCreate(&e));
     if (const char* e = std::getenv("SE3ICP_L12_EXTRA")) l12_extra_ = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = std::getenv("SE3ICP_NN_TRACE")) nn_trace_ = std::atoi(e) != 0;
     return 0;
@@ -95,7 +111,7 @@ Engine::~Engine() {
                      &d_corr_idx_, &d_corr_dist_, &d_flag_list_, &d_flag_count_, &d_trim_key_, &d_red_partial_,
                      &d_red_out_, &d_work_, &d_wb_, &d_wn_, &d_chunks_, &d_partial_, &d_centers_,
                      &d_rechecked_, &d_keys0_, &d_keys1_, &d_vals1_, &d_sort_tmp_, &d_stats_,
-                     &d_qlist_, &d_qcount_, &d_hist_, &d_cert_d1_, &d_cert_l2_, &d_cert_it_, &d_margin_, &d_sqlist_,
+                     &d_qlist_, &d_qcount_, &d_hist_, &d_cert_d1_, &d_cert_l2_, &d_cert_it_, &d_margin_, &d_sqlist_, &d_state_, &d_ctl_,
                      &t3_.perm, &t3_.pos, &t3_.vec, &t3_.blo, &t3_.bhi, &t3_.lo, &t3_.hi,
                      &t12_.perm, &t12_.pos, &t12_.vec, &t12_.blo, &t12_.bhi, &t12_.lo, &t12_.hi};
     for (DevBuf* b : all)
@@ -105,8 +121,13 @@ Engine::~Engine() {
     if (h_partial_) (void)hipHostFree(h_partial_);
     if (h_rechecked_) (void)hipHostFree(h_rechecked_);
     if (h_hist_) (void)hipHostFree(h_hist_);
+    if (h_lrf_stats_) (void)hipHostFree(h_lrf_stats_);
     for (auto& e : ev_)
         if (e) (void)hipEventDestroy(e);
+    for (auto& e : loop_ev_)
+        if (e) (void)hipEventDestroy(e);
+    if (h_state_) (void)hipHostFree(h_state_);
+    if (h_ctl_) (void)hipHostFree(h_ctl_);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -257,7 +278,7 @@ int Engine::root_norms(const TreeBufs& tb, int D, std::vector<float>* out, hipSt
                             nclouds_, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpy2DAsync(hi.data(), sizeof(float) * D, tb.hi.p, sizeof(float) * D * nnodes, sizeof(float) * D,
                             nclouds_, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    SYNC_STREAM(s);
     out->assign(nclouds_, 0.f);
     for (int c = 0; c < nclouds_; ++c) {
         double n2 = 0;
@@ -317,7 +338,7 @@ int Engine::setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool nor
     launch_ingest(v, (const ChunkWork*)d_chunks_.p, nch, (double*)d_partial_.p, s);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(h_partial_, d_partial_.p, sizeof(double) * 9 * nch, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    SYNC_STREAM(s);
     std::vector<double> cen(3 * nclouds_, 0.0);
     {
         std::vector<double> sum(3 * nclouds_, 0.0);
@@ -336,7 +357,7 @@ int Engine::setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool nor
         launch_radius(v, (const ChunkWork*)d_chunks_.p, nch, (const double*)d_centers_.p, (double*)d_partial_.p, s);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(h_partial_, d_partial_.p, sizeof(double) * nch, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        SYNC_STREAM(s);
         std::vector<double> rad(nclouds_, -1.0);
         for (int k = 0; k < nch; ++k) rad[h_chunks_[k].cloud] = std::max(rad[h_chunks_[k].cloud], h_partial_[k]);
         if (scales_out) scales_out->assign(nclouds_ / 2, 1.0);
@@ -381,24 +402,11 @@ int Engine::setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool nor
         launch_lrf(v, knn_list_ ? 1 : 0, s);
         HIPCHK(hipEventRecord(ev_[7], s));
         HIPCHK(hipGetLastError());
-        unsigned long long stats[kStatCols * kStatSlots];
-        HIPCHK(hipMemcpyAsync(stats, d_stats_.p, sizeof(stats), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        double sum[kStatCols] = {};
-        for (int i = 0; i < kStatSlots; ++i)
-            for (int k = 0; k < kStatCols; ++k) sum[k] += (double)stats[kStatCols * i + k];
-        float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, ev_[6], ev_[7]));
-        ktimes_.lrf_ms = ms;
-        ktimes_.lrf_queries = sum[0];
-        ktimes_.lrf_leaves = sum[1];
-        ktimes_.lrf_merges = sum[2];
-        ktimes_.lrf_box_tests = sum[3];
-        ktimes_.lrf_candidates = sum[4];
-#ifdef SE3ICP_PROF
-        std::fprintf(stderr, "[prof] k_lrf cycles/query: knn %.0f sort %.0f sums %.0f finish %.0f (queries %.0f)\n",
-                     sum[8] / sum[0], sum[9] / sum[0], sum[10] / sum[0], sum[11] / sum[0], sum[0]);
-#endif
+        // work counters: copied now, read at the next synchronisation (read_lrf_stats)
+        if (pinned(h_lrf_stats_, h_lrf_stats_cap_, (size_t)kStatCols * kStatSlots)) return SE3ICP_ERR_OUT_OF_MEMORY;
+        HIPCHK(hipMemcpyAsync(h_lrf_stats_, d_stats_.p, sizeof(unsigned long long) * kStatCols * kStatSlots,
+                              hipMemcpyDeviceToHost, s));
+        lrf_stats_pending_ = true;
     }
     HIPCHK(hipGetLastError());
     // 5) 12-D kd-trees over the alpha/beta-weighted SE(3) elements
@@ -408,6 +416,35 @@ int Engine::setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool nor
         if (rc) return rc;
     }
     return 0;
+}
+
+// k_lrf time and work counters of the last setup (after the stream has passed them)
+int Engine::read_lrf_stats() {
+    if (!lrf_stats_pending_) return 0;
+    lrf_stats_pending_ = false;
+    double sum[kStatCols] = {};
+    for (int i = 0; i < kStatSlots; ++i)
+        for (int k = 0; k < kStatCols; ++k) sum[k] += (double)h_lrf_stats_[kStatCols * i + k];
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, ev_[6], ev_[7]));
+    ktimes_.lrf_ms = ms;
+    ktimes_.lrf_queries = sum[0];
+    ktimes_.lrf_leaves = sum[1];
+    ktimes_.lrf_merges = sum[2];
+    ktimes_.lrf_box_tests = sum[3];
+    ktimes_.lrf_candidates = sum[4];
+#ifdef SE3ICP_PROF
+    std::fprintf(stderr, "[prof] k_lrf cycles/query: knn %.0f sort %.0f sums %.0f finish %.0f (queries %.0f)\n",
+                 sum[8] / sum[0], sum[9] / sum[0], sum[10] / sum[0], sum[11] / sum[0], sum[0]);
+#endif
+    return 0;
+}
+
+// Wait for everything queued on `s` (polling, see spin_wait).
+int Engine::sync_stream(hipStream_t s) {
+    HIPCHK(hipEventRecord(ev_[15], s));
+    HIPCHK(spin_wait(ev_[15]));
+    return read_lrf_stats();
 }
 
 // loop NN work chunks: nodes of level tree_L_ - 4 of every source tree (<= kChunkQ
@@ -513,151 +550,155 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     const double t_setup = wall_ms();
     ktimes_.setup_ms = t_setup - t_begin;
 
-    // ---- per-pair loop state (ISR.cpp:629-651)
-    struct St {
-        M4 T = M4::eye();
-        int iter = 0, pure = 0;
-        bool sw = false, done = false;
-        double mse_prev = 1e7, mse_cur = 1e7, rel = 1e7;
-        double sf = 1.0;
-        int nkeep = 0;
-        bool trim = false;
-        int phase = PHASE_IDLE, phase_start = 1;
-    };
-    std::vector<St> st(npairs);
+    // ---- per-pair loop state (ISR.cpp:629-651); iteration 1 is opened here, every later
+    // one by k_reduce_final on the device (pairmath.hpp), so the host only queues work
+    if (!ensure<PairState>(d_state_, npairs) || !ensure<int32_t>(d_ctl_, 8) || pinned(h_state_, h_state_cap_, npairs) ||
+        pinned(h_ctl_, h_ctl_cap_, 8 * kLoopRing))
+        return SE3ICP_ERR_OUT_OF_MEMORY;
     const float ratio = std::min(1.0f, std::max(0.0f, (float)prm.estimated_overlap));  // PCL setOverlapRatio(float)
+    int n_se3 = 0, n_r3 = 0;
+    bool any_trim = false;
     for (int p = 0; p < npairs; ++p) {
-        st[p].sf = se3 ? scales[p] : 1.0;
+        PairState& S = h_state_[p];
+        std::memset(&S, 0, sizeof(S));
+        S.T = M4::eye();
+        S.mse_prev = S.mse_cur = S.rel = 1e7;
+        S.sf = se3 ? scales[p] : 1.0;
+        S.mse = prm.mse;
+        S.mse_switch = prm.mse_switch_error;
+        S.kind = mi.kind;
+        S.max_iter = prm.max_num_iterations;
+        S.max_se3 = prm.max_num_se3_iterations;
+        S.phase = PHASE_IDLE;
+        S.phase_start = 1;
         const unsigned nv = (unsigned)std::floor(ratio * (float)ns[p]);
-        st[p].nkeep = (int)nv;
-        st[p].trim = (int64_t)nv < ns[p];
+        const bool trim = (int64_t)nv < ns[p];
+        S.K = trim ? (double)nv : (double)ns[p];
         PairDev& P = h_pairs_[p];
         std::memset(&P, 0, sizeof(P));
         P.src = 2 * p;
         P.tgt = 2 * p + 1;
         P.est = mi.est;
         P.cf = mi.kind == KIND_CF;
-        P.trim = st[p].trim;
-        P.nkeep = st[p].nkeep;
+        P.trim = trim;
+        P.nkeep = (int)nv;
         P.tgt_norm12 = se3 ? n12[2 * p + 1] : 0.f;
         P.tgt_norm3 = n3[2 * p + 1];
         for (int a = 0; a < 3; ++a) P.f32_center[a] = h_setup_[2 * p].f32_center[a];
+        pair_open_iteration(S, P);
+        std::memcpy(h_hist_ + 12 * (size_t)p, P.T, sizeof(P.T));
+        n_se3 += P.phase == PHASE_SE3;
+        n_r3 += P.phase == PHASE_R3;
+        any_trim |= trim;
     }
+    HIPCHK(hipMemcpyAsync(d_pairs_.p, h_pairs_, sizeof(PairDev) * npairs, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_state_.p, h_state_, sizeof(PairState) * npairs, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync((double*)d_hist_.p + (size_t)(1 % kHist) * npairs * 12, h_hist_, sizeof(double) * 12 * npairs,
+                          hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(d_flag_count_.p, 0, 3 * sizeof(int32_t), s));
+    HIPCHK(hipMemsetAsync(d_ctl_.p, 0, 8 * sizeof(int32_t), s));
     View v = view();
     const int recheck_blocks = 512;
     double nn_ms = 0;
-    int active = npairs;
-    while (active > 0) {
-        bool any_se3 = false, any_r3 = false, any_trim = false;
-        int hist_row = 0;
-        for (int p = 0; p < npairs; ++p) {
-            PairDev& P = h_pairs_[p];
-            St& S = st[p];
-            if (S.done) { P.phase = PHASE_IDLE; continue; }
-            S.iter++;                                                 // ISR.cpp:656
-            const bool se3_nn = (mi.kind == KIND_PURE) || (se3 && !S.sw);
-            if (se3_nn) S.pure++;                                     // ISR.cpp:660
-            P.phase = se3_nn ? PHASE_SE3 : PHASE_R3;
-            if (P.phase != S.phase) {  // NN certificates of the other metric are void
-                S.phase = P.phase;
-                S.phase_start = S.iter;
-            }
-            P.iter = S.iter;
-            P.phase_start = S.phase_start;
-            for (int r = 0; r < 3; ++r)
-                for (int c = 0; c < 4; ++c) P.T[r * 4 + c] = S.T.m[r][c];
-            std::memcpy(h_hist_ + 12 * (size_t)p, P.T, sizeof(P.T));
-            hist_row = S.iter;  // equal for every active pair (lockstep)
-            any_se3 |= se3_nn;
-            any_r3 |= !se3_nn;
-            any_trim |= S.trim;
-        }
-        HIPCHK(hipMemcpyAsync(d_pairs_.p, h_pairs_, sizeof(PairDev) * npairs, hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemcpyAsync((double*)d_hist_.p + (size_t)(hist_row % kHist) * npairs * 12, h_hist_,
-                              sizeof(double) * 12 * npairs, hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemsetAsync(d_flag_count_.p, 0, 3 * sizeof(int32_t), s));
-        HIPCHK(hipEventRecord(ev_[0], s));
+    // Iteration `it` is queued while iteration it-1 still runs; the host then waits for
+    // it-1 and reads how many pairs iteration it has (counted by it-1's k_reduce_final).
+    // Zero means iteration `it` is empty and the loop is over.  NN grids of a phase are
+    // queued while any pair may be in it: SE(3) until a finished iteration shows none
+    // left, R3 from iteration 2 on (a pair may switch after any iteration).
+    // SE3ICP_NN_TRACE waits for every iteration (per-iteration work counters).
+    const int lag = nn_trace_ ? 0 : 1;
+    auto enqueue = [&](int it) -> int {
+        hipEvent_t* ev = &loop_ev_[(it % kLoopRing) * kLoopEv];
+        // SE(3) phase: iterations 1..max_num_se3_iterations at most (ISR.cpp:718-723, 1118)
+        const bool do_se3 =
+            n_se3 > 0 && (prm.max_num_se3_iterations < 1 || it <= prm.max_num_se3_iterations);
+        const bool do_r3 = n_r3 > 0 || (mi.kind != KIND_ICP && mi.kind != KIND_PURE && it >= 2);
+        // HIP events around the NN grids always (bench.py's roofline); around every other
+        // stage only when profiling (each marker costs the stream a few microseconds)
+        const bool detail = profile_ || nn_trace_;
+        if (detail) HIPCHK(hipEventRecord(ev[0], s));
         launch_nn_prep(v, s);
-        HIPCHK(hipEventRecord(ev_[8], s));
-        if (any_se3) launch_nn_se3(v, s);
-        HIPCHK(hipEventRecord(ev_[1], s));
-        if (any_r3) launch_nn_r3(v, s);
-        HIPCHK(hipEventRecord(ev_[2], s));
+        HIPCHK(hipEventRecord(ev[1], s));
+        if (do_se3) launch_nn_se3(v, s);
+        HIPCHK(hipEventRecord(ev[2], s));
+        if (do_r3) launch_nn_r3(v, s);
+        HIPCHK(hipEventRecord(ev[3], s));
         launch_recheck(v, recheck_blocks, s);
-        HIPCHK(hipEventRecord(ev_[3], s));
+        if (detail) HIPCHK(hipEventRecord(ev[4], s));
         if (any_trim) launch_trim(v, s);
-        HIPCHK(hipEventRecord(ev_[4], s));
-        launch_reduce(v, (const int32_t*)d_wb_.p, (const int32_t*)d_wn_.p, s);
-        HIPCHK(hipEventRecord(ev_[5], s));
+        if (detail) HIPCHK(hipEventRecord(ev[5], s));
+        launch_reduce(v, (const int32_t*)d_wb_.p, (const int32_t*)d_wn_.p, (PairState*)d_state_.p, (double*)d_hist_.p,
+                      (int32_t*)d_ctl_.p, it, s);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(h_red_, d_red_out_.p, sizeof(double) * kRedVals * npairs, hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
-        {
-            float ms[5];
-            for (int k = 0; k < 5; ++k) HIPCHK(hipEventElapsedTime(&ms[k], ev_[k], ev_[k + 1]));
-            float prep_ms = 0;
-            HIPCHK(hipEventElapsedTime(&prep_ms, ev_[0], ev_[8]));
-            ms[0] -= prep_ms;
-            ktimes_.nn_prep_ms += prep_ms;
-            ktimes_.nn_se3_ms += ms[0];
-            ktimes_.nn_r3_ms += ms[1];
-            ktimes_.recheck_ms += ms[2];
-            ktimes_.trim_ms += ms[3];
-            ktimes_.reduce_ms += ms[4];
-            nn_ms += prep_ms + ms[0] + ms[1] + ms[2];
-            if (nn_trace_) {  // per-iteration NN work (diagnostics): diffs of the device counters
-                unsigned long long stats[kStatCols * kStatSlots];
-                HIPCHK(hipMemcpy(stats, d_stats_.p, sizeof(stats), hipMemcpyDeviceToHost));
-                double sum[kStatCols] = {};
-                for (int i = 0; i < kStatSlots; ++i)
-                    for (int k = 0; k < kStatCols; ++k) sum[k] += (double)stats[kStatCols * i + k];
-                std::fprintf(stderr,
-                             "[nn] iter %d: se3 %.0f/%.0f searched, evals %.3g boxes %.3g | r3 %.0f/%.0f, evals %.3g "
-                             "boxes %.3g | prep %.3f nn12 %.3f nn3 %.3f recheck %.3f ms\n",
-                             hist_row, sum[5] - trace_prev_[5], sum[4] - trace_prev_[4], sum[0] - trace_prev_[0],
-                             sum[1] - trace_prev_[1], sum[7] - trace_prev_[7], sum[6] - trace_prev_[6],
-                             sum[2] - trace_prev_[2], sum[3] - trace_prev_[3], prep_ms, ms[0], ms[1], ms[2]);
-                for (int k = 0; k < kStatCols; ++k) trace_prev_[k] = sum[k];
-            }
-            if (any_se3) ktimes_.nn_se3_launches++;
-            if (any_r3) ktimes_.nn_r3_launches++;
+        HIPCHK(hipMemcpyAsync(h_ctl_ + 4 * (it % kLoopRing), (int32_t*)d_ctl_.p + 4 * (it & 1), 4 * sizeof(int32_t),
+                              hipMemcpyDeviceToHost, s));
+        HIPCHK(hipEventRecord(ev[6], s));
+        loop_detail_[it % kLoopRing] = detail;
+        loop_flags_[it % kLoopRing] = (do_se3 ? 1 : 0) | (do_r3 ? 2 : 0);
+        return 0;
+    };
+    // wait for iteration `it`, add its kernel times; returns the pairs of iteration it+1
+    auto finish = [&](int it) -> int {
+        hipEvent_t* ev = &loop_ev_[(it % kLoopRing) * kLoopEv];
+        HIPCHK(spin_wait(ev[6]));
+        float ms[6] = {};
+        for (int k = 1; k < 3; ++k) HIPCHK(hipEventElapsedTime(&ms[k], ev[k], ev[k + 1]));
+        if (loop_detail_[it % kLoopRing]) {
+            HIPCHK(hipEventElapsedTime(&ms[0], ev[0], ev[1]));
+            for (int k = 3; k < 6; ++k) HIPCHK(hipEventElapsedTime(&ms[k], ev[k], ev[k + 1]));
         }
-        for (int p = 0; p < npairs; ++p) {
-            St& S = st[p];
-            if (S.done) continue;
-            const double* acc = h_red_ + (size_t)p * kRedVals;
-            const double K = S.trim ? (double)S.nkeep : (double)ns[p];
-            // ISR.cpp:684-686 (mean of the kept distances; NaN when nothing is kept, as the reference)
-            S.mse_prev = S.mse_cur;
-            S.mse_cur = acc[27] / K;
-            S.rel = std::fabs(S.mse_cur - S.mse_prev);
-            // ISR.cpp:689-703 estimator
-            M4 Ti;
-            if (K <= 0) Ti = M4::eye();
-            else if (mi.est == EST_PT2PT) Ti = umeyama_from_moments(acc, acc[15]);
-            else Ti = solve_normal_equations(acc);
-            // ISR.cpp:706-716: the source cloud and its SE(3) elements follow T on the fly
-            const M4 Tprev = S.T;
-            S.T = mul4(Ti, S.T);
-            const double change = frob_diff4(Tprev, S.T);
-            if (mi.kind == KIND_ICP) {  // ISR.cpp:547-550
-                if (S.iter == prm.max_num_iterations || S.rel < prm.mse) S.done = true;
-            } else if (mi.kind == KIND_PURE) {  // ISR.cpp:1118-1119
-                if (S.iter == prm.max_num_se3_iterations || S.rel < S.sf * prm.mse) S.done = true;
-            } else if (!S.sw) {  // ISR.cpp:718-723
-                if (S.iter == prm.max_num_se3_iterations || change < prm.mse_switch_error) S.sw = true;
-            } else {  // ISR.cpp:724-729
-                if (S.iter == prm.max_num_iterations || S.rel < S.sf * prm.mse) S.done = true;
-            }
-            if (S.iter >= 100000) S.done = true;  // the reference would loop forever
-            if (S.done) --active;
+        ktimes_.nn_prep_ms += ms[0];
+        ktimes_.nn_se3_ms += ms[1];
+        ktimes_.nn_r3_ms += ms[2];
+        ktimes_.recheck_ms += ms[3];
+        ktimes_.trim_ms += ms[4];
+        ktimes_.reduce_ms += ms[5];
+        nn_ms += ms[0] + ms[1] + ms[2] + ms[3];
+        const int flags = loop_flags_[it % kLoopRing];
+        if (flags & 1) ktimes_.nn_se3_launches++;
+        if (flags & 2) ktimes_.nn_r3_launches++;
+        if (nn_trace_) {  // per-iteration NN work (diagnostics): diffs of the device counters
+            unsigned long long stats[kStatCols * kStatSlots];
+            HIPCHK(hipMemcpy(stats, d_stats_.p, sizeof(stats), hipMemcpyDeviceToHost));
+            double sum[kStatCols] = {};
+            for (int i = 0; i < kStatSlots; ++i)
+                for (int k = 0; k < kStatCols; ++k) sum[k] += (double)stats[kStatCols * i + k];
+            std::fprintf(stderr,
+                         "[nn] iter %d: se3 %.0f/%.0f searched, evals %.3g boxes %.3g | r3 %.0f/%.0f, evals %.3g "
+                         "boxes %.3g | prep %.3f nn12 %.3f nn3 %.3f recheck %.3f ms\n",
+                         it, sum[5] - trace_prev_[5], sum[4] - trace_prev_[4], sum[0] - trace_prev_[0],
+                         sum[1] - trace_prev_[1], sum[7] - trace_prev_[7], sum[6] - trace_prev_[6],
+                         sum[2] - trace_prev_[2], sum[3] - trace_prev_[3], ms[0], ms[1], ms[2], ms[3]);
+            for (int k = 0; k < kStatCols; ++k) trace_prev_[k] = sum[k];
+        }
+        const int32_t* c = h_ctl_ + 4 * (it % kLoopRing);
+        n_se3 = c[1];
+        n_r3 = c[2];
+        return c[0];
+    };
+    static_assert(kLoopRing >= 2, "one iteration in flight while the previous one is read");
+    int it = 1;
+    if (enqueue(it)) return SE3ICP_ERR_HIP;
+    for (;;) {
+        if (lag == 0) {
+            if (finish(it) == 0) break;
+            ++it;
+            if (enqueue(it)) return SE3ICP_ERR_HIP;
+            continue;
+        }
+        ++it;
+        if (enqueue(it)) return SE3ICP_ERR_HIP;  // phase flags as of iteration it-2
+        if (finish(it - 1) == 0) {               // iteration `it` is empty
+            (void)finish(it);
+            break;
         }
     }
+    HIPCHK(hipMemcpyAsync(h_state_, d_state_.p, sizeof(PairState) * npairs, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(h_rechecked_, d_rechecked_.p, sizeof(int32_t) * npairs, hipMemcpyDeviceToHost, s));
     {
         unsigned long long stats[kStatCols * kStatSlots];
         HIPCHK(hipMemcpyAsync(stats, d_stats_.p, sizeof(stats), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        SYNC_STREAM(s);
         double sum[kStatCols] = {};
         for (int i = 0; i < kStatSlots; ++i)
             for (int k = 0; k < kStatCols; ++k) sum[k] += (double)stats[kStatCols * i + k];
@@ -678,7 +719,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
 
     int worst = 0;
     for (int p = 0; p < npairs; ++p) {
-        St& S = st[p];
+        const PairState& S = h_state_[p];
         M4 T = S.T;
         if (se3) {  // ISR.cpp:735-738 de-normalization
             const double* cs = &centers[3 * (2 * p)];
@@ -728,7 +769,7 @@ int Engine::knn_self(const double* xyz, int64_t n, int k, int32_t* idx) {
     if (rc) return rc;
     HIPCHK(hipMemcpy2DAsync(idx, sizeof(int32_t) * k, d_knn_.p, sizeof(int32_t) * kmax_, sizeof(int32_t) * k, n,
                             hipMemcpyDeviceToHost, stream_));
-    HIPCHK(hipStreamSynchronize(stream_));
+    SYNC_STREAM(stream_);
     return 0;
 }
 
@@ -753,7 +794,7 @@ int Engine::toldi_frames(const double* xyz, int64_t n, int k, double* frames) {
     if (rc) return rc;
     std::vector<double> fr(12 * (size_t)ld_);
     HIPCHK(hipMemcpyAsync(fr.data(), d_fr64_.p, sizeof(double) * 12 * ld_, hipMemcpyDeviceToHost, stream_));
-    HIPCHK(hipStreamSynchronize(stream_));
+    SYNC_STREAM(stream_);
     for (int64_t i = 0; i < n; ++i) {
         double* F = frames + 16 * i;
         // packing [R00 R10 R20 R01 R11 R21 R02 R12 R22 t0 t1 t2] -> row-major 4x4
@@ -786,7 +827,7 @@ int Engine::estimate_normals(const double* xyz, int64_t n, int k, double* normal
     if (rc) return rc;
     std::vector<double> nr(3 * (size_t)ld_);
     HIPCHK(hipMemcpyAsync(nr.data(), d_nrm64_.p, sizeof(double) * 3 * ld_, hipMemcpyDeviceToHost, stream_));
-    HIPCHK(hipStreamSynchronize(stream_));
+    SYNC_STREAM(stream_);
     for (int64_t i = 0; i < n; ++i)
         for (int a = 0; a < 3; ++a) normals[3 * i + a] = nr[(size_t)a * ld_ + i];
     return 0;
@@ -873,7 +914,7 @@ int Engine::nn(const double* query, int64_t nq, const double* data, int64_t nd, 
     HIPCHK(hipMemcpyAsync(idx, d_corr_idx_.p, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, s));
     int32_t rech = 0;
     HIPCHK(hipMemcpyAsync(&rech, d_rechecked_.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    SYNC_STREAM(s);
     if (num_rechecked) *num_rechecked = rech;
     if (d2) {
         for (int64_t i = 0; i < nq; ++i) {

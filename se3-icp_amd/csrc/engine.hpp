@@ -3,8 +3,9 @@
 // One Engine per HIP device.  register_batch() runs every pair of a batch in
 // lockstep: each iteration launches one grid per stage covering all active pairs
 // (pairs in the SE(3) phase and pairs already switched to the R3 phase share the
-// iteration), then reads back 28 doubles per pair and does the f64 solve and the
-// reference's switch / convergence logic (ISR.cpp:654-732) on the host.
+// iteration); the f64 solve and the reference's switch / convergence logic
+// (ISR.cpp:654-732) run on the device at the end of the iteration (pairmath.hpp), and
+// the host queues the next iteration before the previous one has finished.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -12,7 +13,7 @@
 #include <stdint.h>
 #include <vector>
 
-#include "hostmath.hpp"
+#include "pairmath.hpp"
 #include "se3icp.h"
 #include "view.hpp"
 
@@ -84,6 +85,8 @@ class Engine {
     int setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool normalize_pairs, double scale_pre,
                      bool build12, std::vector<double>* centers, std::vector<double>* scales, hipStream_t s);
     int setup_chunks(int npairs, hipStream_t s);
+    int read_lrf_stats();
+    int sync_stream(hipStream_t s);
     View view() const;
 
     int dev_;
@@ -114,7 +117,7 @@ class Engine {
         d_cov64_, d_conf64_, d_knn_, d_corr_idx_, d_corr_dist_, d_flag_list_, d_flag_count_,
         d_trim_key_, d_red_partial_, d_red_out_, d_work_, d_wb_, d_wn_, d_chunks_, d_partial_, d_centers_,
         d_rechecked_, d_keys0_, d_keys1_, d_vals1_, d_sort_tmp_, d_stats_, d_qlist_, d_qcount_, d_hist_, d_cert_d1_,
-        d_cert_l2_, d_cert_it_, d_margin_, d_sqlist_;
+        d_cert_l2_, d_cert_it_, d_margin_, d_sqlist_, d_state_, d_ctl_;
     TreeBufs t3_, t12_;
     // pinned host mirrors
     PairDev* h_pairs_ = nullptr;
@@ -123,7 +126,18 @@ class Engine {
     int32_t* h_rechecked_ = nullptr;
     double* h_hist_ = nullptr;  // one pose-history row (npairs x 12)
     size_t h_pairs_cap_ = 0, h_red_cap_ = 0, h_partial_cap_ = 0, h_rechecked_cap_ = 0, h_hist_cap_ = 0;
+    PairState* h_state_ = nullptr;  // loop state of every pair (read back after the loop)
+    int32_t* h_ctl_ = nullptr;      // [kLoopRing][4] pairs active in the next iteration (all, SE(3), R3)
+    size_t h_state_cap_ = 0, h_ctl_cap_ = 0;
+    unsigned long long* h_lrf_stats_ = nullptr;  // k_lrf work counters (read at the next sync)
+    size_t h_lrf_stats_cap_ = 0;
+    bool lrf_stats_pending_ = false;
     hipEvent_t ev_[16];
+    // loop iterations in flight: kernel-time events and launched NN phases per ring slot
+    static constexpr int kLoopRing = 4, kLoopEv = 7;
+    hipEvent_t loop_ev_[kLoopRing * kLoopEv];
+    int loop_flags_[kLoopRing] = {};
+    bool loop_detail_[kLoopRing] = {};
 };
 
 // process-wide engine per device (lazily created)

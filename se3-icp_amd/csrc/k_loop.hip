@@ -9,7 +9,8 @@
 //               pt2pt moments (umeyama, ISR.cpp:692), pt2pl JTJ/JTr (ISR.cpp:695),
 //               GICP JTJ/JTr with M^-1 = (Ct+Cs)^-1 (ISR.cpp:698, 57-110), MSE sum
 //               (ISR.cpp:379-400).  A second kernel sums the partials of each pair in
-//               a fixed order (deterministic).
+//               a fixed order (deterministic), solves the pair's step and advances its
+//               loop state on the device (pairmath.hpp).
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
@@ -17,6 +18,7 @@
 #include <cmath>
 
 #include "loopdev.hpp"
+#include "pairmath.hpp"
 #include "wave.hpp"
 #include "tree.hpp"
 
@@ -435,11 +437,22 @@ __global__ __launch_bounds__(256) void k_reduce(View v) {
 }
 
 // Sum each pair's block partials in block order (deterministic); the block list of
-// pair p is the contiguous work-table range where work[b].pair == p.
-__global__ __launch_bounds__(256) void k_reduce_final(View v, const int32_t* pair_wb, const int32_t* pair_wn) {
+// pair p is the contiguous work-table range where work[b].pair == p.  Then one lane
+// closes the pair's iteration `it` on the device (estimator solve, pose update,
+// switch / convergence: pairmath.hpp) and opens iteration it+1 (PairDev, pose history
+// row), so the next iteration's kernels are already queued behind this one.
+// ctl[it & 1][0..2] counts the pairs active in iteration it+1 (all, SE(3), R3).
+__global__ __launch_bounds__(256) void k_reduce_final(View v, const int32_t* pair_wb, const int32_t* pair_wn,
+                                                      PairState* state, double* hist, int32_t* ctl, int it) {
     const int p = blockIdx.x;
-    if (v.pairs[p].phase == PHASE_IDLE) return;
+    if ((int)(p == 0) & (int)(threadIdx.x < 4)) {
+        ctl[4 * ((it + 1) & 1) + threadIdx.x] = 0;             // counters of the next iteration
+        if (threadIdx.x < 3) v.flag_count[threadIdx.x] = 0;    // recheck / single-query lists
+    }
+    PairDev* P = v.pairs + p;
+    if (P->phase == PHASE_IDLE) return;
     __shared__ double part[8][kRedVals];
+    __shared__ double tot[kRedVals];
     const int i = threadIdx.x % kRedVals, s = threadIdx.x / kRedVals;
     const int wb = pair_wb[p], wn = pair_wn[p];
     if (s < 8) {
@@ -453,6 +466,21 @@ __global__ __launch_bounds__(256) void k_reduce_final(View v, const int32_t* pai
 #pragma unroll
         for (int k = 0; k < 8; ++k) sum += part[k][threadIdx.x];
         v.red_out[(size_t)p * kRedVals + threadIdx.x] = sum;
+        tot[threadIdx.x] = sum;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        PairState S = state[p];
+        pair_close_iteration(S, P->est, tot);
+        pair_open_iteration(S, *P);
+        state[p] = S;
+        if (!S.done) {
+            double* h = hist + ((size_t)(S.iter % kHist) * v.npairs + p) * 12;
+            for (int k = 0; k < 12; ++k) h[k] = P->T[k];
+            int32_t* c = ctl + 4 * (it & 1);
+            atomicAdd(c, 1);
+            atomicAdd(c + (P->phase == PHASE_SE3 ? 1 : 2), 1);
+        }
     }
 }
 
@@ -464,9 +492,10 @@ void launch_recheck(const View& v, int nblocks, hipStream_t s) {
 void launch_trim(const View& v, hipStream_t s) {
     hipLaunchKernelGGL(k_trim, dim3(v.npairs), dim3(1024), 0, s, v);
 }
-void launch_reduce(const View& v, const int32_t* pair_wb, const int32_t* pair_wn, hipStream_t s) {
+void launch_reduce(const View& v, const int32_t* pair_wb, const int32_t* pair_wn, PairState* state, double* hist,
+                   int32_t* ctl, int it, hipStream_t s) {
     hipLaunchKernelGGL(k_reduce, dim3(v.nwork), dim3(256), 0, s, v);
-    hipLaunchKernelGGL(k_reduce_final, dim3(v.npairs), dim3(256), 0, s, v, pair_wb, pair_wn);
+    hipLaunchKernelGGL(k_reduce_final, dim3(v.npairs), dim3(256), 0, s, v, pair_wb, pair_wn, state, hist, ctl, it);
 }
 
 }  // namespace se3icp

@@ -7,7 +7,7 @@ from ._lib import (MAX_KNN, METHODS, Params, Result, Se3IcpError, default_params
                    method_id, status_string)
 from .io import read_ply_xyz, write_ply_xyz  # noqa: F401
 from .registration import (IterativeSE3Registration, PairResult, cli_params, estimate_normals,  # noqa: F401
-                           kitti_params, knn_self, last_kernel_times, lounge_params, nearest_neighbors,
+                           kitti_params, knn_self, last_kernel_times, set_profiling, lounge_params, nearest_neighbors,
                            register_batch, register_batch_device, toldi_frames)
 
 __all__ = [

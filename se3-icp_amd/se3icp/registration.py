@@ -275,6 +275,11 @@ def nearest_neighbors(query, data, device: int = 0):
     return idx, d2, int(nr.value)
 
 
+def set_profiling(on: bool, device: int = 0) -> None:
+    """HIP events around every loop stage (not only the NN grids) from the next batch on."""
+    _lib.check(_lib.load().se3icp_set_profiling(device, 1 if on else 0))
+
+
 def last_kernel_times(device: int = 0) -> dict:
     out = (C.c_double * 23)()
     _lib.check(_lib.load().se3icp_last_kernel_times(device, out))
