@@ -22,6 +22,8 @@ constexpr int kBlock = 256;       // threads per block of the streaming/sweep ke
 constexpr int kRedVals = 28;      // 21 JTJ upper + 6 JTr + 1 mse-sum (pt2pt reuses the slots)
 constexpr int kStatCols = 12;     // columns of the device work-counter table (View::stats); 8..11: SE3ICP_PROF section cycles
 constexpr int kHist = 256;        // pose history ring of the loop (View::hist), iterations
+constexpr int kTrimList = 4096;   // k_trim: LDS key list / window capacity per pair
+constexpr int kTrimBlocks = 32;   // k_trim_window: blocks per pair
 constexpr int kChunkQ = 1024;     // source tree positions per NN work chunk (16 query groups)
 
 enum Phase : int32_t { PHASE_IDLE = 0, PHASE_SE3 = 1, PHASE_R3 = 2 };

@@ -111,7 +111,7 @@ Engine::~Engine() {
                      &d_corr_idx_, &d_corr_dist_, &d_flag_list_, &d_flag_count_, &d_trim_key_, &d_red_partial_,
                      &d_red_out_, &d_work_, &d_wb_, &d_wn_, &d_chunks_, &d_partial_, &d_centers_,
                      &d_rechecked_, &d_keys0_, &d_keys1_, &d_vals1_, &d_sort_tmp_, &d_stats_,
-                     &d_qlist_, &d_qcount_, &d_hist_, &d_cert_d1_, &d_cert_l2_, &d_cert_it_, &d_margin_, &d_sqlist_, &d_state_, &d_ctl_,
+                     &d_qlist_, &d_qcount_, &d_hist_, &d_cert_d1_, &d_cert_l2_, &d_cert_it_, &d_margin_, &d_sqlist_, &d_state_, &d_ctl_, &d_trim_cand_, &d_trim_ctr_,
                      &t3_.perm, &t3_.pos, &t3_.vec, &t3_.blo, &t3_.bhi, &t3_.lo, &t3_.hi,
                      &t12_.perm, &t12_.pos, &t12_.vec, &t12_.blo, &t12_.bhi, &t12_.lo, &t12_.hi};
     for (DevBuf* b : all)
@@ -195,6 +195,8 @@ View Engine::view() const {
     v.flag_list = (int32_t*)d_flag_list_.p;
     v.flag_count = (int32_t*)d_flag_count_.p;
     v.trim_key = (uint64_t*)d_trim_key_.p;
+    v.trim_cand = (unsigned long long*)d_trim_cand_.p;
+    v.trim_ctr = (unsigned*)d_trim_ctr_.p;
     v.red_partial = (double*)d_red_partial_.p;
     v.red_out = (double*)d_red_out_.p;
     v.work = (const BlockWork*)d_work_.p;
@@ -501,7 +503,8 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     int rc = alloc_points(ntot, kmax);
     if (rc) return rc;
     if (!ensure<PairDev>(d_pairs_, npairs) || !ensure<BlockWork>(d_work_, nwork_) || !ensure<int32_t>(d_wb_, npairs) ||
-        !ensure<int32_t>(d_wn_, npairs) || !ensure<uint64_t>(d_trim_key_, npairs) ||
+        !ensure<int32_t>(d_wn_, npairs) || !ensure<uint64_t>(d_trim_key_, 2 * (size_t)npairs) ||
+        !ensure<unsigned long long>(d_trim_cand_, (size_t)npairs * kTrimList) || !ensure<unsigned>(d_trim_ctr_, 4 * (size_t)npairs) ||
         !ensure<double>(d_red_partial_, (size_t)nwork_ * kRedVals) || !ensure<double>(d_red_out_, (size_t)npairs * kRedVals) ||
         !ensure<int32_t>(d_rechecked_, npairs))
         return SE3ICP_ERR_OUT_OF_MEMORY;
@@ -597,6 +600,8 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
                           hipMemcpyHostToDevice, s));
     HIPCHK(hipMemsetAsync(d_flag_count_.p, 0, 3 * sizeof(int32_t), s));
     HIPCHK(hipMemsetAsync(d_ctl_.p, 0, 8 * sizeof(int32_t), s));
+    HIPCHK(hipMemsetAsync((uint64_t*)d_trim_key_.p + npairs, 0, sizeof(uint64_t) * npairs, s));  // no trim window yet
+    HIPCHK(hipMemsetAsync(d_trim_ctr_.p, 0, sizeof(unsigned) * 4 * npairs, s));
     View v = view();
     const int recheck_blocks = 512;
     double nn_ms = 0;

@@ -4,7 +4,8 @@
 //   recheck     queries whose f32 arg-min k_nn.hip could not certify: an exact f64 sweep
 //               in nanoflann's arithmetic (ties -> lowest index).
 //   trim        PCL CorrespondenceRejectorTrimmed: the floor(ratio*N)-th smallest
-//               (float dist, query) key by MSB radix select (ISR.cpp:669-671).
+//               (float dist, query) key, from a window around the previous cut or by
+//               MSB radix select (ISR.cpp:669-671).
 //   reduce      per-correspondence Jacobian terms of the estimator, summed per block:
 //               pt2pt moments (umeyama, ISR.cpp:692), pt2pl JTJ/JTr (ISR.cpp:695),
 //               GICP JTJ/JTr with M^-1 = (Ct+Cs)^-1 (ISR.cpp:698, 57-110), MSE sum
@@ -178,30 +179,160 @@ __device__ __forceinline__ void hist_add_aggregated(unsigned* hist, bool act, un
     }
 }
 
-constexpr int kTrimList = 4096;
+__device__ __forceinline__ unsigned wsum_u32(unsigned x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
 
-// One 1024-thread block per trimming pair: the nkeep-th smallest 64-bit key
-// (float distance bits << 32 | query index) by MSB radix select.  The first digit
-// is the top 12 bits; further 8-bit digits are counted over all keys (global re-reads)
-// until the selected bin holds at most kTrimList keys, which are then compacted into
-// LDS where the remaining digits are resolved.
+
+// PCL CorrespondenceRejectorTrimmed (ISR.cpp:669-671): the nkeep-th smallest 64-bit
+// key (float distance bits << 32 | query index) of each trimming pair.
+//  * Window (from the 2nd iteration of a phase on): the cut distance moves little between
+//    ICP iterations, so k_trim_window (kTrimBlocks blocks per pair) counts the keys below
+//    [d_prev(1-w), d_prev(1+w)] and appends the keys inside it to a global list; k_trim
+//    ranks the list (each candidate counts the smaller ones, LDS broadcast reads) if the
+//    cut rank falls inside.  w adapts toward a few hundred keys.
+//  * Otherwise k_trim runs an MSB radix select: the first digit is the top 12 bits;
+//    further 8-bit digits are counted over all keys (global re-reads) until the selected
+//    bin holds at most kTrimList keys, which are then compacted into LDS where the
+//    remaining digits are resolved.
+// Both give the same key.  Window state: trim_key[npairs + pair] (f32 d_prev bits << 32 |
+// f32 w bits; 0 = none).  Per pair scratch: trim_cand[pair][kTrimList] and
+// trim_ctr[pair][4] = {in-window count, below count, -, -}, reset by k_trim.
+__device__ __forceinline__ unsigned long long trim_window_state(const View& v, const PairDev* P, int pair) {
+    // the first iteration of a phase has no usable window (the R3 cut is far below the SE(3) one)
+    return P->iter == P->phase_start ? 0ull : (unsigned long long)v.trim_key[v.npairs + pair];
+}
+
+__global__ __launch_bounds__(256) void k_trim_window(View v) {
+    constexpr int kLoc = 2048;  // in-window keys a block collects before one global append
+    __shared__ unsigned long long s_loc[kLoc];
+    __shared__ unsigned s_n, s_below, s_base;
+    const int pair = blockIdx.x / kTrimBlocks, sub = blockIdx.x % kTrimBlocks;
+    const PairDev* P = v.pairs + pair;
+    if ((int)(P->phase == PHASE_IDLE) | (int)(P->trim == 0) | (int)(P->nkeep <= 0)) return;
+    const unsigned long long wstate = trim_window_state(v, P, pair);
+    if (wstate == 0ull) return;
+    const int lane = threadIdx.x & 63;
+    const CloudDev cs = v.clouds[P->src];
+    const int n = cs.n;
+    const unsigned* dist = reinterpret_cast<const unsigned*>(v.corr_dist) + cs.off;
+    unsigned* ctr = v.trim_ctr + 4 * pair;
+    unsigned long long* cand = v.trim_cand + (size_t)pair * kTrimList;
+    const float dprev = __uint_as_float((unsigned)(wstate >> 32));
+    const float wv = __uint_as_float((unsigned)wstate);
+    const unsigned lo = __float_as_uint(dprev * (1.0f - wv));
+    const unsigned hi = __float_as_uint(dprev * (1.0f + wv));
+    const int per = ((n + kTrimBlocks - 1) / kTrimBlocks + 63) & ~63;
+    const int i_beg = sub * per, i_end = min(n, i_beg + per);
+    if (threadIdx.x == 0) { s_n = 0; s_below = 0; }
+    __syncthreads();
+    constexpr int U = 4;
+    unsigned below = 0;
+    for (int i0 = i_beg; i0 < i_end; i0 += U * blockDim.x) {
+        unsigned u[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int i = i0 + j * blockDim.x + threadIdx.x;
+            u[j] = i < i_end ? dist[i] : 0xffffffffu;
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const int i = i0 + j * blockDim.x + threadIdx.x;
+            below += (unsigned)((int)(i < i_end) & (int)(u[j] < lo));
+            const bool sel = (int)(i < i_end) & (int)(u[j] >= lo) & (int)(u[j] <= hi);
+            const unsigned long long m = __ballot(sel);
+            if (m == 0) continue;
+            unsigned base = 0;
+            if (lane == 0) base = atomicAdd(&s_n, (unsigned)__popcll(m));
+            base = __shfl(base, 0, 64);
+            const unsigned at = base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+            if ((int)sel & (int)(at < (unsigned)kLoc)) s_loc[at] = ((unsigned long long)u[j] << 32) | (unsigned)i;
+        }
+    }
+    below = wsum_u32(below);
+    if ((int)(lane == 0) & (int)(below > 0)) atomicAdd(&s_below, below);
+    __syncthreads();
+    // one global reservation per block (a block that overflowed its list forces a miss)
+    const unsigned nloc = s_n;
+    if (threadIdx.x == 0) {
+        s_base = nloc ? atomicAdd(ctr, nloc <= (unsigned)kLoc ? nloc : (unsigned)kTrimList + 1u) : 0u;
+        if (s_below) atomicAdd(ctr + 1, s_below);
+    }
+    __syncthreads();
+    const unsigned base = s_base;
+    if (nloc <= (unsigned)kLoc)
+        for (unsigned e = threadIdx.x; e < nloc; e += blockDim.x)
+            if (base + e < (unsigned)kTrimList) cand[base + e] = s_loc[e];
+}
+
+// One 1024-thread block per trimming pair (see above).
 __global__ __launch_bounds__(1024) void k_trim(View v) {
     __shared__ unsigned hist[4096];
     __shared__ unsigned long long s_list[kTrimList];
     __shared__ unsigned s_cnt;
     __shared__ int s_bin;
     __shared__ unsigned s_before;
-    const PairDev* P = v.pairs + blockIdx.x;
+    const int pair = blockIdx.x;
+    const PairDev* P = v.pairs + pair;
     if (P->phase == PHASE_IDLE || !P->trim) return;
     const CloudDev cs = v.clouds[P->src];
     const int n = cs.n;
     if (P->nkeep <= 0) {
-        if (threadIdx.x == 0) v.trim_key[blockIdx.x] = 0ull;  // keep none (handled by reduce)
+        if (threadIdx.x == 0) v.trim_key[pair] = 0ull;  // keep none (handled by reduce)
         return;
     }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const unsigned* dist = reinterpret_cast<const unsigned*>(v.corr_dist) + cs.off;
     constexpr int U = 8;  // independent loads in flight per thread
+    uint64_t* win = v.trim_key + v.npairs + pair;
+    unsigned* ctr = v.trim_ctr + 4 * pair;
+    const unsigned long long* cand = v.trim_cand + (size_t)pair * kTrimList;
+    const unsigned long long wstate = trim_window_state(v, P, pair);
+    float wv = wstate != 0ull ? __uint_as_float((unsigned)wstate) : 0.02f;
+    if (wstate != 0ull) {
+        const unsigned k = (unsigned)P->nkeep;  // rank (1-based) of the cut key
+        const unsigned cnt = ctr[0], nb = ctr[1];
+        const bool hit = cnt <= (unsigned)kTrimList && nb < k && k <= nb + cnt;
+        // adapt the window: too full -> halve, missed -> x4, sparse -> x1.5
+        if (cnt > 768u) wv *= 0.5f;
+        else if (!hit) wv *= 4.0f;
+        else if (cnt < 96u) wv *= 1.5f;
+        wv = fminf(wv, 0.9f);
+#ifdef SE3ICP_PROF
+        if (threadIdx.x == 0)
+            printf("[trim] it %d pair %d hit %d cnt %u below %u k %u dprev %g w %g\n", P->iter, pair, (int)hit, cnt,
+                   nb, k, (double)__uint_as_float((unsigned)(wstate >> 32)), (double)__uint_as_float((unsigned)wstate));
+#endif
+        if (hit) {
+            constexpr unsigned R = 16;  // independent LDS reads in flight per rank count
+            const unsigned cpad = (cnt + R - 1) & ~(R - 1);
+            for (unsigned e = threadIdx.x; e < cpad; e += blockDim.x) s_list[e] = e < cnt ? cand[e] : ~0ull;
+            __syncthreads();
+            const unsigned r = k - nb - 1;  // 0-based rank inside the window (keys are distinct)
+            for (unsigned e = threadIdx.x; e < cnt; e += blockDim.x) {
+                const unsigned long long key = s_list[e];
+                unsigned less = 0;
+                for (unsigned j = 0; j < cpad; j += R) {
+                    unsigned long long t[R];
+#pragma unroll
+                    for (unsigned q = 0; q < R; ++q) t[q] = s_list[j + q];
+#pragma unroll
+                    for (unsigned q = 0; q < R; ++q) less += (unsigned)(t[q] < key);
+                }
+                if (less == r) {
+                    v.trim_key[pair] = key;
+                    *win = (key & 0xffffffff00000000ull) | __float_as_uint(wv);
+                }
+            }
+            __syncthreads();
+            if (threadIdx.x < 2) ctr[threadIdx.x] = 0u;
+            return;
+        }
+        __syncthreads();
+        if (threadIdx.x < 2) ctr[threadIdx.x] = 0u;
+    }
     unsigned long long prefix = 0, mask = 0;
     unsigned k = (unsigned)P->nkeep;  // rank (1-based) within the keys matching prefix/mask
     unsigned sel_count = (unsigned)n;
@@ -277,7 +408,10 @@ __global__ __launch_bounds__(1024) void k_trim(View v) {
         pos += w;
         __syncthreads();
     }
-    if (threadIdx.x == 0) v.trim_key[blockIdx.x] = prefix;
+    if (threadIdx.x == 0) {
+        v.trim_key[pair] = prefix;
+        *win = (prefix & 0xffffffff00000000ull) | __float_as_uint(wv);
+    }
 }
 
 // ------------------------------------------------------------------ reduce
@@ -490,6 +624,7 @@ void launch_recheck(const View& v, int nblocks, hipStream_t s) {
     hipLaunchKernelGGL(k_recheck, dim3(nblocks), dim3(256), 0, s, v);
 }
 void launch_trim(const View& v, hipStream_t s) {
+    hipLaunchKernelGGL(k_trim_window, dim3(v.npairs * kTrimBlocks), dim3(256), 0, s, v);
     hipLaunchKernelGGL(k_trim, dim3(v.npairs), dim3(1024), 0, s, v);
 }
 void launch_reduce(const View& v, const int32_t* pair_wb, const int32_t* pair_wn, PairState* state, double* hist,

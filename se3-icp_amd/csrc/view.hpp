@@ -63,7 +63,9 @@ struct View {
     unsigned long long* stats;  // [4] NN work counters: se3 dist evals, se3 box tests, r3 dist evals, r3 box tests
     int32_t* flag_list;
     int32_t* flag_count;  // [3] recheck list, single-query lists (SE(3), R3)
-    uint64_t* trim_key;   // [npairs]
+    uint64_t* trim_key;   // [npairs] cut key, then [npairs] k_trim window state
+    unsigned long long* trim_cand;  // [npairs][kTrimList] k_trim window keys
+    unsigned* trim_ctr;   // [npairs][4] k_trim counters (zero between launches)
     double* red_partial;  // [nwork * kRedVals]
     double* red_out;      // [npairs * kRedVals]
     const BlockWork* work;
