@@ -162,6 +162,21 @@ int se3icp_estimate_normals(int device, const double* xyz, int64_t n, int k, dou
 int se3icp_nn(int device, const double* query, int64_t nq, const double* data, int64_t nd, int dim,
               int32_t* idx, double* d2, int32_t* num_rechecked);
 
+/* ------------------------------------------------------------- data generators
+ * The synthetic registration problems of examples/benchmark_synthetic.cpp:91-160
+ * (add_noise_to_point_cloud B_SYN:13-56, RandomDownSample, T_c applied to the target),
+ * generated on device `device` for n_cases cases at once: source_c = a random subset of
+ * k = (int)(ratio * n) points of `base` plus N(0, noise_var I) noise, target_c = an
+ * independent random subset of T_c * base plus noise.  base: host [n*3]; T: host
+ * [n_cases*16] row-major.  src_out / tgt_out: [n_cases*k*3] AoS, device pointers when
+ * outputs_on_device (ready for se3icp_register_batch_device with offsets c*k), host
+ * pointers otherwise.  Returns k (>= 0) or a negative se3icp_status.  Counter-based
+ * random streams (Philox4x32-10 keyed by `seed`): same distributions as the
+ * reference's mt19937 draws, not the same samples. */
+int64_t se3icp_synthetic_pairs(int device, const double* base, int64_t n, int32_t n_cases, const double* T,
+                               double ratio, double noise_var, uint64_t seed, double* src_out, double* tgt_out,
+                               int outputs_on_device);
+
 /* ------------------------------------------------------------- diagnostics
  * Not part of the reference boundary: per-kernel GPU times (HIP events) of the
  * last batch on `device`, used by bench.py for the roofline figures.

@@ -250,3 +250,44 @@ def bunny_pair(bunny_unique: np.ndarray, seed: int = 1, noise_var: float = 0.005
     src = src + rng.normal(0, sd, src.shape)
     tgt = tgt + rng.normal(0, sd, tgt.shape)
     return np.ascontiguousarray(src), np.ascontiguousarray(tgt), T
+
+
+def synthetic_cases(n_cases: int, seed: int = 1, easy: bool = False):
+    """Ground-truth transforms of examples/benchmark_synthetic.cpp:103-145: t ~ U(-tr, tr)^3,
+    R = rot_3d(U(-rr, rr)^3) with the "moderate" ranges active in the reference (10, pi/2)
+    or the "easy" ones (5, pi/4).  Host numpy (PCG64); returns [n_cases, 4, 4]."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    tr, rr = (5.0, np.pi / 4) if easy else (10.0, np.pi / 2)
+    Ts = []
+    for _ in range(n_cases):
+        t = rng.uniform(-tr, tr, 3)
+        Ts.append(make_T(rot_3d(*rng.uniform(-rr, rr, 3)), t))
+    return np.stack(Ts)
+
+
+def synthetic_pairs_gpu(base: np.ndarray, Ts: np.ndarray, ratio: float = 0.02, noise_var: float = 0.005,
+                        seed: int = 1, device: int = 0, out=None):
+    """The benchmark_synthetic.cpp:91-160 problems generated on the GPU (k_gen.hip,
+    se3icp_synthetic_pairs): for each T in Ts, an independent random subset of
+    k = int(ratio * n) points of `base` (source) and of T @ base (target), each plus
+    N(0, noise_var I).  With out=None returns host arrays (src [C, k, 3], tgt [C, k, 3]);
+    with out=(src_ptr, tgt_ptr) writes into device buffers and returns k."""
+    import ctypes as C
+    from . import _lib
+    b = np.ascontiguousarray(base, dtype=np.float64)
+    T = np.ascontiguousarray(Ts, dtype=np.float64).reshape(-1, 16)
+    dp = C.POINTER(C.c_double)
+    L = _lib.load()
+    if out is not None:
+        k = L.se3icp_synthetic_pairs(device, b.ctypes.data_as(dp), b.shape[0], T.shape[0], T.ctypes.data_as(dp),
+                                     ratio, noise_var, seed, C.c_void_p(out[0]), C.c_void_p(out[1]), 1)
+        _lib.check(int(min(k, 0)), "synthetic_pairs")
+        return int(k)
+    k = int(ratio * b.shape[0])
+    src = np.zeros((T.shape[0], max(k, 0), 3))
+    tgt = np.zeros_like(src)
+    r = L.se3icp_synthetic_pairs(device, b.ctypes.data_as(dp), b.shape[0], T.shape[0], T.ctypes.data_as(dp), ratio,
+                                 noise_var, seed, src.ctypes.data_as(C.c_void_p), tgt.ctypes.data_as(C.c_void_p), 0)
+    _lib.check(int(min(r, 0)), "synthetic_pairs")
+    assert r == k, (r, k)
+    return src, tgt

@@ -35,3 +35,21 @@ def fixture_T_gt():
 def bunny_unique():
     import numpy as np
     return np.load(os.path.join(GOLDEN, "bunny_unique_f32.npy")).astype(np.float64)
+
+
+_torch_gpu_ready = False
+
+
+def pytest_runtest_setup(item):
+    """GPU tests: bring up torch's HIP context before libse3icp's first HIP call, as
+    bench.py does (torch only plumbs device buffers for the tests that need them)."""
+    global _torch_gpu_ready
+    if _torch_gpu_ready or item.get_closest_marker("gpu") is None:
+        return
+    _torch_gpu_ready = True
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.init()
+    except Exception:  # the test itself reports a missing device
+        pass
