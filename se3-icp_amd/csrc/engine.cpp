@@ -111,7 +111,7 @@ Engine::~Engine() {
                      &d_corr_idx_, &d_corr_dist_, &d_flag_list_, &d_flag_count_, &d_trim_key_, &d_red_partial_,
                      &d_red_out_, &d_work_, &d_wb_, &d_wn_, &d_chunks_, &d_partial_, &d_centers_,
                      &d_rechecked_, &d_keys0_, &d_keys1_, &d_vals1_, &d_sort_tmp_, &d_stats_,
-                     &d_qlist_, &d_qcount_, &d_hist_, &d_cert_d1_, &d_cert_l2_, &d_cert_it_, &d_margin_, &d_sqlist_, &d_state_, &d_ctl_, &d_trim_cand_, &d_trim_ctr_,
+                     &d_qlist_, &d_qcount_, &d_hist_, &d_cert_d1_, &d_cert_l2_, &d_cert_it_, &d_margin_, &d_sqlist_, &d_state_, &d_ctl_, &d_trim_cand_, &d_trim_ctr_, &d_scales_,
                      &t3_.perm, &t3_.pos, &t3_.vec, &t3_.blo, &t3_.bhi, &t3_.lo, &t3_.hi,
                      &t12_.perm, &t12_.pos, &t12_.vec, &t12_.blo, &t12_.bhi, &t12_.lo, &t12_.hi};
     for (DevBuf* b : all)
@@ -272,27 +272,6 @@ int Engine::build_tree(int D, const float* vec, hipStream_t s, const double* vec
     return 0;
 }
 
-// Upper bound of |x| over each cloud's tree vectors, from the (inflated) root box.
-int Engine::root_norms(const TreeBufs& tb, int D, std::vector<float>* out, hipStream_t s) {
-    const int nnodes = 2 << tb.L;
-    std::vector<float> lo((size_t)nclouds_ * D), hi((size_t)nclouds_ * D);
-    HIPCHK(hipMemcpy2DAsync(lo.data(), sizeof(float) * D, tb.lo.p, sizeof(float) * D * nnodes, sizeof(float) * D,
-                            nclouds_, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipMemcpy2DAsync(hi.data(), sizeof(float) * D, tb.hi.p, sizeof(float) * D * nnodes, sizeof(float) * D,
-                            nclouds_, hipMemcpyDeviceToHost, s));
-    SYNC_STREAM(s);
-    out->assign(nclouds_, 0.f);
-    for (int c = 0; c < nclouds_; ++c) {
-        double n2 = 0;
-        for (int d = 0; d < D; ++d) {
-            const double m = std::max(std::fabs((double)lo[(size_t)c * D + d]), std::fabs((double)hi[(size_t)c * D + d]));
-            n2 += m * m;
-        }
-        (*out)[c] = (float)(std::sqrt(n2) * (1.0 + 1e-6));
-    }
-    return 0;
-}
-
 // ----------------------------------------------------------------------------- setup
 int Engine::setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool normalize_pairs, double scale_pre,
                          bool build12, std::vector<double>* centers_out, std::vector<double>* scales_out,
@@ -339,43 +318,34 @@ int Engine::setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool nor
     // 1) ingest: SoA copy + sums + bbox
     launch_ingest(v, (const ChunkWork*)d_chunks_.p, nch, (double*)d_partial_.p, s);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(h_partial_, d_partial_.p, sizeof(double) * 9 * nch, hipMemcpyDeviceToHost, s));
-    SYNC_STREAM(s);
-    std::vector<double> cen(3 * nclouds_, 0.0);
-    {
-        std::vector<double> sum(3 * nclouds_, 0.0);
-        for (int k = 0; k < nch; ++k) {
-            const int c = h_chunks_[k].cloud;
-            for (int a = 0; a < 3; ++a) sum[3 * c + a] += h_partial_[9 * k + a];
-        }
-        for (int c = 0; c < nclouds_; ++c)
-            for (int a = 0; a < 3; ++a) cen[3 * c + a] = clouds[c].n > 0 ? sum[3 * c + a] / (double)clouds[c].n : 0.0;
-    }
-    if (centers_out) *centers_out = cen;
-
-    // 2) normalization parameters (ISR.cpp:568-574)
     if (normalize_pairs) {
-        HIPCHK(hipMemcpyAsync(d_centers_.p, cen.data(), sizeof(double) * 3 * nclouds_, hipMemcpyHostToDevice, s));
+        // 2) normalization parameters (ISR.cpp:568-574) on the device: no host round trip;
+        // the centers (d_centers_) and scales (d_scales_) stay there for the loop and the
+        // final de-normalization
+        if (!ensure<double>(d_scales_, std::max(1, nclouds_ / 2))) return SE3ICP_ERR_OUT_OF_MEMORY;
+        launch_pair_centers(v, (const ChunkWork*)d_chunks_.p, nch, (const double*)d_partial_.p, (double*)d_centers_.p,
+                            s);
         launch_radius(v, (const ChunkWork*)d_chunks_.p, nch, (const double*)d_centers_.p, (double*)d_partial_.p, s);
+        launch_pair_scales(v, (const ChunkWork*)d_chunks_.p, nch, (const double*)d_partial_.p,
+                           (const double*)d_centers_.p, scale_pre, (double*)d_scales_.p, s);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(h_partial_, d_partial_.p, sizeof(double) * nch, hipMemcpyDeviceToHost, s));
-        SYNC_STREAM(s);
-        std::vector<double> rad(nclouds_, -1.0);
-        for (int k = 0; k < nch; ++k) rad[h_chunks_[k].cloud] = std::max(rad[h_chunks_[k].cloud], h_partial_[k]);
-        if (scales_out) scales_out->assign(nclouds_ / 2, 1.0);
-        for (int p = 0; p < nclouds_ / 2; ++p) {
-            const double rmax = std::max(rad[2 * p], rad[2 * p + 1]);
-            const double sf = scale_pre * (1.0 / rmax);
-            for (int c = 2 * p; c <= 2 * p + 1; ++c) {
-                for (int a = 0; a < 3; ++a) {
-                    h_setup_[c].norm_center[a] = cen[3 * c + a];
-                    h_setup_[c].f32_center[a] = 0.0;
-                }
-                h_setup_[c].norm_scale = sf;
-            }
-            if (scales_out) (*scales_out)[p] = sf;
-        }
+        for (int c = 0; c < nclouds_; ++c)  // (the device holds the normalization fields)
+            for (int a = 0; a < 3; ++a) h_setup_[c].f32_center[a] = 0.0;
     } else {
+        HIPCHK(hipMemcpyAsync(h_partial_, d_partial_.p, sizeof(double) * 9 * nch, hipMemcpyDeviceToHost, s));
+        SYNC_STREAM(s);
+        std::vector<double> cen(3 * nclouds_, 0.0);
+        {
+            std::vector<double> sum(3 * nclouds_, 0.0);
+            for (int k = 0; k < nch; ++k) {
+                const int c = h_chunks_[k].cloud;
+                for (int a = 0; a < 3; ++a) sum[3 * c + a] += h_partial_[9 * k + a];
+            }
+            for (int c = 0; c < nclouds_; ++c)
+                for (int a = 0; a < 3; ++a)
+                    cen[3 * c + a] = clouds[c].n > 0 ? sum[3 * c + a] / (double)clouds[c].n : 0.0;
+        }
+        if (centers_out) *centers_out = cen;
         for (int c = 0; c < nclouds_; ++c) {
             // raw coordinates; f32 copies centered on the target (pairs) / own centroid (single clouds)
             const int cc = (nclouds_ % 2 == 0 && npairs_ > 0) ? (c | 1) : c;
@@ -385,8 +355,8 @@ int Engine::setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool nor
             }
             h_setup_[c].norm_scale = 1.0;
         }
+        HIPCHK(hipMemcpyAsync(d_setup_.p, h_setup_.data(), sizeof(CloudSetup) * nclouds_, hipMemcpyHostToDevice, s));
     }
-    HIPCHK(hipMemcpyAsync(d_setup_.p, h_setup_.data(), sizeof(CloudSetup) * nclouds_, hipMemcpyHostToDevice, s));
 
     // 3) normalize in place + f32 copy
     launch_normalize(v, (const ChunkWork*)d_chunks_.p, nch, (double*)d_partial_.p, s);
@@ -537,19 +507,14 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
             st.norm_scale = 1.0;
         }
     }
-    std::vector<double> centers, scales;
-    rc = setup_clouds(clouds, on_device, se3, prm.scale_preprocessing, se3, &centers, &scales, s);
+    std::vector<double> centers;  // run_icp only (run_se3_*: normalization parameters on the device)
+    rc = setup_clouds(clouds, on_device, se3, prm.scale_preprocessing, se3, &centers, nullptr, s);
     if (rc) return rc;
     rc = setup_chunks(npairs, s);
     if (rc) return rc;
     HIPCHK(hipMemsetAsync(d_corr_idx_.p, 0xff, sizeof(int32_t) * ld_, s));  // no previous match yet
     HIPCHK(hipMemsetAsync(d_stats_.p, 0, sizeof(unsigned long long) * kStatCols * kStatSlots, s));
     for (double& t : trace_prev_) t = 0;
-    // norm bounds of the target search vectors (f32 error certificate) from the root boxes
-    std::vector<float> n12, n3;
-    rc = root_norms(t3_, 3, &n3, s);
-    if (!rc && se3) rc = root_norms(t12_, 12, &n12, s);
-    if (rc) return rc;
     const double t_setup = wall_ms();
     ktimes_.setup_ms = t_setup - t_begin;
 
@@ -566,7 +531,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         std::memset(&S, 0, sizeof(S));
         S.T = M4::eye();
         S.mse_prev = S.mse_cur = S.rel = 1e7;
-        S.sf = se3 ? scales[p] : 1.0;
+        S.sf = 1.0;  // run_se3_*: the device's scale, written by k_pair_norms
         S.mse = prm.mse;
         S.mse_switch = prm.mse_switch_error;
         S.kind = mi.kind;
@@ -585,8 +550,6 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         P.cf = mi.kind == KIND_CF;
         P.trim = trim;
         P.nkeep = (int)nv;
-        P.tgt_norm12 = se3 ? n12[2 * p + 1] : 0.f;
-        P.tgt_norm3 = n3[2 * p + 1];
         for (int a = 0; a < 3; ++a) P.f32_center[a] = h_setup_[2 * p].f32_center[a];
         pair_open_iteration(S, P);
         std::memcpy(h_hist_ + 12 * (size_t)p, P.T, sizeof(P.T));
@@ -600,6 +563,12 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
                           hipMemcpyHostToDevice, s));
     HIPCHK(hipMemsetAsync(d_flag_count_.p, 0, 3 * sizeof(int32_t), s));
     HIPCHK(hipMemsetAsync(d_ctl_.p, 0, 8 * sizeof(int32_t), s));
+    // norm bounds of the target search vectors (f32 error certificate) from the root
+    // boxes, and the normalization scales into the loop state
+    launch_pair_norms(view(), 2 << t3_.L, se3 ? 2 << t12_.L : 0, se3 ? (const double*)d_scales_.p : nullptr,
+                      (double*)((char*)d_state_.p + offsetof(PairState, sf)), (int)(sizeof(PairState) / sizeof(double)),
+                      s);
+    HIPCHK(hipGetLastError());
     HIPCHK(hipMemsetAsync((uint64_t*)d_trim_key_.p + npairs, 0, sizeof(uint64_t) * npairs, s));  // no trim window yet
     HIPCHK(hipMemsetAsync(d_trim_ctr_.p, 0, sizeof(unsigned) * 4 * npairs, s));
     View v = view();
@@ -699,6 +668,8 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         }
     }
     HIPCHK(hipMemcpyAsync(h_state_, d_state_.p, sizeof(PairState) * npairs, hipMemcpyDeviceToHost, s));
+    if (se3)  // the device's GetCenter results, for the de-normalization (h_partial_ holds >= 9 * nclouds)
+        HIPCHK(hipMemcpyAsync(h_partial_, d_centers_.p, sizeof(double) * 3 * nclouds_, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(h_rechecked_, d_rechecked_.p, sizeof(int32_t) * npairs, hipMemcpyDeviceToHost, s));
     {
         unsigned long long stats[kStatCols * kStatSlots];
@@ -727,8 +698,8 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         const PairState& S = h_state_[p];
         M4 T = S.T;
         if (se3) {  // ISR.cpp:735-738 de-normalization
-            const double* cs = &centers[3 * (2 * p)];
-            const double* ct = &centers[3 * (2 * p + 1)];
+            const double* cs = &h_partial_[3 * (2 * p)];
+            const double* ct = &h_partial_[3 * (2 * p + 1)];
             for (int r = 0; r < 3; ++r) {
                 const double Rc = T.m[r][0] * cs[0] + T.m[r][1] * cs[1] + T.m[r][2] * cs[2];
                 T.m[r][3] = (1.0 / S.sf) * T.m[r][3] - Rc + ct[r];

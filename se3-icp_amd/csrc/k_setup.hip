@@ -7,8 +7,9 @@
 //   frames     TOLDI LRF -> SE(3) 12-vector (ISR.cpp:241-316), alpha/beta weights
 //              (ISR.cpp:597-607), EstimateNormals (ISR.cpp:643), GICP covariance
 //              (ISR.cpp:33-52), all fused per point.
-// All reductions write fixed per-chunk partials that the host combines in order,
-// so results are deterministic run to run.
+// All reductions write fixed per-chunk partials combined in chunk order (on the device
+// for the registration path: k_pair_centers / k_pair_scales), so results are
+// deterministic run to run.
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
@@ -146,9 +147,86 @@ __global__ __launch_bounds__(256) void k_normalize(View v, const ChunkWork* chun
     }
 }
 
+// ------------------------------------------------------------------ normalization parameters
+// The host-side combination of the chunk partials, moved to the device so the setup
+// never waits for the host: one thread per pair, partials combined in chunk order
+// (the same additions in the same order as a host loop, so bit-identical).
+// GetCenter (arithmetic mean) of both clouds, ISR.cpp:568-570.
+__global__ void k_pair_centers(View v, const ChunkWork* chunks, int nch, const double* partial, double* centers) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= v.nclouds) return;
+    double sum[3] = {0.0, 0.0, 0.0};
+    for (int k = 0; k < nch; ++k)
+        if (chunks[k].cloud == c)
+            for (int a = 0; a < 3; ++a) sum[a] += partial[9 * (size_t)k + a];
+    const int n = v.clouds[c].n;
+    for (int a = 0; a < 3; ++a) centers[3 * c + a] = n > 0 ? sum[a] / (double)n : 0.0;
+}
+
+// s = scale_pre / max(r_src, r_tgt) (ISR.cpp:571-574) and the clouds' CloudSetup
+// normalization fields (ISR.cpp:576-582).
+__global__ void k_pair_scales(View v, const ChunkWork* chunks, int nch, const double* partial, const double* centers,
+                              double scale_pre, double* scales) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (2 * p + 1 >= v.nclouds) return;
+    double rad[2] = {-1.0, -1.0};
+    for (int k = 0; k < nch; ++k) {
+        const int c = chunks[k].cloud;
+        if ((c >> 1) == p) rad[c & 1] = fmax(rad[c & 1], partial[k]);
+    }
+    const double rmax = fmax(rad[0], rad[1]);
+    const double sf = scale_pre * (1.0 / rmax);
+    for (int c = 2 * p; c <= 2 * p + 1; ++c) {
+        CloudSetup& st = v.setup[c];
+        for (int a = 0; a < 3; ++a) {
+            st.norm_center[a] = centers[3 * c + a];
+            st.f32_center[a] = 0.0;
+        }
+        st.norm_scale = sf;
+    }
+    scales[p] = sf;
+}
+
+// Norm bounds of the targets' search vectors (f32 error certificate, k_nn.hip) from the
+// root boxes of their kd-trees: PairDev.tgt_norm3 / tgt_norm12, and PairState.sf.
+__device__ float root_norm(const float* lo, const float* hi, int D) {
+    double n2 = 0;
+    for (int d = 0; d < D; ++d) {
+        const double m = fmax(fabs((double)lo[d]), fabs((double)hi[d]));
+        n2 += m * m;
+    }
+    return (float)(sqrt(n2) * (1.0 + 1e-6));
+}
+__global__ void k_pair_norms(View v, int nnodes3, int nnodes12, const double* scales, double* state_sf,
+                             int state_stride) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= v.npairs) return;
+    const int c = 2 * p + 1;
+    PairDev& P = v.pairs[p];
+    P.tgt_norm3 = root_norm(v.t3.lo + (size_t)c * nnodes3 * 3, v.t3.hi + (size_t)c * nnodes3 * 3, 3);
+    P.tgt_norm12 = nnodes12 > 0 ? root_norm(v.t12.lo + (size_t)c * nnodes12 * 12, v.t12.hi + (size_t)c * nnodes12 * 12, 12)
+                                : 0.f;
+    if (scales) state_sf[(size_t)p * state_stride] = scales[p];
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ launchers
+void launch_pair_centers(const View& v, const ChunkWork* chunks, int nchunks, const double* partial, double* centers,
+                         hipStream_t s) {
+    hipLaunchKernelGGL(k_pair_centers, dim3((v.nclouds + 63) / 64), dim3(64), 0, s, v, chunks, nchunks, partial,
+                       centers);
+}
+void launch_pair_scales(const View& v, const ChunkWork* chunks, int nchunks, const double* partial,
+                        const double* centers, double scale_pre, double* scales, hipStream_t s) {
+    hipLaunchKernelGGL(k_pair_scales, dim3((v.nclouds / 2 + 63) / 64), dim3(64), 0, s, v, chunks, nchunks, partial,
+                       centers, scale_pre, scales);
+}
+void launch_pair_norms(const View& v, int nnodes3, int nnodes12, const double* scales, double* state_sf,
+                       int state_stride, hipStream_t s) {
+    hipLaunchKernelGGL(k_pair_norms, dim3((v.npairs + 63) / 64), dim3(64), 0, s, v, nnodes3, nnodes12, scales,
+                       state_sf, state_stride);
+}
 void launch_ingest(const View& v, const ChunkWork* chunks, int nchunks, double* partial, hipStream_t s) {
     if (nchunks > 0) hipLaunchKernelGGL(k_ingest, dim3(nchunks), dim3(256), 0, s, v, chunks, partial);
 }

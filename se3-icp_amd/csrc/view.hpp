@@ -102,6 +102,16 @@ void launch_radius(const View& v, const ChunkWork* chunks, int nchunks, const do
                    double* partial /*[nchunks]*/, hipStream_t s);
 void launch_normalize(const View& v, const ChunkWork* chunks, int nchunks, double* partial /*[nchunks*7]*/,
                       hipStream_t s);
+// device-side normalization parameters of pairs (clouds 2p, 2p+1): centers [nclouds*3]
+// from the ingest partials, scales [npairs] and the CloudSetup fields from the radius
+// partials; then the targets' root-box norm bounds into PairDev (and scales into the
+// PairState sf fields, stride in doubles) once the trees and the pair records exist
+void launch_pair_centers(const View& v, const ChunkWork* chunks, int nchunks, const double* partial, double* centers,
+                         hipStream_t s);
+void launch_pair_scales(const View& v, const ChunkWork* chunks, int nchunks, const double* partial,
+                        const double* centers, double scale_pre, double* scales, hipStream_t s);
+void launch_pair_norms(const View& v, int nnodes3, int nnodes12, const double* scales, double* state_sf,
+                       int state_stride, hipStream_t s);
 // fused kNN + TOLDI frame + normals/GICP covariance (k_knn.hip); knn list only if v.knn
 void launch_lrf(const View& v, int write_knn, hipStream_t s);
 
