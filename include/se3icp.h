@@ -86,8 +86,8 @@ typedef struct se3icp_result {
     int32_t status;                   /* se3icp_status of this pair             */
     int32_t num_rechecked;            /* NN queries re-resolved in f64 (diagnostic) */
     double scaling_factor;            /* 3 / max radius (1 for run_icp)         */
-    double time_setup_ms;             /* normalization + TOLDI + normals (batch wall time) */
-    double time_loop_ms;              /* ICP loop (batch wall time)             */
+    double time_setup_ms;             /* normalization + TOLDI + normals (batch, GPU timeline) */
+    double time_loop_ms;              /* ICP loop (batch, GPU timeline)                        */
     double time_se3_correspondence_search_ms; /* time_se3_correspondence_search_ */
 } se3icp_result;
 

@@ -31,10 +31,6 @@ namespace {
         if (rc_) return rc_;              \
     } while (0)
 
-double wall_ms() {
-    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-
 // Kind (KIND_ICP / SE3 / CF / PURE): pairmath.hpp
 
 struct MethodInfo {
@@ -454,8 +450,10 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     if (kmax > kMaxKnn) return SE3ICP_ERR_K_TOO_LARGE;
     HIPCHK(hipSetDevice(dev_));
     hipStream_t s = user_stream ? user_stream : stream_;
-    const double t_begin = wall_ms();
     ktimes_ = KernelTimes{};
+    // phase times on the GPU timeline (the host does not wait for the setup): events
+    // 12 (begin), 13 (setup done), 14 (loop done)
+    HIPCHK(hipEventRecord(ev_[12], s));
 
     npairs_ = npairs;
     int64_t ntot = 0;
@@ -515,8 +513,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     HIPCHK(hipMemsetAsync(d_corr_idx_.p, 0xff, sizeof(int32_t) * ld_, s));  // no previous match yet
     HIPCHK(hipMemsetAsync(d_stats_.p, 0, sizeof(unsigned long long) * kStatCols * kStatSlots, s));
     for (double& t : trace_prev_) t = 0;
-    const double t_setup = wall_ms();
-    ktimes_.setup_ms = t_setup - t_begin;
+    HIPCHK(hipEventRecord(ev_[13], s));
 
     // ---- per-pair loop state (ISR.cpp:629-651); iteration 1 is opened here, every later
     // one by k_reduce_final on the device (pairmath.hpp), so the host only queues work
@@ -667,6 +664,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
             break;
         }
     }
+    HIPCHK(hipEventRecord(ev_[14], s));
     HIPCHK(hipMemcpyAsync(h_state_, d_state_.p, sizeof(PairState) * npairs, hipMemcpyDeviceToHost, s));
     if (se3)  // the device's GetCenter results, for the de-normalization (h_partial_ holds >= 9 * nclouds)
         HIPCHK(hipMemcpyAsync(h_partial_, d_centers_.p, sizeof(double) * 3 * nclouds_, hipMemcpyDeviceToHost, s));
@@ -691,7 +689,10 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
                      sum[9], 100.0 * sum[8] / std::max(1.0, sum[10]));
 #endif
     }
-    const double t_end = wall_ms();
+    float setup_ms = 0, loop_ms = 0;
+    HIPCHK(hipEventElapsedTime(&setup_ms, ev_[12], ev_[13]));
+    HIPCHK(hipEventElapsedTime(&loop_ms, ev_[13], ev_[14]));
+    ktimes_.setup_ms = setup_ms;
 
     int worst = 0;
     for (int p = 0; p < npairs; ++p) {
@@ -718,8 +719,8 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         R.status = finite ? SE3ICP_OK : SE3ICP_ERR_NONFINITE;
         R.num_rechecked = h_rechecked_[p];
         R.scaling_factor = S.sf;
-        R.time_setup_ms = t_setup - t_begin;
-        R.time_loop_ms = t_end - t_setup;
+        R.time_setup_ms = setup_ms;
+        R.time_loop_ms = loop_ms;
         R.time_se3_correspondence_search_ms = nn_ms;
         if (R.status != SE3ICP_OK) worst = R.status;
     }
