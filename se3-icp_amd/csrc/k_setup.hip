@@ -7,7 +7,7 @@
 //   frames     TOLDI LRF -> SE(3) 12-vector (ISR.cpp:241-316), alpha/beta weights
 //              (ISR.cpp:597-607), EstimateNormals (ISR.cpp:643), GICP covariance
 //              (ISR.cpp:33-52), all fused per point.
-// All reductions write fixed per-chunk partials combined in chunk order (on the device
+// All reductions write fixed per-chunk partials combined in a fixed order (on the device
 // for the registration path: k_pair_centers / k_pair_scales), so results are
 // deterministic run to run.
 #include <hip/hip_runtime.h>
@@ -148,43 +148,45 @@ __global__ __launch_bounds__(256) void k_normalize(View v, const ChunkWork* chun
 }
 
 // ------------------------------------------------------------------ normalization parameters
-// The host-side combination of the chunk partials, moved to the device so the setup
-// never waits for the host: one thread per pair, partials combined in chunk order
-// (the same additions in the same order as a host loop, so bit-identical).
-// GetCenter (arithmetic mean) of both clouds, ISR.cpp:568-570.
-__global__ void k_pair_centers(View v, const ChunkWork* chunks, int nch, const double* partial, double* centers) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= v.nclouds) return;
+// The combination of the chunk partials, on the device so the setup never waits for the
+// host: one wavefront per cloud / pair, lane l folds chunks l, l+64, ... in order, then a
+// fixed butterfly combines the lanes (deterministic run to run).
+// GetCenter (arithmetic mean) of every cloud, ISR.cpp:568-570.
+__global__ __launch_bounds__(64) void k_pair_centers(View v, const ChunkWork* chunks, int nch, const double* partial,
+                                                     double* centers) {
+    const int c = blockIdx.x, lane = threadIdx.x;
     double sum[3] = {0.0, 0.0, 0.0};
-    for (int k = 0; k < nch; ++k)
+    for (int k = lane; k < nch; k += 64)
         if (chunks[k].cloud == c)
             for (int a = 0; a < 3; ++a) sum[a] += partial[9 * (size_t)k + a];
+    for (int a = 0; a < 3; ++a) sum[a] = wave_reduce(sum[a], OpAdd());
     const int n = v.clouds[c].n;
-    for (int a = 0; a < 3; ++a) centers[3 * c + a] = n > 0 ? sum[a] / (double)n : 0.0;
+    if (lane < 3) centers[3 * c + lane] = n > 0 ? sum[lane] / (double)n : 0.0;
 }
 
 // s = scale_pre / max(r_src, r_tgt) (ISR.cpp:571-574) and the clouds' CloudSetup
 // normalization fields (ISR.cpp:576-582).
-__global__ void k_pair_scales(View v, const ChunkWork* chunks, int nch, const double* partial, const double* centers,
-                              double scale_pre, double* scales) {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (2 * p + 1 >= v.nclouds) return;
+__global__ __launch_bounds__(64) void k_pair_scales(View v, const ChunkWork* chunks, int nch, const double* partial,
+                                                    const double* centers, double scale_pre, double* scales) {
+    const int p = blockIdx.x, lane = threadIdx.x;
     double rad[2] = {-1.0, -1.0};
-    for (int k = 0; k < nch; ++k) {
+    for (int k = lane; k < nch; k += 64) {
         const int c = chunks[k].cloud;
         if ((c >> 1) == p) rad[c & 1] = fmax(rad[c & 1], partial[k]);
     }
+    rad[0] = wave_reduce(rad[0], OpMax());
+    rad[1] = wave_reduce(rad[1], OpMax());
     const double rmax = fmax(rad[0], rad[1]);
     const double sf = scale_pre * (1.0 / rmax);
-    for (int c = 2 * p; c <= 2 * p + 1; ++c) {
-        CloudSetup& st = v.setup[c];
+    if (lane < 2) {
+        CloudSetup& st = v.setup[2 * p + lane];
         for (int a = 0; a < 3; ++a) {
-            st.norm_center[a] = centers[3 * c + a];
+            st.norm_center[a] = centers[3 * (2 * p + lane) + a];
             st.f32_center[a] = 0.0;
         }
         st.norm_scale = sf;
     }
-    scales[p] = sf;
+    if (lane == 0) scales[p] = sf;
 }
 
 // Norm bounds of the targets' search vectors (f32 error certificate, k_nn.hip) from the
@@ -214,13 +216,12 @@ __global__ void k_pair_norms(View v, int nnodes3, int nnodes12, const double* sc
 // ------------------------------------------------------------------ launchers
 void launch_pair_centers(const View& v, const ChunkWork* chunks, int nchunks, const double* partial, double* centers,
                          hipStream_t s) {
-    hipLaunchKernelGGL(k_pair_centers, dim3((v.nclouds + 63) / 64), dim3(64), 0, s, v, chunks, nchunks, partial,
-                       centers);
+    hipLaunchKernelGGL(k_pair_centers, dim3(v.nclouds), dim3(64), 0, s, v, chunks, nchunks, partial, centers);
 }
 void launch_pair_scales(const View& v, const ChunkWork* chunks, int nchunks, const double* partial,
                         const double* centers, double scale_pre, double* scales, hipStream_t s) {
-    hipLaunchKernelGGL(k_pair_scales, dim3((v.nclouds / 2 + 63) / 64), dim3(64), 0, s, v, chunks, nchunks, partial,
-                       centers, scale_pre, scales);
+    hipLaunchKernelGGL(k_pair_scales, dim3(v.nclouds / 2), dim3(64), 0, s, v, chunks, nchunks, partial, centers,
+                       scale_pre, scales);
 }
 void launch_pair_norms(const View& v, int nnodes3, int nnodes12, const double* scales, double* state_sf,
                        int state_stride, hipStream_t s) {
