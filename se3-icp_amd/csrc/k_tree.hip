@@ -150,7 +150,11 @@ __global__ __launch_bounds__(256) void k_tree_keys32(TreeView t, int level, int 
 // permutation stays in LDS and every level is a bitonic sort of (sub-node, coordinate
 // along the sub-node's widest dimension) keys -- the same median splits as the global
 // levels, without a device-wide radix sort per level.
-constexpr int kLocalMax = 4096;
+#ifndef SE3ICP_LOCAL_MAX
+#define SE3ICP_LOCAL_MAX 4096
+#endif
+constexpr int kLocalMax = SE3ICP_LOCAL_MAX;  // power of two
+constexpr int kLocalBits = __builtin_ctz(kLocalMax);  // element field of the block sort keys
 constexpr int kWaveSortPer = 8;  // sub-nodes of <= 512 points: register sort by one wave
 #ifndef SE3ICP_TREE_SPLIT
 #define SE3ICP_TREE_SPLIT 1
@@ -277,7 +281,7 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
             continue;
         }
         // large sub-nodes: block-wide bitonic sort of (sub-node, coordinate, element) keys
-        // (7 + 32 + 12 bits), 8 per thread in registers; only the 6 stages with partners
+        // (7 + 32 + log2(kLocalMax) bits), kLocalMax / 512 per thread in registers; only the stages with partners
         // in another wave go through LDS
         {
             constexpr int PER = kLocalMax / kLocalThreads;
@@ -290,7 +294,8 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
                     const int sub = tree_node_of(A + e, n, l) - (i << r);
                     const float* row = t.vec + (size_t)s_best[sub] * t.ld;
                     const uint32_t c = ord_bits(row[cl.off + s_val[e]]);
-                    k[u] = ((unsigned long long)(unsigned)sub << 44) | ((unsigned long long)c << 12) | (unsigned)e;
+                    k[u] = ((unsigned long long)(unsigned)sub << (32 + kLocalBits)) | ((unsigned long long)c << kLocalBits) |
+                           (unsigned)e;
                 }
             }
             bitonic_net<PER, kLocalMax, 64 * PER>(k, tid, s_key);
@@ -303,7 +308,7 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
 #pragma unroll
             for (int u = 0; u < PER; ++u) {
                 const int e = tid * PER + u;
-                nv[u] = e < m ? s_val[(int)(s_key[e] & 0xfffu)] : 0;
+                nv[u] = e < m ? s_val[(int)(s_key[e] & (unsigned long long)(kLocalMax - 1))] : 0;
             }
             __syncthreads();
 #pragma unroll
