@@ -242,3 +242,52 @@ def test_kitti_full_size_pair_matches_oracle(se3icp_mod, refcpu):
     assert np.linalg.norm(got.T - ref["T"]) <= 1e-5
     assert got.num_iterations == ref["num_iterations"]
     assert got.num_pure_se3_iterations == ref["num_pure_se3_iterations"]
+
+
+# --------------------------------------------------------------------------- per-iteration parity
+@pytest.mark.parametrize("variant", ["pt2pt", "pt2pl", "gicp"])
+def test_first_iterations_match_oracle(se3icp_mod, refcpu, bunny_unique, variant):
+    """the pose after each of the first three SE(3) iterations
+    (run_se3_pure stopped at max_num_se3_iterations = k, ISR.cpp:1118-1119), on a noisy,
+    trimmed pair (overlap 0.7: the trimmed sets feed the estimator).  The loop state
+    lives on the device (k_reduce_final), so this pins the device-side solve and the
+    windowed trim iteration by iteration."""
+    from se3icp import datasets
+    src, tgt, _ = datasets.bunny_pair(bunny_unique, seed=2, subsample=0.1)
+    for k in (1, 2, 3):
+        kw = dict(estimated_overlap=0.7, max_num_se3_iterations=k, mse=1e-12, mse_switch_error=1e-12,
+                  number_of_nn_for_LRF=60)
+        got = se3icp_mod.register_batch([(src, tgt)], "se3_pure_" + variant, se3icp_mod.default_params(**kw))[0]
+        ref = refcpu.register(src, tgt, refcpu.RUN_SE3_PURE, variant, refcpu.default_params(**kw))
+        assert got.num_iterations == ref["num_iterations"] == k
+        assert np.linalg.norm(got.T - ref["T"]) <= 1e-9 * max(1.0, np.linalg.norm(ref["T"])), (k, got.T, ref["T"])
+
+
+def test_se3_phase_without_iteration_cap_matches_oracle(se3icp_mod, refcpu, fixture_clouds):
+    """max_num_se3_iterations = 0: `iter == max` never holds, so only the pose change ends
+    the SE(3) phase (ISR.cpp:718-723); the host must keep queueing SE(3) searches."""
+    src, tgt = fixture_clouds
+    kw = dict(estimated_overlap=1.0, max_num_se3_iterations=0, mse=1e-5, mse_switch_error=5e-5,
+              number_of_nn_for_LRF=90)
+    got = se3icp_mod.register_batch([(src, tgt)], "se3_pt2pl", se3icp_mod.default_params(**kw))[0]
+    ref = refcpu.register(src, tgt, refcpu.RUN_SE3_ICP, "pt2pl", refcpu.default_params(**kw))
+    assert got.num_iterations == ref["num_iterations"]
+    assert got.num_pure_se3_iterations == ref["num_pure_se3_iterations"]
+    assert np.linalg.norm(got.T - ref["T"]) <= 1e-5
+
+
+def test_batch_with_pairs_finishing_at_different_iterations(se3icp_mod, refcpu, bunny_unique, fixture_clouds):
+    """Lockstep batch: pairs switch and converge at different iterations (the device
+    marks finished pairs idle, later iterations run only the rest); every pair equals
+    its own single-pair oracle run."""
+    from se3icp import datasets
+    pairs = [fixture_clouds] + [datasets.bunny_pair(bunny_unique, seed=s, subsample=0.08)[:2] for s in (3, 4)]
+    params = se3icp_mod.cli_params()
+    got = se3icp_mod.register_batch(pairs, "se3_pt2pl", params)
+    its = []
+    for (s, t), g in zip(pairs, got):
+        ref = refcpu.register(s, t, refcpu.RUN_SE3_ICP, "pt2pl", refcpu.cli_params())
+        assert np.linalg.norm(g.T - ref["T"]) <= 1e-5
+        assert abs(g.num_iterations - ref["num_iterations"]) <= 1
+        its.append(g.num_iterations)
+    assert len(set(its)) > 1, its  # the batch really had pairs finishing at different iterations
