@@ -131,6 +131,8 @@ class Engine {
     unsigned long long* h_lrf_stats_ = nullptr;  // k_lrf work counters (read at the next sync)
     size_t h_lrf_stats_cap_ = 0;
     bool lrf_stats_pending_ = false;
+    // 6/7: k_lrf time; 12/13/14: batch begin / setup done / loop done (GPU-timeline phase
+    // times); 15: sync_stream; the rest unused
     hipEvent_t ev_[16];
     // loop iterations in flight: kernel-time events and launched NN phases per ring slot
     static constexpr int kLoopRing = 4, kLoopEv = 7;
