@@ -589,10 +589,15 @@ __global__ __launch_bounds__(256) void k_reduce_final(View v, const int32_t* pai
     __shared__ double tot[kRedVals];
     const int i = threadIdx.x % kRedVals, s = threadIdx.x / kRedVals;
     const int wb = pair_wb[p], wn = pair_wn[p];
-    if (s < 8) {
-        double sum = 0;
-        for (int b = s; b < wn; b += 8) sum += v.red_partial[(size_t)(wb + b) * kRedVals + i];
-        part[s][i] = sum;
+    if (s < 8) {  // four independent chains per lane: four loads in flight
+        double s4[4] = {0.0, 0.0, 0.0, 0.0};
+        const double* rp = v.red_partial + (size_t)wb * kRedVals + i;
+        int b = s;
+        for (; b + 24 < wn; b += 32)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) s4[u] += rp[(size_t)(b + 8 * u) * kRedVals];
+        for (; b < wn; b += 8) s4[0] += rp[(size_t)b * kRedVals];
+        part[s][i] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
     }
     __syncthreads();
     if (threadIdx.x < kRedVals) {
