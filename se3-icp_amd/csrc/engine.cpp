@@ -107,7 +107,7 @@ Engine::~Engine() {
                      &d_corr_idx_, &d_corr_dist_, &d_flag_list_, &d_flag_count_, &d_trim_key_, &d_red_partial_,
                      &d_red_out_, &d_work_, &d_wb_, &d_wn_, &d_chunks_, &d_partial_, &d_centers_,
                      &d_rechecked_, &d_keys0_, &d_keys1_, &d_vals1_, &d_sort_tmp_, &d_stats_,
-                     &d_qlist_, &d_qcount_, &d_hist_, &d_cert_d1_, &d_cert_l2_, &d_cert_it_, &d_margin_, &d_sqlist_, &d_state_, &d_ctl_, &d_trim_cand_, &d_trim_ctr_, &d_scales_,
+                     &d_qlist_, &d_qcount_, &d_hist_, &d_cert_d1_, &d_cert_l2_, &d_cert_it_, &d_margin_, &d_sqlist_, &d_state_, &d_ctl_, &d_trim_cand_, &d_trim_ctr_, &d_scales_, &d_trim_hist_,
                      &t3_.perm, &t3_.pos, &t3_.vec, &t3_.blo, &t3_.bhi, &t3_.lo, &t3_.hi,
                      &t12_.perm, &t12_.pos, &t12_.vec, &t12_.blo, &t12_.bhi, &t12_.lo, &t12_.hi};
     for (DevBuf* b : all)
@@ -193,6 +193,7 @@ View Engine::view() const {
     v.trim_key = (uint64_t*)d_trim_key_.p;
     v.trim_cand = (unsigned long long*)d_trim_cand_.p;
     v.trim_ctr = (unsigned*)d_trim_ctr_.p;
+    v.trim_hist = (unsigned*)d_trim_hist_.p;
     v.red_partial = (double*)d_red_partial_.p;
     v.red_out = (double*)d_red_out_.p;
     v.work = (const BlockWork*)d_work_.p;
@@ -473,6 +474,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     if (!ensure<PairDev>(d_pairs_, npairs) || !ensure<BlockWork>(d_work_, nwork_) || !ensure<int32_t>(d_wb_, npairs) ||
         !ensure<int32_t>(d_wn_, npairs) || !ensure<uint64_t>(d_trim_key_, 2 * (size_t)npairs) ||
         !ensure<unsigned long long>(d_trim_cand_, (size_t)npairs * kTrimList) || !ensure<unsigned>(d_trim_ctr_, 4 * (size_t)npairs) ||
+        !ensure<unsigned>(d_trim_hist_, 4096 * (size_t)npairs) ||
         !ensure<double>(d_red_partial_, (size_t)nwork_ * kRedVals) || !ensure<double>(d_red_out_, (size_t)npairs * kRedVals) ||
         !ensure<int32_t>(d_rechecked_, npairs))
         return SE3ICP_ERR_OUT_OF_MEMORY;
@@ -568,6 +570,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemsetAsync((uint64_t*)d_trim_key_.p + npairs, 0, sizeof(uint64_t) * npairs, s));  // no trim window yet
     HIPCHK(hipMemsetAsync(d_trim_ctr_.p, 0, sizeof(unsigned) * 4 * npairs, s));
+    HIPCHK(hipMemsetAsync(d_trim_hist_.p, 0, sizeof(unsigned) * 4096 * npairs, s));
     View v = view();
     const int recheck_blocks = 512;
     double nn_ms = 0;

@@ -193,13 +193,15 @@ __device__ __forceinline__ unsigned wsum_u32(unsigned x) {
 //    [d_prev(1-w), d_prev(1+w)] and appends the keys inside it to a global list; k_trim
 //    ranks the list (each candidate counts the smaller ones, LDS broadcast reads) if the
 //    cut rank falls inside.  w adapts toward a few hundred keys.
-//  * Otherwise k_trim runs an MSB radix select: the first digit is the top 12 bits;
-//    further 8-bit digits are counted over all keys (global re-reads) until the selected
-//    bin holds at most kTrimList keys, which are then compacted into LDS where the
-//    remaining digits are resolved.
+//  * Otherwise k_trim runs an MSB radix select: the first digit (top 12 bits) comes from
+//    the histogram k_trim_window builds of every key; further 8-bit digits are counted
+//    over all keys (global re-reads) until the selected bin holds at most kTrimList keys,
+//    which are then compacted into LDS where the remaining digits are resolved.  A window
+//    of more than kRankMax keys is resolved by the same digit passes inside LDS.
 // Both give the same key.  Window state: trim_key[npairs + pair] (f32 d_prev bits << 32 |
 // f32 w bits; 0 = none).  Per pair scratch: trim_cand[pair][kTrimList] and
-// trim_ctr[pair][4] = {in-window count, below count, -, -}, reset by k_trim.
+// trim_ctr[pair][4] = {in-window count, below count, -, -} and trim_hist[pair][4096],
+// reset by k_trim.
 __device__ __forceinline__ unsigned long long trim_window_state(const View& v, const PairDev* P, int pair) {
     // the first iteration of a phase has no usable window (the R3 cut is far below the SE(3) one)
     return P->iter == P->phase_start ? 0ull : (unsigned long long)v.trim_key[v.npairs + pair];
@@ -208,22 +210,24 @@ __device__ __forceinline__ unsigned long long trim_window_state(const View& v, c
 __global__ __launch_bounds__(256) void k_trim_window(View v) {
     constexpr int kLoc = 2048;  // in-window keys a block collects before one global append
     __shared__ unsigned long long s_loc[kLoc];
+    __shared__ unsigned s_hist[4096];  // top 12 key bits: the radix select's first digit
     __shared__ unsigned s_n, s_below, s_base;
     const int pair = blockIdx.x / kTrimBlocks, sub = blockIdx.x % kTrimBlocks;
     const PairDev* P = v.pairs + pair;
     if ((int)(P->phase == PHASE_IDLE) | (int)(P->trim == 0) | (int)(P->nkeep <= 0)) return;
     const unsigned long long wstate = trim_window_state(v, P, pair);
-    if (wstate == 0ull) return;
     const int lane = threadIdx.x & 63;
+    for (int i = threadIdx.x; i < 4096; i += blockDim.x) s_hist[i] = 0u;
     const CloudDev cs = v.clouds[P->src];
     const int n = cs.n;
     const unsigned* dist = reinterpret_cast<const unsigned*>(v.corr_dist) + cs.off;
     unsigned* ctr = v.trim_ctr + 4 * pair;
     unsigned long long* cand = v.trim_cand + (size_t)pair * kTrimList;
+    // no window: an empty one (lo > hi), the pass then only builds the histogram
     const float dprev = __uint_as_float((unsigned)(wstate >> 32));
     const float wv = __uint_as_float((unsigned)wstate);
-    const unsigned lo = __float_as_uint(dprev * (1.0f - wv));
-    const unsigned hi = __float_as_uint(dprev * (1.0f + wv));
+    const unsigned lo = wstate ? __float_as_uint(dprev * (1.0f - wv)) : 0xffffffffu;
+    const unsigned hi = wstate ? __float_as_uint(dprev * (1.0f + wv)) : 0u;
     const int per = ((n + kTrimBlocks - 1) / kTrimBlocks + 63) & ~63;
     const int i_beg = sub * per, i_end = min(n, i_beg + per);
     if (threadIdx.x == 0) { s_n = 0; s_below = 0; }
@@ -240,6 +244,7 @@ __global__ __launch_bounds__(256) void k_trim_window(View v) {
 #pragma unroll
         for (int j = 0; j < U; ++j) {
             const int i = i0 + j * blockDim.x + threadIdx.x;
+            if (i < i_end) atomicAdd(&s_hist[u[j] >> 20], 1u);
             below += (unsigned)((int)(i < i_end) & (int)(u[j] < lo));
             const bool sel = (int)(i < i_end) & (int)(u[j] >= lo) & (int)(u[j] <= hi);
             const unsigned long long m = __ballot(sel);
@@ -251,9 +256,12 @@ __global__ __launch_bounds__(256) void k_trim_window(View v) {
             if ((int)sel & (int)(at < (unsigned)kLoc)) s_loc[at] = ((unsigned long long)u[j] << 32) | (unsigned)i;
         }
     }
-    below = wsum_u32(below);
+    below = wstate ? wsum_u32(below) : 0u;  // (no window: only the histogram is wanted)
     if ((int)(lane == 0) & (int)(below > 0)) atomicAdd(&s_below, below);
     __syncthreads();
+    unsigned* gh = v.trim_hist + (size_t)pair * 4096;
+    for (int i = threadIdx.x; i < 4096; i += blockDim.x)
+        if (s_hist[i]) atomicAdd(&gh[i], s_hist[i]);
     // one global reservation per block (a block that overflowed its list forces a miss)
     const unsigned nloc = s_n;
     if (threadIdx.x == 0) {
@@ -291,6 +299,9 @@ __global__ __launch_bounds__(1024) void k_trim(View v) {
     const unsigned long long* cand = v.trim_cand + (size_t)pair * kTrimList;
     const unsigned long long wstate = trim_window_state(v, P, pair);
     float wv = wstate != 0ull ? __uint_as_float((unsigned)wstate) : 0.02f;
+    unsigned* gh = v.trim_hist + (size_t)pair * 4096;  // k_trim_window's first-digit histogram
+    constexpr unsigned kRankMax = 768;  // larger windows: LDS radix select instead of ranking
+    unsigned win_cnt = 0, win_k = 0;
     if (wstate != 0ull) {
         const unsigned k = (unsigned)P->nkeep;  // rank (1-based) of the cut key
         const unsigned cnt = ctr[0], nb = ctr[1];
@@ -305,11 +316,17 @@ __global__ __launch_bounds__(1024) void k_trim(View v) {
             printf("[trim] it %d pair %d hit %d cnt %u below %u k %u dprev %g w %g\n", P->iter, pair, (int)hit, cnt,
                    nb, k, (double)__uint_as_float((unsigned)(wstate >> 32)), (double)__uint_as_float((unsigned)wstate));
 #endif
+        constexpr unsigned R = 16;  // independent LDS reads in flight per rank count
+        const unsigned cpad = (cnt + R - 1) & ~(R - 1);
         if (hit) {
-            constexpr unsigned R = 16;  // independent LDS reads in flight per rank count
-            const unsigned cpad = (cnt + R - 1) & ~(R - 1);
             for (unsigned e = threadIdx.x; e < cpad; e += blockDim.x) s_list[e] = e < cnt ? cand[e] : ~0ull;
             __syncthreads();
+            if (cnt > kRankMax) {  // a wide window: radix select inside the LDS list (below)
+                win_cnt = cnt;
+                win_k = k - nb;
+            }
+        }
+        if ((int)hit & (int)(cnt <= kRankMax)) {
             const unsigned r = k - nb - 1;  // 0-based rank inside the window (keys are distinct)
             for (unsigned e = threadIdx.x; e < cnt; e += blockDim.x) {
                 const unsigned long long key = s_list[e];
@@ -328,6 +345,7 @@ __global__ __launch_bounds__(1024) void k_trim(View v) {
             }
             __syncthreads();
             if (threadIdx.x < 2) ctr[threadIdx.x] = 0u;
+            for (int i = threadIdx.x; i < 4096; i += blockDim.x) gh[i] = 0u;
             return;
         }
         __syncthreads();
@@ -339,6 +357,28 @@ __global__ __launch_bounds__(1024) void k_trim(View v) {
     int pos = 0;                      // key bits resolved (from the top)
     bool in_lds = false;
     unsigned cnt = 0;
+    if (win_cnt) {  // the window's keys are in LDS: all digits resolved there
+        in_lds = true;
+        cnt = win_cnt;
+        sel_count = win_cnt;
+        k = win_k;
+        for (int i = threadIdx.x; i < 4096; i += blockDim.x) gh[i] = 0u;
+    } else {  // first digit (top 12 bits) from k_trim_window's histogram
+        for (int i = threadIdx.x; i < 4096; i += blockDim.x) {
+            hist[i] = gh[i];
+            gh[i] = 0u;
+        }
+        __syncthreads();
+        if (wid == 0) wave_find_bin<64>(hist, k, lane, &s_bin, &s_before);
+        __syncthreads();
+        const unsigned bin = (unsigned)s_bin;
+        k -= s_before;
+        sel_count = hist[bin];
+        prefix = (unsigned long long)bin << 52;
+        mask = 0xfffull << 52;
+        pos = 12;
+        __syncthreads();
+    }
     while (pos < 64) {
         const int w = pos == 0 ? 12 : min(8, 64 - pos);
         const int sh = 64 - pos - w;

@@ -66,6 +66,7 @@ struct View {
     uint64_t* trim_key;   // [npairs] cut key, then [npairs] k_trim window state
     unsigned long long* trim_cand;  // [npairs][kTrimList] k_trim window keys
     unsigned* trim_ctr;   // [npairs][4] k_trim counters (zero between launches)
+    unsigned* trim_hist;  // [npairs][4096] top-12-bit key histogram (zero between launches)
     double* red_partial;  // [nwork * kRedVals]
     double* red_out;      // [npairs * kRedVals]
     const BlockWork* work;
