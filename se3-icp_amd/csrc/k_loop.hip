@@ -282,6 +282,7 @@ __global__ __launch_bounds__(1024) void k_trim(View v) {
     __shared__ unsigned s_cnt;
     __shared__ int s_bin;
     __shared__ unsigned s_before;
+    __shared__ unsigned long long s_found;
     const int pair = blockIdx.x;
     const PairDev* P = v.pairs + pair;
     if (P->phase == PHASE_IDLE || !P->trim) return;
@@ -447,6 +448,14 @@ __global__ __launch_bounds__(1024) void k_trim(View v) {
         mask |= (unsigned long long)dmask << sh;
         pos += w;
         __syncthreads();
+        if ((int)in_lds & (int)(sel_count == 1u) & (int)(pos < 64)) {
+            // one key left with this prefix (the distance bits usually settle it): it is the cut
+            for (unsigned e = threadIdx.x; e < cnt; e += blockDim.x)
+                if ((s_list[e] & mask) == prefix) s_found = s_list[e];
+            __syncthreads();
+            prefix = s_found;
+            break;
+        }
     }
     if (threadIdx.x == 0) {
         v.trim_key[pair] = prefix;
