@@ -312,7 +312,7 @@ __global__ __launch_bounds__(1024) void k_trim(View v) {
         else if (!hit) wv *= 4.0f;
         else if (cnt < 96u) wv *= 1.5f;
         wv = fminf(wv, 0.9f);
-#ifdef SE3ICP_PROF
+#ifdef SE3ICP_TRIM_TRACE  // (diagnostic build: window hits and sizes per pair and iteration)
         if (threadIdx.x == 0)
             printf("[trim] it %d pair %d hit %d cnt %u below %u k %u dprev %g w %g\n", P->iter, pair, (int)hit, cnt,
                    nb, k, (double)__uint_as_float((unsigned)(wstate >> 32)), (double)__uint_as_float((unsigned)wstate));
