@@ -135,12 +135,12 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     # one untimed step with HIP events around every loop stage: the timed steps carry
-    # events only around the NN grids (each marker costs the stream a few microseconds)
+    # events only around the SE(3) NN grids (each marker costs the stream a few microseconds)
     se3icp.set_profiling(True, local)
     step()
     kt_detail = se3icp.last_kernel_times(local)
     se3icp.set_profiling(False, local)
-    for k in ["nn_prep_ms", "recheck_ms", "trim_ms", "reduce_ms"]:
+    for k in ["nn_prep_ms", "nn_r3_ms", "recheck_ms", "trim_ms", "reduce_ms"]:
         ktot[k] = kt_detail[k] * args.steps
 
     # ---- cross-rank: max time, summed work, RCCL gather of the per-pair results

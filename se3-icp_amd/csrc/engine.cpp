@@ -590,13 +590,16 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         // HIP events around the NN grids always (bench.py's roofline); around every other
         // stage only when profiling (each marker costs the stream a few microseconds)
         const bool detail = profile_ || nn_trace_;
+        // (timed steps: the SE(3) NN bracket only when that grid is queued, plus the
+        // iteration's end marker; profiled steps: every stage)
+        const bool t_se3 = detail || do_se3;
         if (detail) HIPCHK(hipEventRecord(ev[0], s));
         launch_nn_prep(v, s);
-        HIPCHK(hipEventRecord(ev[1], s));
+        if (t_se3) HIPCHK(hipEventRecord(ev[1], s));
         if (do_se3) launch_nn_se3(v, s);
-        HIPCHK(hipEventRecord(ev[2], s));
+        if (t_se3) HIPCHK(hipEventRecord(ev[2], s));
         if (do_r3) launch_nn_r3(v, s);
-        HIPCHK(hipEventRecord(ev[3], s));
+        if (detail) HIPCHK(hipEventRecord(ev[3], s));
         launch_recheck(v, recheck_blocks, s);
         if (detail) HIPCHK(hipEventRecord(ev[4], s));
         if (any_trim) launch_trim(v, s);
@@ -616,10 +619,10 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         hipEvent_t* ev = &loop_ev_[(it % kLoopRing) * kLoopEv];
         HIPCHK(spin_wait(ev[6]));
         float ms[6] = {};
-        for (int k = 1; k < 3; ++k) HIPCHK(hipEventElapsedTime(&ms[k], ev[k], ev[k + 1]));
         if (loop_detail_[it % kLoopRing]) {
-            HIPCHK(hipEventElapsedTime(&ms[0], ev[0], ev[1]));
-            for (int k = 3; k < 6; ++k) HIPCHK(hipEventElapsedTime(&ms[k], ev[k], ev[k + 1]));
+            for (int k = 0; k < 6; ++k) HIPCHK(hipEventElapsedTime(&ms[k], ev[k], ev[k + 1]));
+        } else if (loop_flags_[it % kLoopRing] & 1) {
+            HIPCHK(hipEventElapsedTime(&ms[1], ev[1], ev[2]));
         }
         ktimes_.nn_prep_ms += ms[0];
         ktimes_.nn_se3_ms += ms[1];
