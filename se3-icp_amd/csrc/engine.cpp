@@ -107,7 +107,7 @@ Engine::~Engine() {
                      &d_corr_idx_, &d_corr_dist_, &d_flag_list_, &d_flag_count_, &d_trim_key_, &d_red_partial_,
                      &d_red_out_, &d_work_, &d_wb_, &d_wn_, &d_chunks_, &d_partial_, &d_centers_,
                      &d_rechecked_, &d_keys0_, &d_keys1_, &d_vals1_, &d_sort_tmp_, &d_stats_,
-                     &d_qlist_, &d_qcount_, &d_hist_, &d_cert_d1_, &d_cert_l2_, &d_cert_it_, &d_margin_, &d_sqlist_, &d_state_, &d_ctl_, &d_trim_cand_, &d_trim_ctr_, &d_scales_, &d_trim_hist_,
+                     &d_qlist_, &d_qcount_, &d_hist_, &d_cert_d1_, &d_cert_l2_, &d_cert_it_, &d_margin_, &d_sqlist_, &d_state_, &d_trim_cand_, &d_trim_ctr_, &d_scales_, &d_trim_hist_,
                      &t3_.perm, &t3_.pos, &t3_.vec, &t3_.blo, &t3_.bhi, &t3_.lo, &t3_.hi,
                      &t12_.perm, &t12_.pos, &t12_.vec, &t12_.blo, &t12_.bhi, &t12_.lo, &t12_.hi};
     for (DevBuf* b : all)
@@ -123,7 +123,7 @@ Engine::~Engine() {
     for (auto& e : loop_ev_)
         if (e) (void)hipEventDestroy(e);
     if (h_state_) (void)hipHostFree(h_state_);
-    if (h_ctl_) (void)hipHostFree(h_ctl_);
+    if (h_phase_) (void)hipHostFree(h_phase_);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -519,9 +519,19 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
 
     // ---- per-pair loop state (ISR.cpp:629-651); iteration 1 is opened here, every later
     // one by k_reduce_final on the device (pairmath.hpp), so the host only queues work
-    if (!ensure<PairState>(d_state_, npairs) || !ensure<int32_t>(d_ctl_, 8) || pinned(h_state_, h_state_cap_, npairs) ||
-        pinned(h_ctl_, h_ctl_cap_, 8 * kLoopRing))
+    if (!ensure<PairState>(d_state_, npairs) || pinned(h_state_, h_state_cap_, npairs))
         return SE3ICP_ERR_OUT_OF_MEMORY;
+    if (h_phase_cap_ < (size_t)npairs * kLoopRing) {  // coherent host memory the device writes directly
+        if (h_phase_) (void)hipHostFree(h_phase_);
+        h_phase_ = nullptr;
+        h_phase_cap_ = 0;
+        const size_t want = std::max<size_t>((size_t)npairs * kLoopRing, 64);
+        if (hipHostMalloc((void**)&h_phase_, want * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
+                hipSuccess ||
+            hipHostGetDevicePointer((void**)&d_phase_, h_phase_, 0) != hipSuccess)
+            return SE3ICP_ERR_OUT_OF_MEMORY;
+        h_phase_cap_ = want;
+    }
     const float ratio = std::min(1.0f, std::max(0.0f, (float)prm.estimated_overlap));  // PCL setOverlapRatio(float)
     int n_se3 = 0, n_r3 = 0;
     bool any_trim = false;
@@ -561,7 +571,6 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     HIPCHK(hipMemcpyAsync((double*)d_hist_.p + (size_t)(1 % kHist) * npairs * 12, h_hist_, sizeof(double) * 12 * npairs,
                           hipMemcpyHostToDevice, s));
     HIPCHK(hipMemsetAsync(d_flag_count_.p, 0, 3 * sizeof(int32_t), s));
-    HIPCHK(hipMemsetAsync(d_ctl_.p, 0, 8 * sizeof(int32_t), s));
     // norm bounds of the target search vectors (f32 error certificate) from the root
     // boxes, and the normalization scales into the loop state
     launch_pair_norms(view(), 2 << t3_.L, se3 ? 2 << t12_.L : 0, se3 ? (const double*)d_scales_.p : nullptr,
@@ -605,10 +614,8 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         if (any_trim) launch_trim(v, s);
         if (detail) HIPCHK(hipEventRecord(ev[5], s));
         launch_reduce(v, (const int32_t*)d_wb_.p, (const int32_t*)d_wn_.p, (PairState*)d_state_.p, (double*)d_hist_.p,
-                      (int32_t*)d_ctl_.p, it, s);
+                      d_phase_ + (size_t)(it % kLoopRing) * npairs, s);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(h_ctl_ + 4 * (it % kLoopRing), (int32_t*)d_ctl_.p + 4 * (it & 1), 4 * sizeof(int32_t),
-                              hipMemcpyDeviceToHost, s));
         HIPCHK(hipEventRecord(ev[6], s));
         loop_detail_[it % kLoopRing] = detail;
         loop_flags_[it % kLoopRing] = (do_se3 ? 1 : 0) | (do_r3 ? 2 : 0);
@@ -648,10 +655,14 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
                          sum[2] - trace_prev_[2], sum[3] - trace_prev_[3], ms[0], ms[1], ms[2], ms[3]);
             for (int k = 0; k < kStatCols; ++k) trace_prev_[k] = sum[k];
         }
-        const int32_t* c = h_ctl_ + 4 * (it % kLoopRing);
-        n_se3 = c[1];
-        n_r3 = c[2];
-        return c[0];
+        const volatile int32_t* ph = h_phase_ + (size_t)(it % kLoopRing) * npairs;
+        n_se3 = n_r3 = 0;
+        for (int p = 0; p < npairs; ++p) {
+            const int32_t f = ph[p];
+            n_se3 += f == PHASE_SE3;
+            n_r3 += f == PHASE_R3;
+        }
+        return n_se3 + n_r3;
     };
     static_assert(kLoopRing >= 2, "one iteration in flight while the previous one is read");
     int it = 1;

@@ -116,7 +116,7 @@ class Engine {
         d_cov64_, d_conf64_, d_knn_, d_corr_idx_, d_corr_dist_, d_flag_list_, d_flag_count_,
         d_trim_key_, d_red_partial_, d_red_out_, d_work_, d_wb_, d_wn_, d_chunks_, d_partial_, d_centers_,
         d_rechecked_, d_keys0_, d_keys1_, d_vals1_, d_sort_tmp_, d_stats_, d_qlist_, d_qcount_, d_hist_, d_cert_d1_,
-        d_cert_l2_, d_cert_it_, d_margin_, d_sqlist_, d_state_, d_ctl_, d_trim_cand_, d_trim_ctr_, d_scales_, d_trim_hist_;
+        d_cert_l2_, d_cert_it_, d_margin_, d_sqlist_, d_state_, d_trim_cand_, d_trim_ctr_, d_scales_, d_trim_hist_;
     TreeBufs t3_, t12_;
     // pinned host mirrors
     PairDev* h_pairs_ = nullptr;
@@ -126,8 +126,11 @@ class Engine {
     double* h_hist_ = nullptr;  // one pose-history row (npairs x 12)
     size_t h_pairs_cap_ = 0, h_red_cap_ = 0, h_partial_cap_ = 0, h_rechecked_cap_ = 0, h_hist_cap_ = 0;
     PairState* h_state_ = nullptr;  // loop state of every pair (read back after the loop)
-    int32_t* h_ctl_ = nullptr;      // [kLoopRing][4] pairs active in the next iteration (all, SE(3), R3)
-    size_t h_state_cap_ = 0, h_ctl_cap_ = 0;
+    // [kLoopRing][npairs] each pair's phase in the next iteration, written by k_reduce_final
+    // into coherent host memory (h_phase_ host view, d_phase_ device view)
+    int32_t* h_phase_ = nullptr;
+    int32_t* d_phase_ = nullptr;
+    size_t h_state_cap_ = 0, h_phase_cap_ = 0;
     unsigned long long* h_lrf_stats_ = nullptr;  // k_lrf work counters (read at the next sync)
     size_t h_lrf_stats_cap_ = 0;
     bool lrf_stats_pending_ = false;

@@ -624,16 +624,18 @@ __global__ __launch_bounds__(256) void k_reduce(View v) {
 // closes the pair's iteration `it` on the device (estimator solve, pose update,
 // switch / convergence: pairmath.hpp) and opens iteration it+1 (PairDev, pose history
 // row), so the next iteration's kernels are already queued behind this one.
-// ctl[it & 1][0..2] counts the pairs active in iteration it+1 (all, SE(3), R3).
+// next_phase[p] receives pair p's phase in iteration it+1 (PHASE_IDLE once finished); it
+// lives in coherent host memory, so the host reads it once the kernel has completed,
+// without a copy.
 __global__ __launch_bounds__(256) void k_reduce_final(View v, const int32_t* pair_wb, const int32_t* pair_wn,
-                                                      PairState* state, double* hist, int32_t* ctl, int it) {
+                                                      PairState* state, double* hist, int32_t* next_phase) {
     const int p = blockIdx.x;
-    if ((int)(p == 0) & (int)(threadIdx.x < 4)) {
-        ctl[4 * ((it + 1) & 1) + threadIdx.x] = 0;             // counters of the next iteration
-        if (threadIdx.x < 3) v.flag_count[threadIdx.x] = 0;    // recheck / single-query lists
-    }
+    if ((int)(p == 0) & (int)(threadIdx.x < 3)) v.flag_count[threadIdx.x] = 0;  // recheck / single-query lists
     PairDev* P = v.pairs + p;
-    if (P->phase == PHASE_IDLE) return;
+    if (P->phase == PHASE_IDLE) {
+        if (threadIdx.x == 0) next_phase[p] = PHASE_IDLE;
+        return;
+    }
     __shared__ double part[8][kRedVals];
     __shared__ double tot[kRedVals];
     const int i = threadIdx.x % kRedVals, s = threadIdx.x / kRedVals;
@@ -665,10 +667,8 @@ __global__ __launch_bounds__(256) void k_reduce_final(View v, const int32_t* pai
         if (!S.done) {
             double* h = hist + ((size_t)(S.iter % kHist) * v.npairs + p) * 12;
             for (int k = 0; k < 12; ++k) h[k] = P->T[k];
-            int32_t* c = ctl + 4 * (it & 1);
-            atomicAdd(c, 1);
-            atomicAdd(c + (P->phase == PHASE_SE3 ? 1 : 2), 1);
         }
+        next_phase[p] = P->phase;
     }
 }
 
@@ -682,9 +682,9 @@ void launch_trim(const View& v, hipStream_t s) {
     hipLaunchKernelGGL(k_trim, dim3(v.npairs), dim3(1024), 0, s, v);
 }
 void launch_reduce(const View& v, const int32_t* pair_wb, const int32_t* pair_wn, PairState* state, double* hist,
-                   int32_t* ctl, int it, hipStream_t s) {
+                   int32_t* next_phase, hipStream_t s) {
     hipLaunchKernelGGL(k_reduce, dim3(v.nwork), dim3(256), 0, s, v);
-    hipLaunchKernelGGL(k_reduce_final, dim3(v.npairs), dim3(256), 0, s, v, pair_wb, pair_wn, state, hist, ctl, it);
+    hipLaunchKernelGGL(k_reduce_final, dim3(v.npairs), dim3(256), 0, s, v, pair_wb, pair_wn, state, hist, next_phase);
 }
 
 }  // namespace se3icp

@@ -125,10 +125,10 @@ void launch_nn_se3(const View& v, hipStream_t s);
 void launch_nn_r3(const View& v, hipStream_t s);
 void launch_recheck(const View& v, int nblocks, hipStream_t s);
 void launch_trim(const View& v, hipStream_t s);
-// reduce + (k_reduce_final) per-pair solve and loop state machine; ctl[(it & 1) * 4 + 0..2]
-// receives the number of pairs active in iteration it+1 (all, SE(3) phase, R3 phase)
+// reduce + (k_reduce_final) per-pair solve and loop state machine; next_phase[p] receives
+// pair p's phase in the next iteration (PHASE_IDLE: finished)
 struct PairState;
 void launch_reduce(const View& v, const int32_t* pair_wb, const int32_t* pair_wn, PairState* state, double* hist,
-                   int32_t* ctl, int it, hipStream_t s);
+                   int32_t* next_phase, hipStream_t s);
 
 }  // namespace se3icp
