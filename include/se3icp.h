@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SE3ICP_ABI_VERSION 1
+#define SE3ICP_ABI_VERSION 2
 
 typedef enum se3icp_status {
     SE3ICP_OK = 0,
@@ -89,6 +89,9 @@ typedef struct se3icp_result {
     double time_setup_ms;             /* normalization + TOLDI + normals (batch, GPU timeline) */
     double time_loop_ms;              /* ICP loop (batch, GPU timeline)                        */
     double time_se3_correspondence_search_ms; /* time_se3_correspondence_search_ */
+    double time_before_pure_icp_ms;   /* time_before_pure_icp_: the whole run_se3_icp_with_cf
+                                         (ISR.cpp:754, 957-958), GPU timeline; 0 for the other
+                                         methods (the reference never sets it there) */
 } se3icp_result;
 
 /* ------------------------------------------------------------- misc */
@@ -189,6 +192,35 @@ int64_t se3icp_synthetic_pairs(int device, const double* base, int64_t n, int32_
  *            (NN certificates: queries of all iterations / those searched) */
 int se3icp_set_profiling(int device, int on);
 int se3icp_last_kernel_times(int device, double* out);
+
+/* Per-iteration correspondence record of ONE pair of the next batch registered on
+ * `device` (diagnostic; the parity tests compare it with the reference's loop
+ * iteration by iteration).  Each row it (0-based) holds what iteration it+1 built:
+ *   corr_idx / corr_dist  the pre-trim correspondence of every source point: target
+ *                         index and the float distance of the pcl::Correspondence
+ *                         (ISR.cpp:444-470 SE(3) phase, 402-416 R3 phase);
+ *   trim_key              the trimmed rejector's cut (ISR.cpp:669-671): source point i
+ *                         is kept iff (float bits of corr_dist[i]) << 32 | i <= trim_key;
+ *                         UINT64_MAX when nothing is trimmed (overlap 1);
+ *   T, mse                current_estimated_T_ after the iteration (normalized frame,
+ *                         row-major) and the MSE it computed (ISR.cpp:684-711);
+ *   phase                 1 = SE(3) correspondences, 2 = R3.
+ * Any array may be NULL.  The record is armed by se3icp_set_trace (pointers are kept
+ * until that batch returns, then the trace disarms itself; NULL disarms) and makes the
+ * batch wait for every iteration (slower; never used by bench.py). */
+typedef struct se3icp_trace {
+    int32_t pair;            /* pair index within the next batch */
+    int32_t max_iters;       /* rows of the arrays below */
+    int32_t* corr_idx;       /* [max_iters * n_src] */
+    float* corr_dist;        /* [max_iters * n_src] */
+    uint64_t* trim_key;      /* [max_iters] */
+    double* T;               /* [max_iters * 16] */
+    double* mse;             /* [max_iters] */
+    int32_t* phase;          /* [max_iters] */
+    int32_t iters_recorded;  /* out: rows written */
+    int32_t _reserved;
+} se3icp_trace;
+int se3icp_set_trace(int device, se3icp_trace* trace);
 
 #ifdef __cplusplus
 }

@@ -904,19 +904,48 @@ struct Registration {
         for (size_t i = 0; i < ns; i++) {
             if (trace->corr_idx) trace->corr_idx[(size_t)it * ns + i] = raw[i].m;
             if (trace->corr_dist) trace->corr_dist[(size_t)it * ns + i] = raw[i].dist;
+            if (trace->corr_d2 && i < nn_d2a.size()) trace->corr_d2[(size_t)it * ns + i] = nn_d2a[i];
+            if (trace->corr_idx2 && i < nn_idx2.size()) trace->corr_idx2[(size_t)it * ns + i] = nn_idx2[i];
+            if (trace->corr_d2b && i < nn_d2b.size()) trace->corr_d2b[(size_t)it * ns + i] = nn_d2b[i];
         }
+    }
+    // margins of the last search (filled only while a trace asks for them)
+    std::vector<double> nn_d2a, nn_d2b;
+    std::vector<int> nn_idx2;
+    bool want_margin() const { return trace && (trace->corr_d2 || trace->corr_idx2 || trace->corr_d2b); }
+    // the search of one query: 1-NN, or 2-NN (same first result) when margins are traced
+    void search1(const KDTree& tree, const double* q, int i, int& idx, double& d2) {
+        if (!want_margin()) {
+            tree.knn(q, 1, &idx, &d2);
+            return;
+        }
+        int ii[2] = {-1, -1};
+        double dd[2] = {0, std::numeric_limits<double>::infinity()};
+        tree.knn(q, 2, ii, dd);
+        idx = ii[0];
+        d2 = dd[0];
+        nn_d2a[i] = dd[0];
+        nn_idx2[i] = ii[1];
+        nn_d2b[i] = dd[1];
+    }
+    void margins(int n) {
+        if (!want_margin()) return;
+        nn_d2a.assign(n, 0.0);
+        nn_idx2.assign(n, -1);
+        nn_d2b.assign(n, std::numeric_limits<double>::infinity());
     }
 
     // ISR.cpp:402-416
     void nn_xyz(const KDTree& tree, std::vector<Corr>& corr) {
         const int n = (int)source_moving_.points.size();
         corr.resize(n);
+        margins(n);
 #pragma omp parallel for schedule(dynamic, 512)
         for (int i = 0; i < n; i++) {
             const double q[3] = {source_moving_.points[i].x, source_moving_.points[i].y, source_moving_.points[i].z};
             int idx = -1;
             double d2 = 0;
-            tree.knn(q, 1, &idx, &d2);
+            search1(tree, q, i, idx, d2);
             corr[i] = Corr{i, idx, float(std::sqrt(d2))};
         }
     }
@@ -924,13 +953,14 @@ struct Registration {
     void nn_se3(const KDTree& tree, std::vector<Corr>& corr) {
         const int n = (int)source_se3_cloud_.size();
         corr.resize(n);
+        margins(n);
 #pragma omp parallel for schedule(dynamic, 512)
         for (int i = 0; i < n; i++) {
             double q[12];
             se3_vec(source_se3_cloud_[i], q);
             int idx = -1;
             double d2 = 0;
-            tree.knn(q, 1, &idx, &d2);
+            search1(tree, q, i, idx, d2);
             const Mat4& Mt = target_se3_cloud_[idx];
             Vec3 dv(source_se3_cloud_[i].m[0][3] - Mt.m[0][3], source_se3_cloud_[i].m[1][3] - Mt.m[1][3],
                     source_se3_cloud_[i].m[2][3] - Mt.m[2][3]);

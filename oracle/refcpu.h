@@ -65,6 +65,11 @@ typedef struct refcpu_result {
  *   n_kept    [max_trace_iters]     trimmed correspondence count
  *   corr_idx  [max_trace_iters*n_src] NN target index per source point (pre-trim)
  *   corr_dist [max_trace_iters*n_src] float distance stored in the PCL correspondence
+ *   corr_d2   [max_trace_iters*n_src] squared search distance (12-D or 3-D) of the match
+ *   corr_idx2 [max_trace_iters*n_src] second-nearest target (a 2-NN search when set)
+ *   corr_d2b  [max_trace_iters*n_src] its squared search distance
+ * (the last three measure each query's arg-min margin, so a parity test can tell a
+ *  rounding-level near-tie from a wrong correspondence)
  */
 typedef struct refcpu_trace {
     int32_t max_trace_iters;
@@ -74,6 +79,9 @@ typedef struct refcpu_trace {
     int32_t* n_kept;
     int32_t* corr_idx;
     float* corr_dist;
+    double* corr_d2;
+    int32_t* corr_idx2;
+    double* corr_d2b;
 } refcpu_trace;
 
 void refcpu_default_params(refcpu_params* p);

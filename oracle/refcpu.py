@@ -55,6 +55,9 @@ class Trace(C.Structure):
         ("n_kept", C.POINTER(C.c_int32)),
         ("corr_idx", C.POINTER(C.c_int32)),
         ("corr_dist", C.POINTER(C.c_float)),
+        ("corr_d2", C.POINTER(C.c_double)),
+        ("corr_idx2", C.POINTER(C.c_int32)),
+        ("corr_d2b", C.POINTER(C.c_double)),
     ]
 
 
@@ -120,8 +123,10 @@ def num_threads() -> int:
 
 
 def register(src, tgt, run_kind=RUN_SE3_ICP, variant="pt2pl", params: Params | None = None,
-             trace_iters: int = 0):
-    """Run the restated registration.  Returns a dict (and trace arrays if requested)."""
+             trace_iters: int = 0, trace_margins: bool = False):
+    """Run the restated registration.  Returns a dict (and trace arrays if requested;
+    trace_margins adds each query's squared search distance and its second-nearest
+    target from a 2-NN search)."""
     src = np.ascontiguousarray(src, dtype=np.float64)
     tgt = np.ascontiguousarray(tgt, dtype=np.float64)
     params = params or default_params()
@@ -135,8 +140,13 @@ def register(src, tgt, run_kind=RUN_SE3_ICP, variant="pt2pl", params: Params | N
         out["n_kept"] = np.zeros(trace_iters, np.int32)
         out["corr_idx"] = np.full((trace_iters, ns), -1, np.int32)
         out["corr_dist"] = np.zeros((trace_iters, ns), np.float32)
+        if trace_margins:
+            out["corr_d2"] = np.zeros((trace_iters, ns))
+            out["corr_idx2"] = np.full((trace_iters, ns), -1, np.int32)
+            out["corr_d2b"] = np.zeros((trace_iters, ns))
         tr = Trace(trace_iters, 0, _d(out["Ti"]), _d(out["mse"]), _i(out["n_kept"]), _i(out["corr_idx"]),
-                   out["corr_dist"].ctypes.data_as(C.POINTER(C.c_float)))
+                   out["corr_dist"].ctypes.data_as(C.POINTER(C.c_float)), _d(out.get("corr_d2")),
+                   _i(out.get("corr_idx2")), _d(out.get("corr_d2b")))
     v = VARIANTS[variant] if isinstance(variant, str) else int(variant)
     rc = lib().refcpu_register(_d(src), src.shape[0], _d(tgt), tgt.shape[0], run_kind, v, C.byref(params),
                                C.byref(res), C.byref(tr) if tr is not None else None)

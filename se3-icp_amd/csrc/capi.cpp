@@ -215,7 +215,10 @@ int se3icp_run_se3_icp(se3icp_registration* r, const char* variant) {
 
 int se3icp_run_se3_icp_with_cf(se3icp_registration* r) {
     if (!r) return SE3ICP_ERR_INVALID_ARG;
-    return run_object(r, SE3ICP_SE3_GICP_WITH_CF);
+    const int rc = run_object(r, SE3ICP_SE3_GICP_WITH_CF);
+    if (rc == SE3ICP_OK || rc == SE3ICP_ERR_NONFINITE)  // ISR.cpp:794 (printed once the run returns)
+        std::cout << "### scaling factor = " << r->res.scaling_factor << std::endl;
+    return rc;
 }
 
 int se3icp_run_se3_pure(se3icp_registration* r, const char* variant) {
@@ -225,7 +228,9 @@ int se3icp_run_se3_pure(se3icp_registration* r, const char* variant) {
         std::cerr << "Invalid variant name. Choose one of: pt2pt, pt2pl, gicp \n";
         return SE3ICP_ERR_INVALID_METHOD;
     }
-    return run_object(r, SE3ICP_SE3_PURE_PT2PT + v);
+    const int rc = run_object(r, SE3ICP_SE3_PURE_PT2PT + v);
+    if (rc == SE3ICP_OK || rc == SE3ICP_ERR_NONFINITE) std::cout << "pure se3 finished" << std::endl;  // ISR.cpp:1127
+    return rc;
 }
 
 int se3icp_get_result(const se3icp_registration* r, se3icp_result* out) {
@@ -270,6 +275,15 @@ int se3icp_set_profiling(int device, int on) {
     Engine* e = usable_engine(device);
     if (!e) return SE3ICP_ERR_NO_DEVICE;
     e->set_profiling(on != 0);
+    return 0;
+}
+
+int se3icp_set_trace(int device, se3icp_trace* trace) {
+    Engine* e = usable_engine(device);
+    if (!e) return SE3ICP_ERR_NO_DEVICE;
+    if (trace && (trace->max_iters < 0 || trace->pair < 0)) return SE3ICP_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(e->mutex());
+    e->set_trace(trace);
     return 0;
 }
 

@@ -434,7 +434,11 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
                            const int64_t* nt, bool on_device, int method, const se3icp_params& prm,
                            se3icp_result* out, hipStream_t user_stream) {
     if (!ok_) return SE3ICP_ERR_NO_DEVICE;
+    se3icp_trace* tr = trace_;  // one-shot: the record covers this batch only
+    trace_ = nullptr;
     if (npairs <= 0 || !src || !tgt || !ns || !nt || !out) return SE3ICP_ERR_INVALID_ARG;
+    if (tr && (tr->pair < 0 || tr->pair >= npairs || tr->max_iters < 0)) return SE3ICP_ERR_INVALID_ARG;
+    if (tr) tr->iters_recorded = 0;
     MethodInfo mi;
     if (!decode_method(method, &mi)) return SE3ICP_ERR_INVALID_METHOD;
     for (int p = 0; p < npairs; ++p) {
@@ -589,7 +593,8 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     // queued while any pair may be in it: SE(3) until a finished iteration shows none
     // left, R3 from iteration 2 on (a pair may switch after any iteration).
     // SE3ICP_NN_TRACE waits for every iteration (per-iteration work counters).
-    const int lag = nn_trace_ ? 0 : 1;
+    const int lag = (nn_trace_ || tr) ? 0 : 1;
+    int trace_phase = tr ? h_pairs_[tr->pair].phase : 0;  // phase of the iteration being recorded
     auto enqueue = [&](int it) -> int {
         hipEvent_t* ev = &loop_ev_[(it % kLoopRing) * kLoopEv];
         // SE(3) phase: iterations 1..max_num_se3_iterations at most (ISR.cpp:718-723, 1118)
@@ -669,7 +674,12 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     if (enqueue(it)) return SE3ICP_ERR_HIP;
     for (;;) {
         if (lag == 0) {
-            if (finish(it) == 0) break;
+            const int left = finish(it);
+            if (tr) {
+                rc = record_trace(tr, it, trace_phase, s);
+                if (rc) return rc;
+            }
+            if (left == 0) break;
             ++it;
             if (enqueue(it)) return SE3ICP_ERR_HIP;
             continue;
@@ -739,9 +749,47 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         R.time_setup_ms = setup_ms;
         R.time_loop_ms = loop_ms;
         R.time_se3_correspondence_search_ms = nn_ms;
+        R.time_before_pure_icp_ms = mi.kind == KIND_CF ? (double)(setup_ms + loop_ms) : 0.0;
         if (R.status != SE3ICP_OK) worst = R.status;
     }
     return worst;
+}
+
+// Row it-1 of the armed trace after iteration `it` completed (the stream is idle: the
+// trace runs the loop without look-ahead).  phase_of_it: the pair's phase in iteration
+// it, updated to its phase in iteration it+1.
+int Engine::record_trace(se3icp_trace* tr, int it, int& phase_of_it, hipStream_t s) {
+    const int p = tr->pair;
+    PairState S;
+    HIPCHK(hipMemcpyAsync(&S, (const PairState*)d_state_.p + p, sizeof(S), hipMemcpyDeviceToHost, s));
+    uint64_t cut = UINT64_MAX;
+    if (h_pairs_[p].trim) HIPCHK(hipMemcpyAsync(&cut, (const uint64_t*)d_trim_key_.p + p, sizeof(cut), hipMemcpyDeviceToHost, s));
+    const int phase = phase_of_it;
+    const int r = it - 1;
+    const bool active = phase != PHASE_IDLE && r < tr->max_iters;
+    const CloudDev& cs = h_clouds_[2 * p];
+    if (active) {
+        if (tr->corr_idx)
+            HIPCHK(hipMemcpyAsync(tr->corr_idx + (size_t)r * cs.n, (const int32_t*)d_corr_idx_.p + cs.off,
+                                  sizeof(int32_t) * cs.n, hipMemcpyDeviceToHost, s));
+        if (tr->corr_dist)
+            HIPCHK(hipMemcpyAsync(tr->corr_dist + (size_t)r * cs.n, (const float*)d_corr_dist_.p + cs.off,
+                                  sizeof(float) * cs.n, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    if (active) {
+        // a pair that took part in iteration it has iter >= it (one that finished at j keeps j)
+        if (S.iter < it) return SE3ICP_ERR_HIP;
+        if (tr->trim_key) tr->trim_key[r] = cut;
+        if (tr->T)
+            for (int i = 0; i < 4; ++i)
+                for (int j = 0; j < 4; ++j) tr->T[(size_t)r * 16 + 4 * i + j] = S.T.m[i][j];
+        if (tr->mse) tr->mse[r] = S.mse_cur;
+        if (tr->phase) tr->phase[r] = phase;
+        tr->iters_recorded = it;
+    }
+    phase_of_it = S.done ? PHASE_IDLE : S.phase;
+    return 0;
 }
 
 // ----------------------------------------------------------------------------- stage entry points

@@ -49,6 +49,7 @@ class Engine {
     int device() const { return dev_; }
     std::mutex& mutex() { return mu_; }
     void set_profiling(bool on) { profile_ = on; }
+    void set_trace(se3icp_trace* t) { trace_ = t; }
     const KernelTimes& kernel_times() const { return ktimes_; }
 
     int register_batch(int npairs, const double* const* src, const int64_t* ns, const double* const* tgt,
@@ -102,6 +103,8 @@ class Engine {
     int chunk_level_ = 0, nchunks_ = 0;  // loop NN work chunks (View::chunk_level)
     bool have12_ = false, knn_list_ = false;
     bool nn_trace_ = false;              // SE3ICP_NN_TRACE=1: per-iteration NN work on stderr
+    se3icp_trace* trace_ = nullptr;      // armed per-iteration record of one pair (se3icp_set_trace)
+    int record_trace(se3icp_trace* tr, int it, int& phase_of_it, hipStream_t s);
     double trace_prev_[kStatCols] = {};
     int l12_extra_ = 0;  // extra levels of the 12-D trees (0: leaves of <= 64 targets, measured fastest with compacted sweeps)
     std::vector<CloudDev> h_clouds_;

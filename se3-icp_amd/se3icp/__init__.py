@@ -8,10 +8,10 @@ from ._lib import (MAX_KNN, METHODS, Params, Result, Se3IcpError, default_params
 from .io import read_ply_xyz, write_ply_xyz  # noqa: F401
 from .registration import (IterativeSE3Registration, PairResult, cli_params, estimate_normals,  # noqa: F401
                            kitti_params, knn_self, last_kernel_times, set_profiling, lounge_params, nearest_neighbors,
-                           register_batch, register_batch_device, toldi_frames)
+                           register_batch, register_batch_device, register_batch_traced, toldi_frames)
 
 __all__ = [
-    "IterativeSE3Registration", "register_batch", "register_batch_device", "toldi_frames", "knn_self",
+    "IterativeSE3Registration", "register_batch", "register_batch_device", "register_batch_traced", "toldi_frames", "knn_self",
     "estimate_normals", "nearest_neighbors", "default_params", "cli_params", "kitti_params", "lounge_params",
     "read_ply_xyz", "write_ply_xyz", "METHODS", "MAX_KNN", "Se3IcpError",
 ]

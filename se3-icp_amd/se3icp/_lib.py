@@ -36,7 +36,7 @@ EXPORTED_SYMBOLS = [
     "se3icp_register_batch", "se3icp_register_batch_device", "se3icp_register",
     "se3icp_toldi_frames", "se3icp_knn_self", "se3icp_estimate_normals", "se3icp_nn",
     "se3icp_synthetic_pairs",
-    "se3icp_set_profiling", "se3icp_last_kernel_times",
+    "se3icp_set_profiling", "se3icp_last_kernel_times", "se3icp_set_trace",
     # include/se3icp_cc.h: metrics and pose files of the benchmark drivers (host only)
     "se3icp_cc_rot_3d", "se3icp_cc_angular_error_so3", "se3icp_cc_angular_error_so3_alt",
     "se3icp_cc_error_filterreg", "se3icp_cc_rot2euler", "se3icp_cc_avg_eul_error",
@@ -72,6 +72,22 @@ class Result(C.Structure):
         ("time_setup_ms", C.c_double),
         ("time_loop_ms", C.c_double),
         ("time_se3_correspondence_search_ms", C.c_double),
+        ("time_before_pure_icp_ms", C.c_double),
+    ]
+
+
+class Trace(C.Structure):
+    _fields_ = [
+        ("pair", C.c_int32),
+        ("max_iters", C.c_int32),
+        ("corr_idx", C.POINTER(C.c_int32)),
+        ("corr_dist", C.POINTER(C.c_float)),
+        ("trim_key", C.POINTER(C.c_uint64)),
+        ("T", C.POINTER(C.c_double)),
+        ("mse", C.POINTER(C.c_double)),
+        ("phase", C.POINTER(C.c_int32)),
+        ("iters_recorded", C.c_int32),
+        ("_reserved", C.c_int32),
     ]
 
 
@@ -130,6 +146,7 @@ def load():
                                          vp, vp, C.c_int]
     L.se3icp_set_profiling.argtypes = [C.c_int, C.c_int]
     L.se3icp_last_kernel_times.argtypes = [C.c_int, dp]
+    L.se3icp_set_trace.argtypes = [C.c_int, C.POINTER(Trace)]
     _lib = L
     return L
 

@@ -59,7 +59,6 @@ class IterativeSE3Registration:
         # constructor state of the reference (ISR.cpp:334-348); lrf_radius_ is only used by
         # the dead SHOT code path (ISR.cpp:593-594)
         object.__setattr__(self, "lrf_radius_", 0.8)
-        object.__setattr__(self, "time_before_pure_icp_", 0.0)
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -106,16 +105,13 @@ class IterativeSE3Registration:
 
     def run_se3_icp_with_cf(self):
         """SE(3)-GICP with depth confidences (ISR.cpp:742-959)."""
-        rc = self._L.se3icp_run_se3_icp_with_cf(self._h)
-        self._L.se3icp_get_result(self._h, C.byref(self._res))
-        print(f"### scaling factor = {self._res.scaling_factor:g}")  # ISR.cpp:794
-        return self._finish(rc)
+        # the C-ABI prints the reference's "### scaling factor = s" line (ISR.cpp:794)
+        return self._finish(self._L.se3icp_run_se3_icp_with_cf(self._h))
 
     def run_se3_pure(self, variant_name: str):
         """SE(3) correspondences only, never switching to R3 (ISR.cpp:962-1127)."""
-        rc = self._finish(self._L.se3icp_run_se3_pure(self._h, variant_name.encode()))
-        print("pure se3 finished")
-        return rc
+        # the C-ABI prints the reference's "pure se3 finished" (ISR.cpp:1127)
+        return self._finish(self._L.se3icp_run_se3_pure(self._h, variant_name.encode()))
 
     # ---- results (ISR.hpp:92-98)
     @property
@@ -133,6 +129,10 @@ class IterativeSE3Registration:
     @property
     def time_se3_correspondence_search_(self) -> float:
         return float(self._res.time_se3_correspondence_search_ms)
+
+    @property
+    def time_before_pure_icp_(self) -> float:
+        return float(self._res.time_before_pure_icp_ms)
 
     @property
     def num_rechecked(self) -> int:
@@ -154,6 +154,7 @@ class PairResult:
     time_setup_ms: float
     time_loop_ms: float
     time_nn_ms: float
+    time_before_pure_icp_ms: float
 
 
 def _results(res, n) -> list[PairResult]:
@@ -162,7 +163,8 @@ def _results(res, n) -> list[PairResult]:
         r = res[i]
         out.append(PairResult(np.array(r.T).reshape(4, 4), int(r.num_iterations), int(r.num_pure_se3_iterations),
                               int(r.status), int(r.num_rechecked), float(r.scaling_factor), float(r.time_setup_ms),
-                              float(r.time_loop_ms), float(r.time_se3_correspondence_search_ms)))
+                              float(r.time_loop_ms), float(r.time_se3_correspondence_search_ms),
+                              float(r.time_before_pure_icp_ms)))
     return out
 
 
@@ -230,6 +232,31 @@ def register_batch_device(src_ptr: int, src_off, tgt_ptr: int, tgt_off, method: 
     if rc not in (_lib.OK, _lib.ERR_NONFINITE):
         raise _lib.Se3IcpError(rc, "register_batch_device")
     return _results(res, n)
+
+
+def register_batch_traced(pairs, method: str, params: _lib.Params | None = None, pair: int = 0,
+                          max_iters: int = 160, device: int = 0):
+    """register_batch with the per-iteration record of one pair (se3icp_set_trace): the
+    pre-trim correspondence set (target index, float distance) of every iteration, the
+    trimmed rejector's cut, the pose and the MSE after it and the phase it ran in.
+    Returns (results, trace dict with arrays cut to the recorded iterations)."""
+    L = _lib.load()
+    ns = _as_xyz(pairs[pair][0]).shape[0]
+    tr = {"corr_idx": np.full((max_iters, ns), -1, np.int32), "corr_dist": np.zeros((max_iters, ns), np.float32),
+          "trim_key": np.zeros(max_iters, np.uint64), "T": np.zeros((max_iters, 4, 4)), "mse": np.zeros(max_iters),
+          "phase": np.zeros(max_iters, np.int32)}
+    t = _lib.Trace(pair, max_iters, tr["corr_idx"].ctypes.data_as(C.POINTER(C.c_int32)),
+                   tr["corr_dist"].ctypes.data_as(C.POINTER(C.c_float)),
+                   tr["trim_key"].ctypes.data_as(C.POINTER(C.c_uint64)), tr["T"].ctypes.data_as(C.POINTER(C.c_double)),
+                   tr["mse"].ctypes.data_as(C.POINTER(C.c_double)), tr["phase"].ctypes.data_as(C.POINTER(C.c_int32)),
+                   0, 0)
+    _lib.check(L.se3icp_set_trace(device, C.byref(t)), "set_trace")
+    try:
+        res = register_batch(pairs, method, params, device)
+    finally:
+        L.se3icp_set_trace(device, None)
+    n = int(t.iters_recorded)
+    return res, {k: v[:n] for k, v in tr.items()}
 
 
 # ---- stage entry points (one per reference function on the hot path)

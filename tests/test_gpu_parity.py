@@ -291,3 +291,89 @@ def test_batch_with_pairs_finishing_at_different_iterations(se3icp_mod, refcpu, 
         assert abs(g.num_iterations - ref["num_iterations"]) <= 1
         its.append(g.num_iterations)
     assert len(set(its)) > 1, its  # the batch really had pairs finishing at different iterations
+
+
+# --------------------------------------------------------------------------- BASELINE configs at size
+def _rot_deg(A, B):
+    R = A[:3, :3].T @ B[:3, :3]
+    return float(np.degrees(np.arccos(np.clip((np.trace(R) - 1) / 2, -1, 1))))
+
+
+def test_c2_full_unique_bunny_se3_pt2pt(se3icp_mod, refcpu, bunny_unique):
+    """C2: se3_pt2pt on the whole unique bunny (34,834 points, x50, noise variance 0.005,
+    examples/benchmark_synthetic.cpp:91-160), the driver's parameters (B_SYN:356-363),
+    no subsampling; correspondences checked at every iteration (test_gpu_trace)."""
+    from se3icp import datasets
+    from test_gpu_trace import compare_traces
+    src, tgt, T_gt = datasets.bunny_pair(bunny_unique, seed=1)
+    assert src.shape[0] == tgt.shape[0] == 34834
+    res, gtr = se3icp_mod.register_batch_traced([(src, tgt)], "se3_pt2pt", se3icp_mod.cli_params())
+    ref = refcpu.register(src, tgt, refcpu.RUN_SE3_ICP, "pt2pt", refcpu.cli_params(), trace_iters=160,
+                          trace_margins=True)
+    g = res[0]
+    assert np.linalg.norm(g.T - ref["T"]) <= 1e-5
+    assert g.num_iterations == ref["num_iterations"]
+    assert g.num_pure_se3_iterations == ref["num_pure_se3_iterations"]
+    compare_traces(gtr, ref, 1.0, "C2 bunny 34.8k se3_pt2pt")
+    # B_SYN:238-246 success thresholds
+    assert _rot_deg(g.T, T_gt) <= 2.0 and np.linalg.norm(g.T[:3, 3] - T_gt[:3, 3]) <= 0.25
+
+
+def test_c3_rgbd_batch32_se3_pt2pl(se3icp_mod, refcpu):
+    """C3: a 32-pair se3_pt2pl batch of consecutive RGB-D frames at the default stride
+    (~16k points, the lounge surrogate), examples/benchmark_lounge.cpp:183-189 parameters;
+    every pair against its own oracle run."""
+    from se3icp import datasets
+    pairs, gts = datasets.rgbd_pairs(32, seed=3, stride=4)
+    npts = [p[0].shape[0] for p in pairs]
+    assert min(npts) > 10_000, npts
+    got = se3icp_mod.register_batch(pairs, "se3_pt2pl", se3icp_mod.lounge_params())
+    rp = refcpu.default_params(estimated_overlap=0.75, max_num_se3_iterations=10, mse_switch_error=5e-5,
+                               number_of_nn_for_LRF=90)
+    worst, its_diff = 0.0, 0
+    for (s, t), g in zip(pairs, got):
+        ref = refcpu.register(s, t, refcpu.RUN_SE3_ICP, "pt2pl", rp)
+        worst = max(worst, float(np.linalg.norm(g.T - ref["T"])))
+        its_diff += g.num_iterations != ref["num_iterations"]
+        assert np.linalg.norm(g.T - ref["T"]) <= 1e-5, (g.T, ref["T"])
+    print(f"[C3] 32 pairs, mean {np.mean(npts):.0f} points: max |T_gpu - T_ref|_F {worst:.2e}, "
+          f"iteration-count differences {its_diff}")
+    assert its_diff == 0
+
+
+def test_c5_rgbd_batch256_se3_gicp_with_cf(se3icp_mod, refcpu):
+    """C5: a 256-pair run_se3_icp_with_cf batch (ISR.cpp:742-959) on the RGB-D surrogate.
+    Eight fixed pairs against the oracle; all 256 against the ground truth with the
+    reference's success thresholds (SO(3) error <= 2 deg, translation <= 0.25,
+    examples/benchmark_synthetic.cpp:238-246)."""
+    from se3icp import datasets
+    pairs, gts = datasets.rgbd_pairs(256, seed=5, stride=4)
+    got = se3icp_mod.register_batch(pairs, "se3_gicp_with_cf", se3icp_mod.lounge_params())
+    assert all(g.status == 0 for g in got)
+    assert all(abs(g.time_before_pure_icp_ms - (g.time_setup_ms + g.time_loop_ms)) < 1e-6 for g in got)
+    rp = refcpu.default_params(estimated_overlap=0.75, max_num_se3_iterations=10, mse_switch_error=5e-5,
+                               number_of_nn_for_LRF=90)
+    for i in range(0, 256, 32):
+        s, t = pairs[i]
+        ref = refcpu.register(s, t, refcpu.RUN_SE3_ICP_CF, "gicp", rp)
+        assert np.linalg.norm(got[i].T - ref["T"]) <= 1e-5, (i, got[i].T, ref["T"])
+        assert got[i].num_iterations == ref["num_iterations"], i
+    rot = np.array([_rot_deg(g.T, gt) for g, gt in zip(got, gts)])
+    tra = np.array([np.linalg.norm(g.T[:3, 3] - gt[:3, 3]) for g, gt in zip(got, gts)])
+    print(f"[C5] 256 pairs: rot err max {rot.max():.3f} deg, trans err max {tra.max():.4f} m, "
+          f"iterations {np.mean([g.num_iterations for g in got]):.1f} mean")
+    assert (rot <= 2.0).all() and (tra <= 0.25).all(), (np.nonzero(rot > 2.0)[0], np.nonzero(tra > 0.25)[0])
+
+
+def test_batch_independence_16_vs_two_8(se3icp_mod):
+    """Pairs registered in one lockstep batch are bitwise the ones registered in smaller
+    batches: the premise of sharding the batch over GPUs."""
+    from se3icp import datasets
+    pairs, _ = datasets.kitti_like_pairs(16, seed=4)
+    p = se3icp_mod.kitti_params()
+    full = se3icp_mod.register_batch(pairs, "se3_gicp", p)
+    a = se3icp_mod.register_batch(pairs[:8], "se3_gicp", p)
+    b = se3icp_mod.register_batch(pairs[8:], "se3_gicp", p)
+    for i, (f, h) in enumerate(zip(full, a + b)):
+        assert np.array_equal(f.T, h.T), (i, f.T - h.T)
+        assert (f.num_iterations, f.num_pure_se3_iterations) == (h.num_iterations, h.num_pure_se3_iterations)
