@@ -31,7 +31,9 @@ def exchange_results(dist, device, elapsed_s: float, loop_s: float, iterations: 
     Returns (elapsed_max, loop_max, iterations_sum, poses_all) where poses_all stacks every
     rank's [n, 4, 4] poses in rank order.  `dist` is torch.distributed (or None for one
     rank); `device` the tensor device of the backend (cuda for nccl/RCCL, cpu for gloo).
-    Every rank must hold the same number of pairs (the gather is fixed-size).
+    Ranks may hold different numbers of pairs (shard() of a batch that does not divide
+    evenly): the pair counts are gathered first and every rank's poses are padded to the
+    largest count for the fixed-size all-gather, then cut back.
     """
     import torch
 
@@ -42,8 +44,15 @@ def exchange_results(dist, device, elapsed_s: float, loop_s: float, iterations: 
     dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     tot = torch.tensor([float(iterations)], dtype=torch.float64, device=device)
     dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-    mine = torch.from_numpy(poses).to(device)
-    gathered = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
+    world = dist.get_world_size()
+    cnt = torch.tensor([poses.shape[0]], dtype=torch.int64, device=device)
+    counts = [torch.empty_like(cnt) for _ in range(world)]
+    dist.all_gather(counts, cnt)
+    counts = [int(c.item()) for c in counts]
+    pad = np.zeros((max(counts), 4, 4))
+    pad[:poses.shape[0]] = poses
+    mine = torch.from_numpy(pad).to(device)
+    gathered = [torch.empty_like(mine) for _ in range(world)]
     dist.all_gather(gathered, mine)
-    allp = np.concatenate([g.cpu().numpy() for g in gathered])
+    allp = np.concatenate([g.cpu().numpy()[:c] for g, c in zip(gathered, counts)])
     return float(t_max[0]), float(t_max[1]), int(round(float(tot[0]))), allp

@@ -44,13 +44,18 @@ def _free_port():
     return port
 
 
-def _rank_main(rank, world, port, out_dir):
+def _rank_poses(rank, n):
+    return np.stack([np.eye(4) * (1 + rank) + k for k in range(n)])
+
+
+def _rank_main(rank, world, port, out_dir, total=None):
     import torch
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    poses = np.stack([np.eye(4) * (1 + rank) + k for k in range(3)])
+    n = 3 if total is None else sharding.shard(total, world, rank)[1]
+    poses = _rank_poses(rank, n)
     res = sharding.exchange_results(dist, torch.device("cpu"), elapsed_s=1.0 + rank, loop_s=0.5 * (rank + 1),
                                     iterations=10 * (rank + 1), poses=poses)
     dist.barrier()
@@ -78,3 +83,18 @@ def test_exchange_results_single_rank_is_identity():
     e, l, it, p = sharding.exchange_results(None, None, 1.5, 0.5, 7, poses)
     assert (e, l, it) == (1.5, 0.5, 7)
     np.testing.assert_array_equal(p, poses)
+
+
+def test_exchange_results_uneven_shards_gloo_world2(tmp_path):
+    """5 pairs over 2 ranks: shard() gives 3 + 2; the gather pads to the largest block and
+    returns exactly the 5 poses in rank order."""
+    import torch.multiprocessing as mp
+
+    world, total = 2, 5
+    mp.start_processes(_rank_main, args=(world, _free_port(), str(tmp_path), total), nprocs=world, join=True,
+                       start_method="spawn")
+    expect = np.concatenate([_rank_poses(r, sharding.shard(total, world, r)[1]) for r in range(world)])
+    assert expect.shape[0] == total
+    for r in range(world):
+        d = np.load(tmp_path / f"r{r}.npz")
+        np.testing.assert_array_equal(d["poses"], expect)
