@@ -217,7 +217,8 @@ def main():
                     "leaves_per_query": round(ktot.get("lrf_leaves", 0.0) / nq, 2),
                     "bound_updates_per_query": round(ktot.get("lrf_merges", 0.0) / nq, 2),
                     "box_tests_per_query": round(ktot.get("lrf_box_tests", 0.0) / nq, 2),
-                    "candidates_per_query": round(ktot.get("lrf_candidates", 0.0) / nq, 2)}
+                    "candidates_per_query": round(ktot.get("lrf_candidates", 0.0) / nq, 2),
+                    "exact_kernel_queries_per_step": ktot.get("lrf_fallback", 0.0) / args.steps}
         roof_nn = nn_roofline(ktot, kms)
         roof_lrf = lrf_roofline(ktot, kms, args.steps, W["params"]["number_of_nn_for_LRF"])
         # the bench line's roofline is the step's dominant kernel by GPU time; the other

@@ -183,13 +183,14 @@ int64_t se3icp_synthetic_pairs(int device, const double* base, int64_t n, int32_
 /* ------------------------------------------------------------- diagnostics
  * Not part of the reference boundary: per-kernel GPU times (HIP events) of the
  * last batch on `device`, used by bench.py for the roofline figures.
- * out[23] = {nn_se3_ms, nn_r3_ms, recheck_ms, trim_ms, reduce_ms, setup_ms,
+ * out[24] = {nn_se3_ms, nn_r3_ms, recheck_ms, trim_ms, reduce_ms, setup_ms,
  *            nn_se3_launches, nn_r3_launches, se3_dist_evals, se3_box_tests,
  *            r3_dist_evals, r3_box_tests,   (evals/tests counted per lane)
  *            lrf_ms, lrf_queries, lrf_leaves, lrf_merges, lrf_box_tests,
  *            lrf_candidates,   (kNN/TOLDI/normals kernel)
- *            nn_prep_ms, se3_queries, se3_searched, r3_queries, r3_searched}
- *            (NN certificates: queries of all iterations / those searched) */
+ *            nn_prep_ms, se3_queries, se3_searched, r3_queries, r3_searched,
+ *            (NN certificates: queries of all iterations / those searched)
+ *            lrf_fallback}  (setup queries handed to the exact one-per-wave kNN kernel) */
 int se3icp_set_profiling(int device, int on);
 int se3icp_last_kernel_times(int device, double* out);
 
@@ -221,6 +222,12 @@ typedef struct se3icp_trace {
     int32_t _reserved;
 } se3icp_trace;
 int se3icp_set_trace(int device, se3icp_trace* trace);
+
+/* Diagnostic: 1 = compute the setup's kNN / TOLDI / normals with the exact one-query-per-
+ * wavefront kernel for every point, 0 = the default (eight queries per wavefront, exact
+ * kernel only for the queries it hands over).  Both give bitwise-identical results; the
+ * tests check that.  Also settable with SE3ICP_LRF_EXACT=1. */
+int se3icp_set_lrf_exact(int device, int exact_only);
 
 #ifdef __cplusplus
 }

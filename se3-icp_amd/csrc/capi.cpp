@@ -287,7 +287,15 @@ int se3icp_set_trace(int device, se3icp_trace* trace) {
     return 0;
 }
 
-int se3icp_last_kernel_times(int device, double* out /* [23] */) {
+int se3icp_set_lrf_exact(int device, int exact_only) {
+    Engine* e = usable_engine(device);
+    if (!e) return SE3ICP_ERR_NO_DEVICE;
+    std::lock_guard<std::mutex> lk(e->mutex());
+    e->set_lrf_exact(exact_only != 0);
+    return 0;
+}
+
+int se3icp_last_kernel_times(int device, double* out /* [24] */) {
     Engine* e = usable_engine(device);
     if (!e || !out) return SE3ICP_ERR_NO_DEVICE;
     const auto& k = e->kernel_times();
@@ -314,6 +322,7 @@ int se3icp_last_kernel_times(int device, double* out /* [23] */) {
     out[20] = k.se3_searched;
     out[21] = k.r3_queries;
     out[22] = k.r3_searched;
+    out[23] = k.lrf_fallback;
     return 0;
 }
 

@@ -96,6 +96,7 @@ int Engine::init() {
     for (auto& e : loop_ev_) HIPCHK(hipEventCreate(&e));
     if (const char* e = std::getenv("SE3ICP_L12_EXTRA")) l12_extra_ = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = std::getenv("SE3ICP_NN_TRACE")) nn_trace_ = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SE3ICP_LRF_EXACT")) lrf_exact_only_ = std::atoi(e) != 0;
     return 0;
 }
 
@@ -108,6 +109,7 @@ Engine::~Engine() {
                      &d_red_out_, &d_work_, &d_wb_, &d_wn_, &d_chunks_, &d_partial_, &d_centers_,
                      &d_rechecked_, &d_keys0_, &d_keys1_, &d_vals1_, &d_sort_tmp_, &d_stats_,
                      &d_qlist_, &d_qcount_, &d_hist_, &d_cert_d1_, &d_cert_l2_, &d_cert_it_, &d_margin_, &d_sqlist_, &d_state_, &d_trim_cand_, &d_trim_ctr_, &d_scales_, &d_trim_hist_,
+                     &d_lrf_fb_, &d_lrf_fbn_,
                      &t3_.perm, &t3_.pos, &t3_.vec, &t3_.blo, &t3_.bhi, &t3_.lo, &t3_.hi,
                      &t12_.perm, &t12_.pos, &t12_.vec, &t12_.blo, &t12_.bhi, &t12_.lo, &t12_.hi};
     for (DevBuf* b : all)
@@ -368,7 +370,22 @@ int Engine::setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool nor
     if (any_knn) {
         HIPCHK(hipMemsetAsync(d_stats_.p, 0, sizeof(unsigned long long) * kStatCols * kStatSlots, s));
         HIPCHK(hipEventRecord(ev_[6], s));
-        launch_lrf(v, knn_list_ ? 1 : 0, s);
+        if (knn_list_ || lrf_exact_only_) {
+            launch_lrf(v, knn_list_ ? 1 : 0, s);  // the sorted lists (se3icp_knn_self) need the exact kernel
+        } else {
+            // eight queries per wavefront; the few it cannot resolve from f32 keys go to
+            // the exact one-query-per-wavefront kernel
+            // waves aligned to each cloud's first point (results independent of the batch)
+            std::vector<int32_t> wb(nclouds_ + 1, 0);
+            for (int c = 0; c < nclouds_; ++c) wb[c + 1] = wb[c] + (h_clouds_[c].n + 7) / 8;
+            if (!ensure<int32_t>(d_lrf_fb_, (size_t)ld_) || !ensure<int32_t>(d_lrf_fbn_, 2 + nclouds_ + 1))
+                return SE3ICP_ERR_OUT_OF_MEMORY;
+            int32_t* d_wb = (int32_t*)d_lrf_fbn_.p + 2;
+            HIPCHK(hipMemsetAsync(d_lrf_fbn_.p, 0, sizeof(int32_t), s));
+            HIPCHK(hipMemcpyAsync(d_wb, wb.data(), sizeof(int32_t) * (nclouds_ + 1), hipMemcpyHostToDevice, s));
+            launch_lrf8(v, d_wb, wb[nclouds_], (int32_t*)d_lrf_fb_.p, (int32_t*)d_lrf_fbn_.p, s);
+            launch_lrf_list(v, (const int32_t*)d_lrf_fb_.p, (const int32_t*)d_lrf_fbn_.p, s);
+        }
         HIPCHK(hipEventRecord(ev_[7], s));
         HIPCHK(hipGetLastError());
         // work counters: copied now, read at the next synchronisation (read_lrf_stats)
@@ -402,8 +419,10 @@ int Engine::read_lrf_stats() {
     ktimes_.lrf_merges = sum[2];
     ktimes_.lrf_box_tests = sum[3];
     ktimes_.lrf_candidates = sum[4];
+    ktimes_.lrf_fallback = sum[6];
 #ifdef SE3ICP_PROF
-    std::fprintf(stderr, "[prof] k_lrf cycles/query: knn %.0f sort %.0f sums %.0f finish %.0f (queries %.0f)\n",
+    std::fprintf(stderr, "[prof] k_lrf cycles/query: knn|scan %.0f sort|tighten %.0f sums|final+sums %.0f finish %.0f "
+                 "(queries %.0f, wave cycles summed over the kernel's waves)\n",
                  sum[8] / sum[0], sum[9] / sum[0], sum[10] / sum[0], sum[11] / sum[0], sum[0]);
 #endif
     return 0;
@@ -749,7 +768,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         R.time_setup_ms = setup_ms;
         R.time_loop_ms = loop_ms;
         R.time_se3_correspondence_search_ms = nn_ms;
-        R.time_before_pure_icp_ms = mi.kind == KIND_CF ? (double)(setup_ms + loop_ms) : 0.0;
+        R.time_before_pure_icp_ms = mi.kind == KIND_CF ? (double)setup_ms + (double)loop_ms : 0.0;
         if (R.status != SE3ICP_OK) worst = R.status;
     }
     return worst;

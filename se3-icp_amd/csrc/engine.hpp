@@ -34,6 +34,7 @@ struct KernelTimes {
     double se3_dist_evals = 0, se3_box_tests = 0, r3_dist_evals = 0, r3_box_tests = 0;
     // fused kNN/TOLDI/normals kernel of the setup: time, queries, leaves scanned, sorts
     double lrf_ms = 0, lrf_queries = 0, lrf_leaves = 0, lrf_merges = 0, lrf_box_tests = 0, lrf_candidates = 0;
+    double lrf_fallback = 0;  // queries k_lrf8 handed to the exact kernel
     // NN certificates (k_nn_prep): its time, and per phase the queries of all iterations
     // and those that had to be searched
     double nn_prep_ms = 0, se3_queries = 0, se3_searched = 0, r3_queries = 0, r3_searched = 0;
@@ -50,6 +51,7 @@ class Engine {
     std::mutex& mutex() { return mu_; }
     void set_profiling(bool on) { profile_ = on; }
     void set_trace(se3icp_trace* t) { trace_ = t; }
+    void set_lrf_exact(bool on) { lrf_exact_only_ = on; }
     const KernelTimes& kernel_times() const { return ktimes_; }
 
     int register_batch(int npairs, const double* const* src, const int64_t* ns, const double* const* tgt,
@@ -103,6 +105,7 @@ class Engine {
     int chunk_level_ = 0, nchunks_ = 0;  // loop NN work chunks (View::chunk_level)
     bool have12_ = false, knn_list_ = false;
     bool nn_trace_ = false;              // SE3ICP_NN_TRACE=1: per-iteration NN work on stderr
+    bool lrf_exact_only_ = false;        // SE3ICP_LRF_EXACT=1: the one-query-per-wavefront k_lrf for every point
     se3icp_trace* trace_ = nullptr;      // armed per-iteration record of one pair (se3icp_set_trace)
     int record_trace(se3icp_trace* tr, int it, int& phase_of_it, hipStream_t s);
     double trace_prev_[kStatCols] = {};
@@ -119,7 +122,8 @@ class Engine {
         d_cov64_, d_conf64_, d_knn_, d_corr_idx_, d_corr_dist_, d_flag_list_, d_flag_count_,
         d_trim_key_, d_red_partial_, d_red_out_, d_work_, d_wb_, d_wn_, d_chunks_, d_partial_, d_centers_,
         d_rechecked_, d_keys0_, d_keys1_, d_vals1_, d_sort_tmp_, d_stats_, d_qlist_, d_qcount_, d_hist_, d_cert_d1_,
-        d_cert_l2_, d_cert_it_, d_margin_, d_sqlist_, d_state_, d_trim_cand_, d_trim_ctr_, d_scales_, d_trim_hist_;
+        d_cert_l2_, d_cert_it_, d_margin_, d_sqlist_, d_state_, d_trim_cand_, d_trim_ctr_, d_scales_, d_trim_hist_,
+        d_lrf_fb_, d_lrf_fbn_;  // k_lrf8 -> exact k_lrf hand-over list and its count
     TreeBufs t3_, t12_;
     // pinned host mirrors
     PairDev* h_pairs_ = nullptr;

@@ -19,6 +19,7 @@
 #include <climits>
 
 #include "devmath.hpp"
+#include "knn_util.hpp"
 #include "tree.hpp"
 #include "view.hpp"
 #include "wave.hpp"
@@ -26,6 +27,8 @@
 namespace se3icp {
 
 namespace {
+
+using namespace knn;
 
 constexpr int kWaves = 4;
 constexpr int kBuf = 256;
@@ -39,69 +42,6 @@ constexpr int kQ = 8;  // queries per wave (consecutive tree positions)
 #define PROF_NOW(t) do {} while (0)
 #define PROF_ADD(acc, a, b) do {} while (0)
 #endif
-
-__device__ __forceinline__ double l2_3(double ax, double ay, double az, double bx, double by, double bz) {
-#pragma clang fp contract(off)
-    const double d0 = ax - bx, d1 = ay - by, d2 = az - bz;
-    return (d0 * d0 + d1 * d1) + d2 * d2;
-}
-
-// (d, idx) lexicographic order.  Written with bitwise operators: a short-circuit || / &&
-// on per-lane values becomes divergent control flow (exec-mask branches) on the SIMD.
-__device__ __forceinline__ bool key_less(double da, int ia, double db, int ib) {
-    return (bool)((int)(da < db) | ((int)(da == db) & (int)(ia < ib)));
-}
-__device__ __forceinline__ bool key_le(double da, int ia, double db, int ib) {
-    return (bool)((int)(da < db) | ((int)(da == db) & (int)(ia <= ib)));
-}
-
-#ifndef SE3ICP_LRF_ORDER
-#define SE3ICP_LRF_ORDER 2
-#endif
-#ifndef SE3ICP_LRF_TIGHT
-#define SE3ICP_LRF_TIGHT 0
-#endif
-#ifndef SE3ICP_LRF_XCD
-#define SE3ICP_LRF_XCD 1
-#endif
-#ifndef SE3ICP_LRF_FASTSORT
-#define SE3ICP_LRF_FASTSORT 1
-#endif
-
-// Set bits of a wave-uniform 64-bit mask in outward order from position p (p may lie
-// outside [0, 64)): p, p+1, p-1, p+2, p-2, ... (ORDER 2), or ascending (ORDER 0).
-// Neighbouring leaves in tree order are neighbours in space, so the bound tightens early.
-struct OutwardBits {
-    unsigned long long up, dn;
-    bool flip = false;
-    __device__ OutwardBits(unsigned long long m, int p) {
-#if SE3ICP_LRF_ORDER == 2
-        if (p < 0) { up = m; dn = 0ull; }
-        else if (p >= 64) { up = 0ull; dn = m; }
-        else { dn = m & ((1ull << p) - 1ull); up = m & ~((1ull << p) - 1ull); }
-#else
-        (void)p;
-        up = m;
-        dn = 0ull;
-#endif
-    }
-    __device__ int next() {
-        const bool use_up = up != 0ull && (dn == 0ull || !flip);
-        flip = !flip;
-        if (use_up) { const int t = __builtin_ctzll(up); up &= up - 1ull; return t; }
-        if (dn != 0ull) { const int t = 63 - __builtin_clzll(dn); dn &= ~(1ull << t); return t; }
-        return -1;
-    }
-};
-
-__device__ __forceinline__ double wsum(double x) { return wave_sum(x); }
-
-// bits of the f32 value >= d (d >= 0): the f32 keys preserve <= of the f64 distances
-__device__ __forceinline__ unsigned f32_up_bits(double d) {
-    float f = (float)d;
-    if ((double)f < d) f = __uint_as_float(__float_as_uint(f) + 1u);
-    return __float_as_uint(f);
-}
 
 // Fast path of the final order: one 64-bit key per candidate, (f32 bits of d rounded
 // up) << 32 | idx.  Distinct f32 keys are in the f64 order (f32_up_bits is monotone), so
@@ -224,21 +164,6 @@ __device__ __forceinline__ void wave_bitonic(double* bd, int* bi, int lane, int 
     }
 }
 
-// squared distance from q to a 3-D box (f32; the boxes are inflated to bound the f64 points)
-__device__ __forceinline__ float box_lb3(const float* lo, const float* hi, float qx, float qy, float qz) {
-    const float dx = fmaxf(fmaxf(lo[0] - qx, qx - hi[0]), 0.f);
-    const float dy = fmaxf(fmaxf(lo[1] - qy, qy - hi[1]), 0.f);
-    const float dz = fmaxf(fmaxf(lo[2] - qz, qz - hi[2]), 0.f);
-    return dx * dx + dy * dy + dz * dz;
-}
-
-// Per-query state parked in LDS between the kNN pass and the batched eigen-solves
-// (slots of s_park[wave][query]).
-// PK_SUM: the 21 neighbour sums of a query (see the sums pass), later its 6 TOLDI axis sums.
-// PK_ZN: the TOLDI z axis (smallest-eigenvalue eigenvector) from the batched solve.
-enum ParkSlot { PK_SUM = 0, PK_R = 21, PK_KK = 22, PK_GP = 23, PK_FLAGS = 24, PK_K = 25, PK_NTOP = 26, PK_ZN = 27, PK_N = 30 };
-constexpr int kSums = 21;
-
 // The per-cloud records and node boxes are also passed as restrict-qualified arguments:
 // with no possible aliasing store the compiler can serve their wave-uniform reads from
 // the scalar cache (s_load) instead of vector loads.
@@ -248,7 +173,8 @@ constexpr int kSums = 21;
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_WPE))) void k_lrf(View v, int write_knn, const int32_t* __restrict__ cloud_of,
                                              const CloudSetup* __restrict__ setup,
                                              const CloudDev* __restrict__ clouds, const float* __restrict__ tlo,
-                                             const float* __restrict__ thi) {
+                                             const float* __restrict__ thi, const int32_t* __restrict__ qlist,
+                                             const int32_t* __restrict__ qcount) {
     __shared__ double s_d[kWaves][kBuf];
     __shared__ int s_i[kWaves][kBuf];
     // the queries' sorted neighbour lists: dynamic LDS, kQ x v.kmax ints per wave, sized to
@@ -267,8 +193,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
 #else
     const int bid = blockIdx.x;
 #endif
-    const int w0 = __builtin_amdgcn_readfirstlane((bid * kWaves + wid) * kQ);
-    if (bid * kWaves * kQ >= v.npts) return;  // (block-uniform: the block synchronises later)
+    // queries: tree slots 0 .. npts-1, or (list mode, the queries k_lrf8 hands over) the
+    // slots qlist[0 .. *qcount-1], the grid striding over them
+    const int nvq = qlist ? *qcount : v.npts;
+    auto qslot = [&](int i) __attribute__((always_inline)) { return qlist ? qlist[i] : i; };
+    for (int vb = bid; vb * kWaves * kQ < nvq; vb += (int)gridDim.x) {
+    const int w0 = __builtin_amdgcn_readfirstlane((vb * kWaves + wid) * kQ);
     const TreeRef T = v.t3;
     double* bd = s_d[wid];
     int* bi = s_i[wid];
@@ -293,8 +223,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
 #endif
 
     for (int j = 0; j < kQ; ++j) {
-        const int w = w0 + j;
-        if (w >= v.npts) break;
+        if (w0 + j >= nvq) break;
+        const int w = qslot(w0 + j);
         const int c = cloud_of[w];
         const CloudSetup st = setup[c];
         const int K = st.k_knn;
@@ -562,7 +492,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
 #pragma unroll
         for (int i = 0; i < kSums; ++i) x[i] = 0.0;
         if (flags & 3) {
-            const int w = w0 + qj;
+            const int w = qslot(w0 + qj);
             const int c = cloud_of[w];
             const double* X = TX;  // the lists hold tree slots: tree-ordered coordinates
             const double* Y = TY;
@@ -625,9 +555,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
     }
 
     // ---------------------------------------------------------------- batched eigen-solves
-    // Wave 0 solves the 3x3 problems of the block's kWaves * kQ = 32 queries, lane
-    // wq * kQ + j for query j of wave wq: one solve per 32 queries instead of one per
-    // kQ queries on each wave (the other waves' SIMD slots go to other blocks meanwhile).
+    // The 3x3 problems of the block's kWaves * kQ = 32 queries, lane wq * kQ + j for query
+    // j of wave wq: wave 0 the TOLDI ones, wave 1 the normals at the same time (one solve
+    // per 32 queries instead of one per kQ queries on each wave).
     __builtin_amdgcn_wave_barrier();
     if (write_knn) {  // se3icp_knn_self: the sorted lists
         for (int j = 0; j < kQ; ++j) {
@@ -642,13 +572,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
         }
     }
     __syncthreads();
-    if (wid == 0) {
+    if (wid <= 1) {  // wave 0: the TOLDI problems, wave 1 the normals, side by side
         static_assert(kWaves * kQ <= 64, "one lane per query of the block");
         double* pb = &s_park[lane < kWaves * kQ ? lane / kQ : 0][lane % kQ][0];
         const int b_flags = lane < kWaves * kQ ? (int)pb[PK_FLAGS] : 0;
-        const int wb = bid * kWaves * kQ + lane;  // the query's tree slot
+        const int wb = b_flags ? qslot(vb * kWaves * kQ + lane) : 0;  // the query's tree slot
         d3 zn{0, 0, 0};
-        if (b_flags & 1) {
+        if ((b_flags & 1) && wid == 0) {
             // C = sum over ranks 1..rz of (v - cl)(v - cl)^T with the quirk centroid
             // cl = c - q = (S' - q) / rz  (c = (ranks 1..rz-1 summed) / rz, ISR.cpp:259-265)
             const double rz = (double)((int)pb[PK_KK] / 3);
@@ -667,7 +597,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
                 c6[k] = M[k] - S[ia[k]] * cl[ib[k]] - cl[ia[k]] * S[ib[k]] + rz * cl[ia[k]] * cl[ib[k]];
             zn = jacobi_smallest_evec(c6[0], c6[1], c6[2], c6[3], c6[4], c6[5]);
         }
-        if (b_flags & 2) {
+        if ((b_flags & 2) && wid == 1) {
             const int c = v.cloud_of[wb];
             const int kn = min(v.setup[c].k_nrm, (int)pb[PK_NTOP]);
             double n6[6] = {1, 0, 0, 1, 0, 1};
@@ -695,7 +625,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
                 for (int r = 0; r < 6; ++r) v.cov64[(size_t)r * v.ld + gp] = cv[r];
             }
         }
-        if (b_flags & 1) {
+        if ((b_flags & 1) && wid == 0) {
             pb[PK_ZN] = zn.x;
             pb[PK_ZN + 1] = zn.y;
             pb[PK_ZN + 2] = zn.z;
@@ -711,7 +641,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
         const double nx = pj[PK_ZN], ny = pj[PK_ZN + 1], nz = pj[PK_ZN + 2];
         double x6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         if (flags & 1) {
-            const int w = w0 + qj;
+            const int w = qslot(w0 + qj);
             const double* X = TX;  // (tree slots, see the sums pass)
             const double* Y = TY;
             const double* Z = TZ;
@@ -747,7 +677,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
         const double* pb = &s_park[lane < kWaves * kQ ? lane / kQ : 0][lane % kQ][0];
         const int b_flags = lane < kWaves * kQ ? (int)pb[PK_FLAGS] : 0;
         if (b_flags & 1) {
-            const int w = bid * kWaves * kQ + lane;
+            const int w = qslot(vb * kWaves * kQ + lane);
             const CloudSetup st = v.setup[v.cloud_of[w]];
             const double qx = TX[w], qy = TY[w], qz = TZ[w];
             d3 nrm{pb[PK_ZN], pb[PK_ZN + 1], pb[PK_ZN + 2]};
@@ -782,6 +712,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
         atomicAdd(ctr + 11, c_fin);
     }
 #endif
+    if (!qlist) break;  // (one round per block over the whole point range)
+    __syncthreads();    // (the next round reuses the LDS lists and park)
+    }
 }
 
 }  // namespace
@@ -790,7 +723,14 @@ void launch_lrf(const View& v, int write_knn, hipStream_t s) {
     const int nw = (v.npts + kQ - 1) / kQ;
     const size_t lds = sizeof(int) * (size_t)kWaves * kQ * v.kmax;
     hipLaunchKernelGGL(k_lrf, dim3((nw + kWaves - 1) / kWaves), dim3(64 * kWaves), lds, s, v, write_knn, v.cloud_of,
-                       v.setup, v.clouds, v.t3.lo, v.t3.hi);
+                       v.setup, v.clouds, v.t3.lo, v.t3.hi, nullptr, nullptr);
+}
+
+void launch_lrf_list(const View& v, const int32_t* qlist, const int32_t* qcount, hipStream_t s) {
+    const size_t lds = sizeof(int) * (size_t)kWaves * kQ * v.kmax;
+    const int nblk = std::max(1, std::min(1024, (v.npts + kWaves * kQ - 1) / (kWaves * kQ)));
+    hipLaunchKernelGGL(k_lrf, dim3(nblk), dim3(64 * kWaves), lds, s, v, 0, v.cloud_of, v.setup, v.clouds, v.t3.lo,
+                       v.t3.hi, qlist, qcount);
 }
 
 }  // namespace se3icp

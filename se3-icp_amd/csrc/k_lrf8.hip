@@ -1,0 +1,886 @@
+// k_lrf8.hip — the setup's per-point local geometry, eight queries per wavefront:
+//   exact kNN-k of every point in its own cloud (KDTreeFlann::SearchKNN, ISR.cpp:253),
+//   the TOLDI frame -> alpha/beta-weighted SE(3) 12-vector (ISR.cpp:241-316, 597-607),
+//   Open3D EstimateNormals (ISR.cpp:643, :43) and the GICP covariance (ISR.cpp:33-52).
+//
+// A wavefront takes 8 consecutive points of the 3-D kd-tree order (one cloud).  They lie
+// in one or two leaves and share almost all of their neighbourhoods, so the leaves are
+// scanned once for all eight: each lane holds one point of the leaf and computes its
+// distance to the eight queries (f64, nanoflann arithmetic), and every query appends the
+// points within its own bound to its LDS candidate list.  The ordering work that a
+// one-query-per-wave kernel spends 64 lanes on is done by eight lanes per query, for the
+// eight queries at once, with key-only bitonic networks that run mostly inside registers:
+//   * key = f32 bits of the squared distance rounded up (monotone in the f64 distance);
+//     the lists hold it cut to its top 20 bits, packed with a 12-bit candidate id;
+//   * bound: the Kw-th smallest packed key with the id bits set (sort of the candidates of
+//     the first leaves, again whenever a list would overflow), then only candidates at or
+//     below it are kept (a cut key keeps a few extra candidates, never loses one);
+//   * the TOLDI / normal sums are sums over rank SETS (ranks 1..rz-1, 1..rz, 1..kk-1,
+//     0..kn-1; the reference sums them sequentially, the order changes rounding only),
+//     so the final pass needs the keys at the set boundaries, not a sorted list: a sort
+//     of the full keys (recomputed from the points) gives them, and each candidate is
+//     classified by comparing its key with them.
+// A boundary whose two keys are equal (an f32 tie, or duplicate points at distance 0)
+// cannot be resolved from keys: that query is handed to the exact one-query-per-wave
+// kernel (k_knn.hip k_lrf over a list), as are a cloud's last, partial, wave, clouds with
+// k > kCap - 64, and waves that scan more than kLeaves leaves.  Waves are aligned to the
+// start of each cloud, so a point's result does not depend on the batch around its cloud.  Every other query gets exactly the
+// reference's neighbour sets (ties by lowest index never arise: its boundaries are strict).
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <climits>
+
+#include "devmath.hpp"
+#include "knn_util.hpp"
+#include "tree.hpp"
+#include "view.hpp"
+#include "wave.hpp"
+
+namespace se3icp {
+
+namespace {
+
+using namespace knn;
+
+constexpr int kW = 4;          // waves per block
+constexpr int kQ = 8;          // queries per wave (eight lanes each in the group phases)
+constexpr int kCap = 192;      // candidates buffered per query (u32: cut key | candidate id)
+constexpr int kLeaves = 64;    // leaves one wave may scan: candidate id = (list index << 6) | lane
+constexpr unsigned kIdBits = 0xfffu;     // low bits of a list entry: the candidate id
+constexpr unsigned kAll = 0xfffffffeu;   // bound of the accept-all phase (> every finite key)
+constexpr unsigned kPad = 0xffffffffu;   // sort padding (> every bound)
+
+// park slots per query (doubles)
+enum Park8 {
+    P8_SUM = 0,     // 21 neighbour sums, later the 6 TOLDI axis sums
+    P8_R = 21, P8_KK = 22, P8_GP = 23, P8_FLAGS = 24, P8_K = 25, P8_NTOP = 26, P8_ZN = 27,
+    P8_W = 30,                // the query's tree slot
+    P8_N = 31
+};
+constexpr int kSums8 = 21;
+
+// lane ^ m within a group of eight lanes (m = 1..7 as used by the networks)
+__device__ __forceinline__ unsigned gx(unsigned x, int m) {
+    switch (m) {
+    case 1: return (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    case 2: return (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    case 3: return (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x1B, 0xF, 0xF, false);   // quad_perm [3,2,1,0]
+    case 4: return (unsigned)__builtin_amdgcn_ds_swizzle((int)x, 0x101F);                      // xor 4
+    case 7: return (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    default: return (unsigned)__shfl_xor((int)x, m, 64);
+    }
+}
+__device__ __forceinline__ double gxd(double x, int m) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(x);
+    const unsigned lo = gx((unsigned)u, m), hi = gx((unsigned)(u >> 32), m);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// Ascending bitonic sort of the 8*PER keys of a group of eight lanes (element e =
+// l*PER + s in k[s] of group lane l), every comparator ascending (each merge starts with
+// the "flip" step e <-> e ^ (KK-1)): an in-register compare-exchange is a min and a max.
+// Stages are instantiated at compile time (template recursion) so that every register
+// index is a constant.
+template <int PER, int KK, int JD>
+__device__ __forceinline__ void stage8(unsigned (&k)[PER], int l) {
+    if constexpr (JD == 0) {  // flip
+        if constexpr (KK <= PER) {
+#pragma unroll
+            for (int s = 0; s < PER; ++s) {
+                const int t = s ^ (KK - 1);
+                if (s < t) {
+                    const unsigned a = k[s], b = k[t];
+                    k[s] = min(a, b);
+                    k[t] = max(a, b);
+                }
+            }
+        } else {
+            constexpr int lm = KK / PER - 1;
+            const bool lower = (l & (KK / PER / 2)) == 0;
+#pragma unroll
+            for (int s = 0; s < PER / 2; ++s) {
+                const int t = PER - 1 - s;
+                const unsigned a = gx(k[t], lm), b = gx(k[s], lm);
+                k[s] = lower ? min(k[s], a) : max(k[s], a);
+                k[t] = lower ? min(k[t], b) : max(k[t], b);
+            }
+        }
+    } else if constexpr (JD < PER) {
+#pragma unroll
+        for (int s = 0; s < PER; ++s) {
+            if ((s & JD) == 0) {
+                const int t = s | JD;
+                const unsigned a = k[s], b = k[t];
+                k[s] = min(a, b);
+                k[t] = max(a, b);
+            }
+        }
+    } else {
+        constexpr int lm = JD / PER;
+        const bool lower = (l & lm) == 0;
+#pragma unroll
+        for (int s = 0; s < PER; ++s) {
+            const unsigned p = gx(k[s], lm);
+            k[s] = lower ? min(k[s], p) : max(k[s], p);
+        }
+    }
+}
+template <int PER, int N, int KK = 2, int JD = 0>
+__device__ __forceinline__ void net8(unsigned (&k)[PER], int l) {
+    stage8<PER, KK, JD>(k, l);
+    constexpr int next_jd = JD == 0 ? KK / 4 : JD / 2;
+    if constexpr (next_jd > 0) net8<PER, N, KK, next_jd>(k, l);
+    else if constexpr (KK < N) net8<PER, N, KK * 2, 0>(k, l);
+}
+template <int PER>
+__device__ __forceinline__ void sort8(unsigned (&k)[PER], int l) {
+    net8<PER, 8 * PER>(k, l);
+}
+
+// key of rank r (group-uniform, 0 <= r) of a sorted group; kPad beyond the network
+template <int PER>
+__device__ __forceinline__ unsigned rank_key(const unsigned (&k)[PER], int l, int r) {
+    r = __builtin_amdgcn_readfirstlane(r);  // wave-uniform: one indexed register move (v_movrels)
+    if (r >= 8 * PER) return kPad;
+    unsigned x = k[r % PER];
+    x = (l == r / PER) ? x : 0u;
+    x |= gx(x, 1);
+    x |= gx(x, 2);
+    x |= gx(x, 4);
+    return x;
+}
+
+// Bound tightening of the group's query (eight lanes per query, all groups at once):
+// sort its list entries, bound = the Kw-th smallest cut key with every id bit set, keep the
+// entries at or below it in place (entries of equal cut key stay together: never fewer
+// than Kw).  Returns (bound, kept) for the group.
+template <int PER>
+__device__ __forceinline__ unsigned list_kth(const unsigned* list, int nbg, int l, int r) {
+    unsigned k[PER];
+#pragma unroll
+    for (int s = 0; s < PER; ++s) {
+        const int e = l * PER + s;
+        k[s] = e < nbg ? list[e] : kPad;
+    }
+    sort8<PER>(k, l);
+    return rank_key(k, l, r);
+}
+// sort the run list[0 .. len) (len <= 128) in place
+__device__ __forceinline__ void sort_run(unsigned* list, int len, int l) {
+    unsigned k[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        const int e = l * 16 + s;
+        k[s] = e < len ? list[e] : kPad;
+    }
+    sort8<16>(k, l);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        const int e = l * 16 + s;
+        if (e < len) list[e] = k[s];
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+// entry of rank r of the union of two sorted runs A (na) and B (nb) (distinct entries):
+// i entries of A and r+1-i of B are the r+1 smallest; binary search on i
+__device__ __forceinline__ unsigned kth_of_two(const unsigned* A, int na, const unsigned* B, int nb, int r) {
+    int lo = max(0, r + 1 - nb), hi = min(r + 1, na);
+    while (lo < hi) {
+        const int i = (lo + hi) >> 1;
+        if (A[i] < B[r - i]) lo = i + 1; else hi = i;
+    }
+    const int j = r + 1 - lo;
+    return max(lo > 0 ? A[lo - 1] : 0u, j > 0 ? B[j - 1] : 0u);
+}
+__device__ __forceinline__ uint2 tighten_group(unsigned* lists, int g, int l, int nbg, int nmax, int Kw) {
+    unsigned* list = lists + g * kCap;
+    unsigned tg;
+    if (nmax <= 128) {
+        tg = list_kth<16>(list, nbg, l, Kw - 1);
+    } else {  // two sorted runs of <= 128 (a 256-entry network would need the kernel's registers)
+        const int na = min(nbg, 128), nb = max(nbg - 128, 0);
+        sort_run(list, na, l);
+        sort_run(list + 128, nb, l);
+        tg = kth_of_two(list, na, list + 128, nb, Kw - 1);
+    }
+    tg |= kIdBits;
+    // compaction in place (reads of a round precede its writes, positions only move down)
+    unsigned keep_n = 0;
+    for (int r0 = 0; r0 < nmax; r0 += 8) {
+        const int e = r0 + l;
+        const unsigned ent = e < nbg ? list[e] : kPad;
+        const bool keep = ent <= tg;
+        const unsigned long long m = __ballot(keep);
+        const unsigned gm = (unsigned)(m >> (8 * g)) & 0xffu;
+        __builtin_amdgcn_wave_barrier();
+        if (keep) list[(int)keep_n + __popc(gm & ((1u << l) - 1u))] = ent;
+        keep_n += (unsigned)__popc(gm);
+        __builtin_amdgcn_wave_barrier();
+    }
+    return make_uint2(tg, keep_n);
+}
+
+// point of a list entry: the wave's leaf list holds leaf indices, the id (list index << 6 |
+// lane) picks the point
+__device__ __forceinline__ int entry_slot(unsigned ent, const int* leaves, int off, int n, int L) {
+    const unsigned id = ent & kIdBits;
+    return off + tree_first(n, L, leaves[id >> 6]) + (int)(id & 63u);
+}
+
+// 64-bit version of the group network (keys (full key << 32) | point index: the order of
+// the final lists, canonical — independent of the tree and of the batch around the cloud)
+__device__ __forceinline__ unsigned long long gx64(unsigned long long x, int m) {
+    const unsigned lo = gx((unsigned)x, m), hi = gx((unsigned)(x >> 32), m);
+    return ((unsigned long long)hi << 32) | lo;
+}
+template <int PER, int KK, int JD>
+__device__ __forceinline__ void stage8_64(unsigned long long (&k)[PER], int l) {
+    if constexpr (JD == 0) {
+        if constexpr (KK <= PER) {
+#pragma unroll
+            for (int s = 0; s < PER; ++s) {
+                const int t = s ^ (KK - 1);
+                if (s < t) {
+                    const unsigned long long a = k[s], b = k[t];
+                    const bool sw = b < a;
+                    k[s] = sw ? b : a;
+                    k[t] = sw ? a : b;
+                }
+            }
+        } else {
+            constexpr int lm = KK / PER - 1;
+            const bool lower = (l & (KK / PER / 2)) == 0;
+#pragma unroll
+            for (int s = 0; s < PER / 2; ++s) {
+                const int t = PER - 1 - s;
+                const unsigned long long a = gx64(k[t], lm), b = gx64(k[s], lm);
+                k[s] = ((a < k[s]) == lower) ? a : k[s];
+                k[t] = ((b < k[t]) == lower) ? b : k[t];
+            }
+        }
+    } else if constexpr (JD < PER) {
+#pragma unroll
+        for (int s = 0; s < PER; ++s) {
+            if ((s & JD) == 0) {
+                const int t = s | JD;
+                const unsigned long long a = k[s], b = k[t];
+                const bool sw = b < a;
+                k[s] = sw ? b : a;
+                k[t] = sw ? a : b;
+            }
+        }
+    } else {
+        constexpr int lm = JD / PER;
+        const bool lower = (l & lm) == 0;
+#pragma unroll
+        for (int s = 0; s < PER; ++s) {
+            const unsigned long long p = gx64(k[s], lm);
+            k[s] = ((p < k[s]) == lower) ? p : k[s];
+        }
+    }
+}
+template <int PER, int N, int KK = 2, int JD = 0>
+__device__ __forceinline__ void net8_64(unsigned long long (&k)[PER], int l) {
+    stage8_64<PER, KK, JD>(k, l);
+    constexpr int next_jd = JD == 0 ? KK / 4 : JD / 2;
+    if constexpr (next_jd > 0) net8_64<PER, N, KK, next_jd>(k, l);
+    else if constexpr (KK < N) net8_64<PER, N, KK * 2, 0>(k, l);
+}
+// key part of the entry of rank r (wave-uniform) of a sorted group; kPad beyond it
+__device__ __forceinline__ unsigned rank_key64(const unsigned long long (&k)[16], int l, int r) {
+    r = __builtin_amdgcn_readfirstlane(r);
+    if (r >= 128) return kPad;
+    unsigned x = (unsigned)(k[r % 16] >> 32);
+    x = (l == r / 16) ? x : 0u;
+    x |= gx(x, 1);
+    x |= gx(x, 2);
+    x |= gx(x, 4);
+    return x;
+}
+
+// The final list of the group's query (nbg <= 128 entries): full keys recomputed from the
+// points (nanoflann arithmetic), sorted with the point index as tie-break, the rank-ordered
+// tree slots written back over the list; returns false when two of the ranks the sums use
+// share an f32 key (the query then goes to the exact kernel).
+__device__ __forceinline__ bool final_group(unsigned* lists, const int* leaves, const double* __restrict__ TX,
+                                            const double* __restrict__ TY, const double* __restrict__ TZ,
+                                            const int32_t* __restrict__ perm, const int32_t* __restrict__ pos,
+                                            double qx, double qy, double qz, int off, int n, int L, int g, int l,
+                                            int nbg, int kk, int kn, bool want_t, bool want_n) {
+    unsigned* list = lists + g * kCap;
+    unsigned long long k[16];
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        const int e = l * 16 + s;
+        unsigned long long x = ~0ull;
+        if (e < nbg) {
+            const int slot = entry_slot(list[e], leaves, off, n, L);
+            const unsigned key = f32_up_bits(l2_3(qx, qy, qz, TX[slot], TY[slot], TZ[slot]));
+            x = ((unsigned long long)key << 32) | (unsigned)perm[slot];
+        }
+        k[s] = x;
+    }
+    net8_64<16, 128>(k, l);
+    // No two of the first lim = min(nbg, max(kk, kn) + 1) ranks may share an f32 key: then
+    // the (key, index) order is the exact (f64 d, index) order of the reference's kNN and of
+    // the exact kernel, whose sums this kernel then reproduces bit for bit.
+    const int lim = min(nbg, max(kk, kn) + 1);
+    bool tie = false;
+#pragma unroll
+    for (int s = 0; s + 1 < 16; ++s) {
+        const int e = l * 16 + s;
+        tie |= (bool)((int)(e + 1 < lim) & (int)((unsigned)(k[s] >> 32) == (unsigned)(k[s + 1] >> 32)));
+    }
+    {
+        // the next lane's first key (lane l + 1 of the group)
+        const unsigned first_next = __shfl((unsigned)(k[0] >> 32), (int)(threadIdx.x & 63) + 1, 64);
+        const int e = l * 16 + 15;
+        tie |= (bool)((int)(l < 7) & (int)(e + 1 < lim) & (int)((unsigned)(k[15] >> 32) == first_next));
+    }
+    const bool ok = !(bool)(unsigned)((__ballot(tie) >> (8 * g)) & 0xffull);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        const int e = l * 16 + s;
+        if (e < nbg) list[e] = (unsigned)(off + pos[off + (int)(unsigned)k[s]]);
+    }
+    __builtin_amdgcn_wave_barrier();
+    return ok;
+}
+
+// SE3ICP_PROF builds (make prof): per-section shader-clock cycles into stats columns 8..11
+#ifdef SE3ICP_PROF
+#define PROF8_NOW(t) const unsigned long long t = __builtin_readcyclecounter()
+#define PROF8_ADD(acc, a, b) acc += (b) - (a)
+#else
+#define PROF8_NOW(t) do {} while (0)
+#define PROF8_ADD(acc, a, b) do {} while (0)
+#endif
+
+#ifndef SE3ICP_LRF8_WPE
+#define SE3ICP_LRF8_WPE 4
+#endif
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF8_WPE))) void k_lrf8(
+    View v, const int32_t* __restrict__ cloud_of, const CloudSetup* __restrict__ setup,
+    const CloudDev* __restrict__ clouds, const float* __restrict__ tlo, const float* __restrict__ thi,
+    const double* __restrict__ tx64, const int32_t* __restrict__ wave_base, int nwaves,
+    int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_count) {
+    __shared__ unsigned s_list[kW][kQ][kCap];
+    __shared__ int s_leaf[kW][kLeaves];
+    __shared__ double s_park[kW][kQ][P8_N];
+    __shared__ double s_q[kW][kQ][4];  // the queries' f64 coordinates (read back per leaf: no registers held)
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int g = lane >> 3, l = lane & 7;  // query of the lane's group, lane within the group
+    const int bid = xcd_block(blockIdx.x, gridDim.x);
+    const TreeRef T = v.t3;
+    const double* TX = tx64;
+    const double* TY = tx64 + v.ld;
+    const double* TZ = tx64 + 2 * (size_t)v.ld;
+    const int first_leaf = (1 << T.L) - 1;
+    double* park = &s_park[wid][0][0];
+    unsigned* lists = &s_list[wid][0][0];
+    int* leaves = s_leaf[wid];
+    if (lane < kQ) park[lane * P8_N + P8_FLAGS] = 0.0;
+    unsigned n_leaves = 0, n_sel = 0, n_cand = 0, n_q = 0;
+#ifdef SE3ICP_PROF
+    unsigned long long c_scan = 0, c_tight = 0, c_sums = 0, c_epi = 0;
+#endif
+    PROF8_NOW(t_a0);
+
+    // ---------------------------------------------------------------- the wave's queries
+    // Wave wv covers local points 8*(wv - wave_base[c]) .. +7 of cloud c (waves aligned to
+    // each cloud's start).  mode 0: nothing to do (no kNN wanted, past the end); 1: this
+    // kernel; 2: its queries go to the exact kernel (partial wave, k too large for the lists).
+    const int wv = __builtin_amdgcn_readfirstlane(bid * kW + wid);
+    int mode = 0, c = 0, w0 = 0, qn = 0;
+    CloudSetup st{};
+    CloudDev cl{0, 0};
+    int K = 0, Kw = 0;
+    if (wv < nwaves) {
+        int lo = 0, hi = v.nclouds - 1;  // last cloud with wave_base <= wv
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (wave_base[mid] <= wv) lo = mid; else hi = mid - 1;
+        }
+        c = lo;
+        cl = clouds[c];
+        st = setup[c];
+        K = st.k_knn;
+        w0 = cl.off + kQ * (wv - wave_base[c]);
+        qn = min(kQ, cl.off + cl.n - w0);
+        if (K > 0 && qn > 0) {
+            Kw = min(K, cl.n);
+            mode = (qn == kQ && Kw <= kCap - 64) ? 1 : 2;
+        }
+    }
+    bool fb_wave = mode == 2;
+    // per-query state: bound (wave-uniform arrays) and list lengths
+    unsigned Tq[kQ], nbq[kQ];
+#pragma unroll
+    for (int j = 0; j < kQ; ++j) { Tq[j] = kAll; nbq[j] = 0u; }
+    // the list length of the lane's own group g, kept alongside (picking nbq[g] at run time
+    // would turn the register arrays into scratch memory)
+    unsigned nbv = 0u;
+    volatile double* qv = &s_q[wid][0][0];
+    float fqlo[3] = {0.f, 0.f, 0.f}, fqhi[3] = {0.f, 0.f, 0.f};
+    int nlist = 0;
+    const int n = cl.n;
+    if (mode == 1) {
+        if (lane < kQ) {
+            qv[4 * lane] = TX[w0 + lane];
+            qv[4 * lane + 1] = TY[w0 + lane];
+            qv[4 * lane + 2] = TZ[w0 + lane];
+        }
+        __builtin_amdgcn_wave_barrier();
+        // f32 box of the eight queries (the node boxes' frame)
+        const float fx = lane < kQ ? T.tvec[w0 + lane] : 0.f;
+        const float fy = lane < kQ ? T.tvec[v.ld + w0 + lane] : 0.f;
+        const float fz = lane < kQ ? T.tvec[2 * (size_t)v.ld + w0 + lane] : 0.f;
+        fqlo[0] = fqhi[0] = __shfl(fx, 0, 64);
+        fqlo[1] = fqhi[1] = __shfl(fy, 0, 64);
+        fqlo[2] = fqhi[2] = __shfl(fz, 0, 64);
+#pragma unroll
+        for (int j = 1; j < kQ; ++j) {
+            const float a = __shfl(fx, j, 64), b = __shfl(fy, j, 64), d = __shfl(fz, j, 64);
+            fqlo[0] = fminf(fqlo[0], a); fqhi[0] = fmaxf(fqhi[0], a);
+            fqlo[1] = fminf(fqlo[1], b); fqhi[1] = fmaxf(fqhi[1], b);
+            fqlo[2] = fminf(fqlo[2], d); fqhi[2] = fmaxf(fqhi[2], d);
+        }
+        n_q = kQ;
+    }
+
+    // ---------------------------------------------------------------- bound tightening
+    auto tighten = [&]() __attribute__((always_inline)) {
+        ++n_sel;
+        unsigned nmax = 0;
+#pragma unroll
+        for (int j = 0; j < kQ; ++j) nmax = max(nmax, nbq[j]);
+        __builtin_amdgcn_wave_barrier();
+        const uint2 r = tighten_group(lists, g, l, (int)nbv, (int)nmax, Kw);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int j = 0; j < kQ; ++j) {
+            Tq[j] = (unsigned)__builtin_amdgcn_readlane((int)r.x, 8 * j);
+            nbq[j] = (unsigned)__builtin_amdgcn_readlane((int)r.y, 8 * j);
+        }
+        nbv = r.y;
+    };
+
+    // ---------------------------------------------------------------- leaf scan
+    // Each lane holds one point of leaf i; query j appends it when its entry (cut key |
+    // id) <= Tq[j].  part: 0 the whole leaf, 1 / 2 its first / second 32 points (a leaf that
+    // does not fit a list even after a tightening is appended in two halves).
+    auto scan_leaf = [&](int i, int part) __attribute__((always_inline)) -> bool {
+        if (nlist >= kLeaves) { fb_wave = true; return true; }
+        const int li = nlist++;
+        ++n_leaves;
+        if (lane == 0) leaves[li] = i;
+        const int a = __builtin_amdgcn_readfirstlane(tree_first(n, T.L, i));
+        const int b = __builtin_amdgcn_readfirstlane(tree_first(n, T.L, i + 1));
+        const bool valid = (bool)((int)(lane < b - a) & (int)(part == 0 || (part == 1) == (lane < 32)));
+        const int slot = cl.off + a + (valid ? lane : 0);
+        const double px = TX[slot], py = TY[slot], pz = TZ[slot];
+        const unsigned id = (unsigned)((li << 6) | lane);
+        // the list key: the f32 bits of the rounded-to-nearest distance plus one ulp (>= the
+        // distance: an upper bound, all that the bounds need; the final order uses exact keys)
+        unsigned ent[kQ];
+        unsigned long long m[kQ];
+        bool over = false;
+#pragma unroll
+        for (int j = 0; j < kQ; ++j) {
+            const double d = l2_3(qv[4 * j], qv[4 * j + 1], qv[4 * j + 2], px, py, pz);
+            ent[j] = valid ? (((__float_as_uint((float)d) + 1u) & ~kIdBits) | id) : kPad;
+            m[j] = __ballot(ent[j] <= Tq[j]);
+            over |= nbq[j] + (unsigned)__popcll(m[j]) > (unsigned)kCap;
+        }
+        if (over) {  // a list would overflow: the caller tightens the bounds and rescans the leaf
+            --nlist;
+            --n_leaves;
+            return false;
+        }
+#pragma unroll
+        for (int j = 0; j < kQ; ++j) {
+            if ((m[j] >> lane) & 1ull) {
+                const int at = (int)nbq[j] + __builtin_amdgcn_mbcnt_hi((unsigned)(m[j] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m[j], 0u));
+                lists[j * kCap + at] = ent[j];
+            }
+            const unsigned cnt = (unsigned)__popcll(m[j]);
+            nbq[j] += cnt;
+            nbv += (g == j) ? cnt : 0u;
+        }
+        __builtin_amdgcn_wave_barrier();
+        return true;
+    };
+
+    if (mode == 1) {
+        // The leaves holding the eight queries, then their tree-order neighbours, every
+        // point accepted, until each query has Kw candidates: the first bound.
+        const int lf0 = tree_node_of(w0 - cl.off, n, T.L), lf1 = tree_node_of(w0 + kQ - 1 - cl.off, n, T.L);
+        const int nleaf = 1 << T.L;
+        int s_lo = lf0, s_hi = lf1;
+        // Then every leaf whose box may hold a point within the largest bound of the
+        // eight (squared box-to-box distance from the queries' f32 box, f32 boxes inflated
+        // to bound the f64 points): level-A nodes 64 per instruction, then the leaves of
+        // each open one, scanned outward from the queries and re-tested as bounds shrink.
+        auto thr_f = [&]() __attribute__((always_inline)) {
+            unsigned tm = 0u;
+#pragma unroll
+            for (int j = 0; j < kQ; ++j) tm = max(tm, Tq[j]);
+            return __uint_as_float(f32_up_bits((double)__uint_as_float(tm) * (1.0 + 2e-6)));
+        };
+        auto box_lb = [&](int h) __attribute__((always_inline)) {
+            const float* lo = tlo + ((size_t)c * T.nnodes + h) * 3;
+            const float* hi = thi + ((size_t)c * T.nnodes + h) * 3;
+            float s = 0.f;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const float e = fmaxf(fmaxf(lo[a] - fqhi[a], fqlo[a] - hi[a]), 0.f);
+                s += e * e;
+            }
+            return s;
+        };
+        const int sh = T.L > 6 ? 6 : T.L;
+        const int nA = 1 << (T.L - sh), firstA = nA - 1;
+        // one loop, one scan site: stage 0 the queries' own leaves, 1 their tree-order
+        // neighbours until Kw candidates exist (accept-all), 2 level-A nodes, 3 the leaves
+        // of the current level-A node
+        // A leaf that does not fit a list: tighten and retry; then its two halves (each
+        // after a tightening if needed); still no room (massive ties at the bound): the
+        // exact kernel.  One tightening site keeps the kernel's code and registers small.
+        int stage = 0, nxt = lf0, c0 = 0, l0 = 0;
+        bool up = true, haveA = false;
+        float lbA = INFINITY, lbL = INFINITY;
+        OutwardBits itA(0ull, 0), itL(0ull, 0);
+        int cur = -1, part = 0;
+        bool do_tighten = false, retried = false;
+        while (!fb_wave) {
+            if (do_tighten) {
+                PROF8_NOW(t_t0);
+                tighten();
+                PROF8_NOW(t_t1);
+                PROF8_ADD(c_tight, t_t0, t_t1);
+                do_tighten = false;
+            }
+            if (cur >= 0) {  // appending leaf cur (part)
+                if (scan_leaf(cur, part)) {
+                    if (part == 1) part = 2;
+                    else { cur = -1; part = 0; }
+                    retried = false;
+                } else if (!retried && (int)nbq[0] >= Kw) {
+                    do_tighten = true;
+                    retried = true;
+                } else if (part == 0) {
+                    part = 1;
+                    retried = false;
+                } else {
+                    fb_wave = true;
+                }
+                continue;
+            }
+            int leaf = -1;
+            if (stage == 0) {
+                leaf = nxt++;
+                if (nxt > lf1) stage = 1;
+            } else if (stage == 1) {
+                // (filling the lists beyond Kw while a whole leaf still fits: the first
+                // bound, the Kw-th of more nearby points, is tighter)
+                const bool more_hi = s_hi < nleaf - 1, more_lo = s_lo > 0;
+                const int cand = (more_hi && (up || !more_lo)) ? s_hi + 1 : s_lo - 1;
+                const int csz = (more_hi || more_lo) ? tree_first(n, T.L, cand + 1) - tree_first(n, T.L, cand) : 0;
+                if ((more_hi || more_lo) && ((int)nbq[0] < Kw || (int)nbq[0] + csz <= kCap)) {
+                    leaf = cand;
+                    if (cand > s_hi) s_hi = cand; else s_lo = cand;
+                    up = !up;
+                } else {
+                    do_tighten = true;
+                    stage = 2;
+                    continue;
+                }
+            } else if (stage == 2) {
+                if (!haveA) {
+                    if (c0 >= nA) {  // done; the final sort takes lists of <= 128: tighten once more
+                        unsigned nmax = 0;
+#pragma unroll
+                        for (int j = 0; j < kQ; ++j) nmax = max(nmax, nbq[j]);
+                        if (nmax > 128 && !retried) { do_tighten = true; retried = true; continue; }
+                        if (nmax > 128) fb_wave = true;  // (ties at the bound)
+                        break;
+                    }
+                    const int ai = c0 + lane;
+                    lbA = ai < nA ? box_lb(firstA + ai) : INFINITY;
+                    itA = OutwardBits(__ballot(lbA <= thr_f()), (lf0 >> sh) - c0);
+                    haveA = true;
+                }
+                const int j = itA.next();
+                if (j < 0) { haveA = false; c0 += 64; continue; }
+                if (!(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbA), j)) <= thr_f())) continue;
+                l0 = (c0 + j) << sh;
+                const int li = l0 + lane;
+                lbL = INFINITY;
+                if ((int)(lane < (1 << sh)) & ((int)(li < s_lo) | (int)(li > s_hi))) lbL = box_lb(first_leaf + li);
+                itL = OutwardBits(__ballot(lbL <= thr_f()), lf0 - l0);
+                stage = 3;
+                continue;
+            } else {
+                const int t = itL.next();
+                if (t < 0) { stage = 2; continue; }
+                if (!(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbL), t)) <= thr_f())) continue;
+                leaf = l0 + t;
+            }
+            cur = leaf;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+
+    PROF8_NOW(t_a1);
+    PROF8_ADD(c_scan, t_a0, t_a1);
+    // ---------------------------------------------------------------- final sets
+    // Each list sorted by full key (ties by point index); every set boundary must be strict
+    // (else the query goes to the exact kernel).
+    const int kl = st.k_lrf, kn_want = st.k_nrm;
+    const bool want_t = kl > 0, want_n = kn_want > 0;
+    bool fb_q = fb_wave;  // (group-uniform)
+    const int nbg = (int)nbv;
+    const int nTop = min(Kw, nbg);
+    const int kk = min(kl, nTop), kn = min(kn_want, nTop);
+    const int wq = w0 + g;
+    if (mode == 1 && !fb_wave) {
+        __builtin_amdgcn_wave_barrier();
+        const bool exact = final_group(lists, leaves, TX, TY, TZ, T.perm, T.pos, qv[4 * g], qv[4 * g + 1],
+                                       qv[4 * g + 2], cl.off, n, T.L, g, l, nbg, kk, kn, want_t, want_n);
+        fb_q = (bool)((int)!exact | (int)(nTop < Kw));
+        n_cand += (unsigned)nbg;
+    }
+    // queries for the exact kernel
+    if ((int)(mode != 0) & (int)fb_q & (int)(l == 0) & (int)(g < qn)) {
+        const int at = atomicAdd(fb_count, 1);
+        fb_list[at] = wq;
+        atomicAdd(v.stats + kStatCols * (wv & 63) + 6, 1ull);  // (bench diagnostics: hand-overs)
+    }
+    const bool mine = (bool)((int)(mode == 1) & (int)!fb_q);
+
+    // ---------------------------------------------------------------- per-query sums
+    // (group g, list entries l, l+8, ...; each classified by its full key; see k_knn.hip for
+    // the 21 sums and the TOLDI covariance about the quirk centroid, ISR.cpp:259-272)
+    {
+        double x[kSums8];
+#pragma unroll
+        for (int i = 0; i < kSums8; ++i) x[i] = 0.0;
+        double Rf = 0.0;
+        if (mine) {
+            // the same loops, lane assignment and arithmetic as k_knn.hip's sums pass, over
+            // the same rank order: the two kernels' frames agree bit for bit
+            const double qgx = qv[4 * g], qgy = qv[4 * g + 1], qgz = qv[4 * g + 2];
+            const unsigned* rl = lists + g * kCap;
+            if (want_t) {
+                const int rz = kk / 3;
+                const int hi = min(rz, kk - 1);
+                for (int rk = 1 + l; rk <= hi; rk += 8) {
+                    const int q = (int)rl[rk];
+                    const double vx = TX[q] - qgx, vy = TY[q] - qgy, vz = TZ[q] - qgz;
+                    if (rk < rz) { x[0] += vx; x[1] += vy; x[2] += vz; }
+                    x[3] += vx; x[4] += vy; x[5] += vz;
+                    x[6] += vx * vx; x[7] += vx * vy; x[8] += vx * vz;
+                    x[9] += vy * vy; x[10] += vy * vz; x[11] += vz * vz;
+                }
+                if (l == 0) {
+                    const int far = (int)rl[kk - 1];
+                    const double fdx = qgx - TX[far], fdy = qgy - TY[far], fdz = qgz - TZ[far];
+                    Rf = sqrt(fdx * fdx + fdy * fdy + fdz * fdz);  // ISR.cpp:256
+                }
+            }
+            if (want_n) {  // EstimateNormals (ISR.cpp:643, :43): ranks 0 .. kn-1, self included
+                for (int r = l; r < kn; r += 8) {
+                    const int q = (int)rl[r];
+                    const double px = TX[q], py = TY[q], pz = TZ[q];
+                    x[12] += px; x[13] += py; x[14] += pz;
+                    x[15] += px * px; x[16] += px * py; x[17] += px * pz;
+                    x[18] += py * py; x[19] += py * pz; x[20] += pz * pz;
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < kSums8; ++i) {
+            x[i] += gxd(x[i], 1);
+            x[i] += gxd(x[i], 2);
+            x[i] += gxd(x[i], 4);
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (l == 0) {
+            double* pj = park + g * P8_N;
+            const int flags = mine ? ((want_t ? 1 : 0) | (want_n ? 2 : 0)) : 0;
+            pj[P8_FLAGS] = (double)flags;
+            if (mine) {
+#pragma unroll
+                for (int i = 0; i < kSums8; ++i) pj[P8_SUM + i] = x[i];
+                pj[P8_R] = Rf;
+                pj[P8_KK] = (double)kk;
+                pj[P8_GP] = (double)(cl.off + T.perm[wq]);
+                pj[P8_K] = (double)K;
+                pj[P8_NTOP] = (double)nTop;
+                pj[P8_W] = (double)wq;
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    PROF8_NOW(t_a2);
+    PROF8_ADD(c_sums, t_a1, t_a2);
+    unsigned long long* ctr = v.stats + kStatCols * (wv & 63);
+    if (lane == 0) {  // work counters (bench diagnostics): queries, leaf scans, bound sorts, candidates
+        atomicAdd(ctr + 0, (unsigned long long)n_q);
+        atomicAdd(ctr + 1, (unsigned long long)n_leaves);
+        atomicAdd(ctr + 2, (unsigned long long)n_sel);
+        atomicAdd(ctr + 4, (unsigned long long)n_cand);
+    }
+
+    // ---------------------------------------------------------------- eigen-solves
+    // The 3x3 problems of the block's 32 queries, one lane each: wave 0 the TOLDI ones
+    // (cyclic Jacobi), wave 1 the normals (FastEigen3x3) at the same time.
+    __syncthreads();
+    if (wid <= 1) {  // wave 0: the TOLDI problems, wave 1 the normals, side by side
+        double* pb = &s_park[lane < kW * kQ ? lane / kQ : 0][lane % kQ][0];
+        const int b_flags = lane < kW * kQ ? (int)pb[P8_FLAGS] : 0;
+        const int wb = b_flags ? (int)pb[P8_W] : 0;  // the query's tree slot
+        d3 zn{0, 0, 0};
+        if ((b_flags & 1) && wid == 0) {
+            // C about the quirk centroid cl = (S' - q) / rz (ISR.cpp:259-272), see k_knn.hip
+            const double rz = (double)((int)pb[P8_KK] / 3);
+            const double q3[3] = {TX[wb], TY[wb], TZ[wb]};
+            double cq[3], S[3];
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                cq[a] = (pb[P8_SUM + a] - q3[a]) / rz;
+                S[a] = pb[P8_SUM + 3 + a];
+            }
+            const double* M = pb + P8_SUM + 6;
+            const int ia[6] = {0, 0, 0, 1, 1, 2}, ib[6] = {0, 1, 2, 1, 2, 2};
+            double c6[6];
+#pragma unroll
+            for (int k = 0; k < 6; ++k)
+                c6[k] = M[k] - S[ia[k]] * cq[ib[k]] - cq[ia[k]] * S[ib[k]] + rz * cq[ia[k]] * cq[ib[k]];
+            zn = jacobi_smallest_evec(c6[0], c6[1], c6[2], c6[3], c6[4], c6[5]);
+        }
+        if ((b_flags & 2) && wid == 1) {
+            const int cc = cloud_of[wb];
+            const int knb = min(setup[cc].k_nrm, (int)pb[P8_NTOP]);
+            double n6[6] = {1, 0, 0, 1, 0, 1};
+            if (knb >= 3) {
+                double cu[9];
+#pragma unroll
+                for (int i = 0; i < 9; ++i) cu[i] = pb[P8_SUM + 12 + i] / (double)knb;
+                n6[0] = cu[3] - cu[0] * cu[0];
+                n6[1] = cu[4] - cu[0] * cu[1];
+                n6[2] = cu[5] - cu[0] * cu[2];
+                n6[3] = cu[6] - cu[1] * cu[1];
+                n6[4] = cu[7] - cu[1] * cu[2];
+                n6[5] = cu[8] - cu[2] * cu[2];
+            }
+            d3 nm = fast_eigen3x3(n6[0], n6[1], n6[2], n6[3], n6[4], n6[5]);
+            if (sqrt(dot3(nm, nm)) == 0.0) nm = d3{0, 0, 1};
+            const int gp = (int)pb[P8_GP];
+            v.nrm64[gp] = nm.x;
+            v.nrm64[v.ld + gp] = nm.y;
+            v.nrm64[2 * (size_t)v.ld + gp] = nm.z;
+            if (setup[cc].want_cov) {
+                double cv[6];
+                gicp_cov_from_normal(nm, 1e-3, cv);
+#pragma unroll
+                for (int r = 0; r < 6; ++r) v.cov64[(size_t)r * v.ld + gp] = cv[r];
+            }
+        }
+        if ((b_flags & 1) && wid == 0) {
+            pb[P8_ZN] = zn.x;
+            pb[P8_ZN + 1] = zn.y;
+            pb[P8_ZN + 2] = zn.z;
+        }
+    }
+    __syncthreads();
+
+    // ---------------------------------------------------------------- TOLDI axes (ISR.cpp:286-306)
+    {
+        double* pj = park + g * P8_N;
+        const int flags = (int)pj[P8_FLAGS];
+        double x6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        if (flags & 1) {
+            const double nx = pj[P8_ZN], ny = pj[P8_ZN + 1], nz = pj[P8_ZN + 2];
+            const double qgx = qv[4 * g], qgy = qv[4 * g + 1], qgz = qv[4 * g + 2];
+            const double R = pj[P8_R];
+            const int kkq = (int)pj[P8_KK];
+            const unsigned* rl = lists + g * kCap;
+            for (int r = 1 + l; r < kkq; r += 8) {  // ranks 1 .. kk-1
+                const int slot = (int)rl[r];
+                const double vx = TX[slot] - qgx, vy = TY[slot] - qgy, vz = TZ[slot] - qgz;
+                x6[0] += vx; x6[1] += vy; x6[2] += vz;
+                const double an = nx * vx + ny * vy + nz * vz;
+                const double rr = R - sqrt(vx * vx + vy * vy + vz * vz);
+                const double wgt = (rr * rr) * (an * an);
+                x6[3] += wgt * vx; x6[4] += wgt * vy; x6[5] += wgt * vz;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+            x6[i] += gxd(x6[i], 1);
+            x6[i] += gxd(x6[i], 2);
+            x6[i] += gxd(x6[i], 4);
+        }
+        __builtin_amdgcn_wave_barrier();
+        if ((int)(l == 0) & (int)((flags & 1) != 0)) {
+#pragma unroll
+            for (int i = 0; i < 6; ++i) pj[P8_SUM + i] = x6[i];
+        }
+    }
+    // the frames, on wave 0 for the block's 32 queries
+    __syncthreads();
+    if (wid == 0) {
+        const double* pb = &s_park[lane < kW * kQ ? lane / kQ : 0][lane % kQ][0];
+        const int b_flags = lane < kW * kQ ? (int)pb[P8_FLAGS] : 0;
+        if (b_flags & 1) {
+            const int w = (int)pb[P8_W];
+            const CloudSetup sw = setup[cloud_of[w]];
+            const double qgx = TX[w], qgy = TY[w], qgz = TZ[w];
+            d3 nrm{pb[P8_ZN], pb[P8_ZN + 1], pb[P8_ZN + 2]};
+            if (nrm.x * pb[P8_SUM] + nrm.y * pb[P8_SUM + 1] + nrm.z * pb[P8_SUM + 2] < 0.0)
+                nrm = d3{-nrm.x, -nrm.y, -nrm.z};  // ISR.cpp:298
+            const d3 zax = nrm;
+            const d3 accs{pb[P8_SUM + 3], pb[P8_SUM + 4], pb[P8_SUM + 5]};
+            d3 xax = accs - dot3(accs, zax) * zax;  // ISR.cpp:302-303 (no |x| = 0 guard, as the reference)
+            xax = (1.0 / sqrt(dot3(xax, xax))) * xax;
+            const d3 yax = cross3(zax, xax);  // ISR.cpp:306
+            const double al = sw.alpha, be = sw.beta;
+            const double f12[12] = {al * xax.x, al * xax.y, al * xax.z, al * yax.x, al * yax.y, al * yax.z,
+                                    al * zax.x, al * zax.y, al * zax.z, be * qgx, be * qgy, be * qgz};
+            const int gp = (int)pb[P8_GP];
+#pragma unroll
+            for (int r = 0; r < 12; ++r) {
+                v.fr64[(size_t)r * v.ld + gp] = f12[r];
+                const double f32v = (sw.cf_target && r >= 9) ? (r == 9 ? qgx : (r == 10 ? qgy : qgz)) : f12[r];
+                v.fr32[(size_t)r * v.ld + gp] = (float)f32v;
+            }
+        }
+    }
+#ifdef SE3ICP_PROF
+    PROF8_NOW(t_a3);
+    PROF8_ADD(c_epi, t_a2, t_a3);
+    if (lane == 0) {
+        atomicAdd(ctr + 8, c_scan - c_tight);
+        atomicAdd(ctr + 9, c_tight);
+        atomicAdd(ctr + 10, c_sums);
+        atomicAdd(ctr + 11, c_epi);
+    }
+#endif
+}
+
+}  // namespace
+
+void launch_lrf8(const View& v, const int32_t* wave_base, int nwaves, int32_t* fb_list, int32_t* fb_count,
+                 hipStream_t s) {
+    const int nb = (nwaves + kW - 1) / kW;
+    if (nb == 0) return;
+    hipLaunchKernelGGL(k_lrf8, dim3(nb), dim3(64 * kW), 0, s, v, v.cloud_of, v.setup, v.clouds, v.t3.lo, v.t3.hi,
+                       v.t3.tvec64, wave_base, nwaves, fb_list, fb_count);
+}
+
+}  // namespace se3icp

@@ -115,6 +115,13 @@ void launch_pair_norms(const View& v, int nnodes3, int nnodes12, const double* s
                        int state_stride, hipStream_t s);
 // fused kNN + TOLDI frame + normals/GICP covariance (k_knn.hip); knn list only if v.knn
 void launch_lrf(const View& v, int write_knn, hipStream_t s);
+// the same for the listed tree slots qlist[0 .. *qcount) (device count; grid-strided)
+void launch_lrf_list(const View& v, const int32_t* qlist, const int32_t* qcount, hipStream_t s);
+// eight queries per wavefront (k_lrf8.hip); wave_base[c] = first wave of cloud c (waves
+// aligned to each cloud, nwaves in all); the queries it cannot resolve exactly from f32
+// keys are appended to fb_list (count fb_count, zeroed by the caller) for launch_lrf_list
+void launch_lrf8(const View& v, const int32_t* wave_base, int nwaves, int32_t* fb_list, int32_t* fb_count,
+                 hipStream_t s);
 
 // ---- k_loop.hip
 // exact 1-NN of every active pair's source points: k_nn_prep settles the queries whose

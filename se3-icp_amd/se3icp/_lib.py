@@ -36,7 +36,7 @@ EXPORTED_SYMBOLS = [
     "se3icp_register_batch", "se3icp_register_batch_device", "se3icp_register",
     "se3icp_toldi_frames", "se3icp_knn_self", "se3icp_estimate_normals", "se3icp_nn",
     "se3icp_synthetic_pairs",
-    "se3icp_set_profiling", "se3icp_last_kernel_times", "se3icp_set_trace",
+    "se3icp_set_profiling", "se3icp_last_kernel_times", "se3icp_set_trace", "se3icp_set_lrf_exact",
     # include/se3icp_cc.h: metrics and pose files of the benchmark drivers (host only)
     "se3icp_cc_rot_3d", "se3icp_cc_angular_error_so3", "se3icp_cc_angular_error_so3_alt",
     "se3icp_cc_error_filterreg", "se3icp_cc_rot2euler", "se3icp_cc_avg_eul_error",
@@ -147,6 +147,7 @@ def load():
     L.se3icp_set_profiling.argtypes = [C.c_int, C.c_int]
     L.se3icp_last_kernel_times.argtypes = [C.c_int, dp]
     L.se3icp_set_trace.argtypes = [C.c_int, C.POINTER(Trace)]
+    L.se3icp_set_lrf_exact.argtypes = [C.c_int, C.c_int]
     _lib = L
     return L
 

@@ -302,16 +302,21 @@ def nearest_neighbors(query, data, device: int = 0):
     return idx, d2, int(nr.value)
 
 
+def set_lrf_exact(on: bool, device: int = 0) -> None:
+    """Diagnostic: the exact one-query-per-wavefront kNN/TOLDI kernel for every point."""
+    _lib.check(_lib.load().se3icp_set_lrf_exact(device, 1 if on else 0))
+
+
 def set_profiling(on: bool, device: int = 0) -> None:
     """HIP events around every loop stage (not only the NN grids) from the next batch on."""
     _lib.check(_lib.load().se3icp_set_profiling(device, 1 if on else 0))
 
 
 def last_kernel_times(device: int = 0) -> dict:
-    out = (C.c_double * 23)()
+    out = (C.c_double * 24)()
     _lib.check(_lib.load().se3icp_last_kernel_times(device, out))
     keys = ["nn_se3_ms", "nn_r3_ms", "recheck_ms", "trim_ms", "reduce_ms", "setup_ms", "nn_se3_launches",
             "nn_r3_launches", "se3_dist_evals", "se3_box_tests", "r3_dist_evals", "r3_box_tests",
             "lrf_ms", "lrf_queries", "lrf_leaves", "lrf_merges", "lrf_box_tests", "lrf_candidates",
-            "nn_prep_ms", "se3_queries", "se3_searched", "r3_queries", "r3_searched"]
+            "nn_prep_ms", "se3_queries", "se3_searched", "r3_queries", "r3_searched", "lrf_fallback"]
     return dict(zip(keys, list(out)))

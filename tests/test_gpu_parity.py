@@ -377,3 +377,23 @@ def test_batch_independence_16_vs_two_8(se3icp_mod):
     for i, (f, h) in enumerate(zip(full, a + b)):
         assert np.array_equal(f.T, h.T), (i, f.T - h.T)
         assert (f.num_iterations, f.num_pure_se3_iterations) == (h.num_iterations, h.num_pure_se3_iterations)
+
+
+@pytest.mark.parametrize("k", [90, 30])
+def test_lrf_fast_path_equals_exact_kernel(se3icp_mod, k):
+    """k_lrf8 (eight queries per wavefront) and the exact one-query-per-wavefront k_lrf
+    give bitwise-identical TOLDI frames and normals (same neighbour sets in the same rank
+    order, same arithmetic), at C4 size: the fast path can never change a result."""
+    from se3icp import datasets, registration
+    pairs, _ = datasets.kitti_like_pairs(1, seed=4, first=2, total_pairs=8)
+    pts = pairs[0][0]
+    fast_f = se3icp_mod.toldi_frames(pts, k)
+    fast_n = se3icp_mod.estimate_normals(pts, k)
+    registration.set_lrf_exact(True)
+    try:
+        ex_f = se3icp_mod.toldi_frames(pts, k)
+        ex_n = se3icp_mod.estimate_normals(pts, k)
+    finally:
+        registration.set_lrf_exact(False)
+    assert np.array_equal(fast_f, ex_f), np.nonzero((fast_f != ex_f).reshape(len(pts), -1).any(axis=1))[0][:8]
+    assert np.array_equal(fast_n, ex_n)
