@@ -180,6 +180,25 @@ int64_t se3icp_synthetic_pairs(int device, const double* base, int64_t n, int32_
                                double ratio, double noise_var, uint64_t seed, double* src_out, double* tgt_out,
                                int outputs_on_device);
 
+/* The reference's own synthetic problems, number for number (host; no device needed):
+ * examples/benchmark_synthetic.cpp:91-160 with its random streams -- Open3D's engine
+ * (Seed(1), std::mt19937) for RandomDownSample, std::mt19937 gen(1) with
+ * uniform_real_distribution for T (t in [-t_range, t_range]^3, rot_3d angles in
+ * [-r_range, r_range]; "moderate" setup: 10, pi/2), one static std::mt19937{1} +
+ * normal_distribution for the N(0, noise_var I) noise.  cloud: the full cloud in its file
+ * order (stanford_bunny.ply x 50), n points.  src_out / tgt_out: [n_cases * k * 3]
+ * (k = (int)(ratio * n), every case's noisy source copy and target), T_out [n_cases * 16]
+ * row-major; any output may be NULL.  Returns k or a negative se3icp_status.
+ * flags: SE3ICP_GEN_ARGS_LTR evaluates rot_3d's three angle draws left to right (a
+ * clang-built reference) instead of GCC's right to left. */
+#define SE3ICP_GEN_ARGS_LTR 1
+int64_t se3icp_synthetic_reference(const double* cloud, int64_t n, int32_t n_cases, double ratio, double noise_var,
+                                   double t_range, double r_range, int32_t flags, double* src_out, double* tgt_out,
+                                   double* T_out);
+/* PointCloud::RandomDownSample(ratio) right after utility::random::Seed(seed) (Open3D 0.19):
+ * the kept points in file order into out [k * 3] (may be NULL); returns k. */
+int64_t se3icp_random_downsample(const double* xyz, int64_t n, double ratio, uint32_t seed, double* out);
+
 /* ------------------------------------------------------------- diagnostics
  * Not part of the reference boundary: per-kernel GPU times (HIP events) of the
  * last batch on `device`, used by bench.py for the roofline figures.

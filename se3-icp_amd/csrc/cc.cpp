@@ -2,6 +2,8 @@
 // (include/se3icp_cc.h).  Host code; restated from src/cc.cpp and examples/*.cpp.
 #include "se3icp_cc.h"
 
+#include "refrand.hpp"
+
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -64,14 +66,9 @@ int64_t read12(const char* path, double* out, int64_t cap, int stride) {
 
 extern "C" {
 
-void se3icp_cc_rot_3d(double roll, double pitch, double yaw, double R[9]) {
-    const double cr = std::cos(roll), sr = std::sin(roll), cp = std::cos(pitch), sp = std::sin(pitch);
-    const double cy = std::cos(yaw), sy = std::sin(yaw);
-    // Rz(yaw) * Ry(pitch) * Rx(roll)
-    R[0] = cy * cp; R[1] = cy * sp * sr - sy * cr; R[2] = cy * sp * cr + sy * sr;
-    R[3] = sy * cp; R[4] = sy * sp * sr + cy * cr; R[5] = sy * sp * cr - cy * sr;
-    R[6] = -sp;     R[7] = cp * sr;                R[8] = cp * cr;
-}
+// cc::rot_3d (cc.cpp:22-30): Rz(yaw) Ry(pitch) Rx(roll) through Eigen's quaternion
+// arithmetic, bit for bit (refrand.hpp; pinned by the reference's fixture)
+void se3icp_cc_rot_3d(double roll, double pitch, double yaw, double R[9]) { se3icp::refrand::rot_3d(roll, pitch, yaw, R); }
 
 double se3icp_cc_angular_error_so3(const double R1[9], const double R2[9]) {
     // |vee(log M)| = theta; sin(theta) from the skew part, cos(theta) from the trace

@@ -1,19 +1,22 @@
 // k_gen.hip — the synthetic registration problems of the reference's benchmark
 // (examples/benchmark_synthetic.cpp:91-160), generated on the GPU for batched runs:
 //   source_c = RandomDownSample(base, ratio)       + N(0, noise_var I)   (B_SYN:99, :151)
+//              (one subset for every case, its noise per case)
 //   target_c = RandomDownSample(T_c base, ratio)   + N(0, noise_var I)   (B_SYN:149-153)
 // with add_noise_to_point_cloud (B_SYN:13-56: diagonal covariance noise_var, i.e. standard
 // deviation sqrt(noise_var) per axis) and Open3D RandomDownSample (a random subset of
 // exactly (int)(ratio * n) points, in random order).  Source and target subsets are drawn
-// independently.
+// independently.  The reference's own streams (mt19937, libstdc++ distributions, Open3D's
+// shuffle), number for number, are the host generator gen_ref.cpp.
 //
 // One thread per output point.  The random subset of case c / side s is the image of
 // 0..k-1 under a keyed bijection of [0, n): a 4-round Feistel network on the next even
 // power of two >= n, cycle-walked back into [0, n) (every output index distinct, no sort
 // or shared state).  The noise is Box-Muller on Philox4x32-10 counters (seed, case,
-// side, point).  Counter-based streams replace the reference's mt19937: the protocol and
-// its distributions are the same, the individual samples are not (parity unpinned, see
-// tests/test_generators.py).
+// side, point).  Counter-based streams replace the reference's mt19937 so that a GPU batch
+// of any size is made in one pass: the protocol and its distributions are the same, the
+// individual samples are not (tests/test_generators.py; the exact samples are
+// se3icp_synthetic_reference, tests/test_reference_streams.py).
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -87,7 +90,9 @@ __global__ __launch_bounds__(256) void k_synthetic(const double* __restrict__ ba
     const int side = (int)(t / per_side);  // 0 source, 1 target
     const int64_t r = t - side * per_side;
     const uint32_t c = (uint32_t)(r / k), j = (uint32_t)(r - (int64_t)c * k);
-    const uint32_t key = mix32(seed_lo ^ mix32(seed_hi ^ mix32(2u * c + (uint32_t)side + 1u)));
+    // one source subset shared by every case (the driver downsamples the source once and
+    // copies it per case, B_SYN:99, 146); an independent target subset per case (B_SYN:148)
+    const uint32_t key = mix32(seed_lo ^ mix32(seed_hi ^ mix32(side == 0 ? 1u : 2u * c + 2u)));
     const uint32_t idx = permute_index(j, n, h, key);
     double p[3] = {base[3 * (size_t)idx], base[3 * (size_t)idx + 1], base[3 * (size_t)idx + 2]};
     if (side == 1) {  // target_final_notDS->Transform(T) (B_SYN:149)

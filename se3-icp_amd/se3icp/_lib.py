@@ -35,7 +35,7 @@ EXPORTED_SYMBOLS = [
     "se3icp_get_result",
     "se3icp_register_batch", "se3icp_register_batch_device", "se3icp_register",
     "se3icp_toldi_frames", "se3icp_knn_self", "se3icp_estimate_normals", "se3icp_nn",
-    "se3icp_synthetic_pairs",
+    "se3icp_synthetic_pairs", "se3icp_synthetic_reference", "se3icp_random_downsample",
     "se3icp_set_profiling", "se3icp_last_kernel_times", "se3icp_set_trace", "se3icp_set_lrf_exact",
     # include/se3icp_cc.h: metrics and pose files of the benchmark drivers (host only)
     "se3icp_cc_rot_3d", "se3icp_cc_angular_error_so3", "se3icp_cc_angular_error_so3_alt",
@@ -144,6 +144,11 @@ def load():
     L.se3icp_synthetic_pairs.restype = C.c_int64
     L.se3icp_synthetic_pairs.argtypes = [C.c_int, dp, C.c_int64, C.c_int32, dp, C.c_double, C.c_double, C.c_uint64,
                                          vp, vp, C.c_int]
+    L.se3icp_synthetic_reference.restype = C.c_int64
+    L.se3icp_synthetic_reference.argtypes = [dp, C.c_int64, C.c_int32, C.c_double, C.c_double, C.c_double, C.c_double,
+                                             C.c_int32, dp, dp, dp]
+    L.se3icp_random_downsample.restype = C.c_int64
+    L.se3icp_random_downsample.argtypes = [dp, C.c_int64, C.c_double, C.c_uint32, dp]
     L.se3icp_set_profiling.argtypes = [C.c_int, C.c_int]
     L.se3icp_last_kernel_times.argtypes = [C.c_int, dp]
     L.se3icp_set_trace.argtypes = [C.c_int, C.POINTER(Trace)]

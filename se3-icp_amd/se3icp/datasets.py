@@ -291,3 +291,39 @@ def synthetic_pairs_gpu(base: np.ndarray, Ts: np.ndarray, ratio: float = 0.02, n
     _lib.check(int(min(r, 0)), "synthetic_pairs")
     assert r == k, (r, k)
     return src, tgt
+
+
+# ----------------------------------------------------------------------------- reference streams
+def random_downsample(xyz: np.ndarray, ratio: float = 0.02, seed: int = 1) -> np.ndarray:
+    """Open3D PointCloud::RandomDownSample(ratio) right after utility::random::Seed(seed),
+    number for number (libse3icp host code, std::shuffle over std::mt19937)."""
+    import ctypes as C
+    from . import _lib
+    a = np.ascontiguousarray(xyz, dtype=np.float64)
+    k = int(ratio * a.shape[0])
+    out = np.zeros((k, 3))
+    dp = C.POINTER(C.c_double)
+    r = _lib.load().se3icp_random_downsample(a.ctypes.data_as(dp), a.shape[0], ratio, seed, out.ctypes.data_as(dp))
+    _lib.check(int(min(r, 0)), "random_downsample")
+    return out
+
+
+def synthetic_reference(cloud: np.ndarray, n_cases: int, ratio: float = 0.02, noise_var: float = 0.005,
+                        t_range: float = 10.0, r_range: float = np.pi / 2, args_left_to_right: bool = False):
+    """examples/benchmark_synthetic.cpp:91-160 with the reference's own random streams
+    (se3icp_synthetic_reference): returns (src [C, k, 3], tgt [C, k, 3], T [C, 4, 4]).
+    cloud: the full cloud in file order (stanford_bunny.ply x 50: bunny_full() * 50)."""
+    import ctypes as C
+    from . import _lib
+    a = np.ascontiguousarray(cloud, dtype=np.float64)
+    k = int(ratio * a.shape[0])
+    src = np.zeros((n_cases, k, 3))
+    tgt = np.zeros((n_cases, k, 3))
+    T = np.zeros((n_cases, 4, 4))
+    dp = C.POINTER(C.c_double)
+    r = _lib.load().se3icp_synthetic_reference(a.ctypes.data_as(dp), a.shape[0], n_cases, ratio, noise_var, t_range,
+                                               r_range, 1 if args_left_to_right else 0, src.ctypes.data_as(dp),
+                                               tgt.ctypes.data_as(dp), T.ctypes.data_as(dp))
+    _lib.check(int(min(r, 0)), "synthetic_reference")
+    assert r == k
+    return src, tgt, T

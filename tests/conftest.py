@@ -53,3 +53,12 @@ def pytest_runtest_setup(item):
             torch.cuda.init()
     except Exception:  # the test itself reports a missing device
         pass
+
+
+@pytest.fixture(scope="session")
+def bunny_full():
+    """stanford_bunny.ply's 208,353 vertices in file order (tools/make_bunny_fixtures.py)."""
+    import numpy as np
+    u = np.load(os.path.join(GOLDEN, "bunny_unique_f32.npy"))
+    ids = np.load(os.path.join(GOLDEN, "bunny_vertex_ids.npy"))
+    return u[ids].astype(np.float64)
