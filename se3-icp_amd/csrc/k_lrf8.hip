@@ -424,7 +424,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF8
     // the list length of the lane's own group g, kept alongside (picking nbq[g] at run time
     // would turn the register arrays into scratch memory)
     unsigned nbv = 0u;
-    volatile double* qv = &s_q[wid][0][0];
+    double* qv = &s_q[wid][0][0];
     float fqlo[3] = {0.f, 0.f, 0.f}, fqhi[3] = {0.f, 0.f, 0.f};
     int nlist = 0;
     const int n = cl.n;
