@@ -45,7 +45,10 @@ using namespace knn;
 
 constexpr int kW = 4;          // waves per block
 constexpr int kQ = 8;          // queries per wave (eight lanes each in the group phases)
-constexpr int kCap = 192;      // candidates buffered per query (u32: cut key | candidate id)
+#ifndef SE3ICP_LRF8_CAP
+#define SE3ICP_LRF8_CAP 192
+#endif
+constexpr int kCap = SE3ICP_LRF8_CAP;  // candidates buffered per query (u32: cut key | candidate id), <= 256
 constexpr int kLeaves = 64;    // leaves one wave may scan: candidate id = (list index << 6) | lane
 constexpr unsigned kIdBits = 0xfffu;     // low bits of a list entry: the candidate id
 constexpr unsigned kAll = 0xfffffffeu;   // bound of the accept-all phase (> every finite key)
@@ -556,6 +559,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF8
         OutwardBits itA(0ull, 0), itL(0ull, 0);
         int cur = -1, part = 0;
         bool do_tighten = false, retried = false;
+        float tf = INFINITY;  // f32 box-test bound of the union of the eight (set with each tightening)
         while (!fb_wave) {
             if (do_tighten) {
                 PROF8_NOW(t_t0);
@@ -563,6 +567,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF8
                 PROF8_NOW(t_t1);
                 PROF8_ADD(c_tight, t_t0, t_t1);
                 do_tighten = false;
+                tf = thr_f();  // the box-test bound changes only here
             }
             if (cur >= 0) {  // appending leaf cur (part)
                 if (scan_leaf(cur, part)) {
@@ -611,23 +616,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF8
                     }
                     const int ai = c0 + lane;
                     lbA = ai < nA ? box_lb(firstA + ai) : INFINITY;
-                    itA = OutwardBits(__ballot(lbA <= thr_f()), (lf0 >> sh) - c0);
+                    itA = OutwardBits(__ballot(lbA <= tf), (lf0 >> sh) - c0);
                     haveA = true;
                 }
                 const int j = itA.next();
                 if (j < 0) { haveA = false; c0 += 64; continue; }
-                if (!(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbA), j)) <= thr_f())) continue;
+                if (!(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbA), j)) <= tf)) continue;
                 l0 = (c0 + j) << sh;
                 const int li = l0 + lane;
                 lbL = INFINITY;
                 if ((int)(lane < (1 << sh)) & ((int)(li < s_lo) | (int)(li > s_hi))) lbL = box_lb(first_leaf + li);
-                itL = OutwardBits(__ballot(lbL <= thr_f()), lf0 - l0);
+                itL = OutwardBits(__ballot(lbL <= tf), lf0 - l0);
                 stage = 3;
                 continue;
             } else {
                 const int t = itL.next();
                 if (t < 0) { stage = 2; continue; }
-                if (!(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbL), t)) <= thr_f())) continue;
+                if (!(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbL), t)) <= tf)) continue;
                 leaf = l0 + t;
             }
             cur = leaf;
