@@ -424,6 +424,8 @@ int Engine::read_lrf_stats() {
     std::fprintf(stderr, "[prof] k_lrf cycles/query: knn|scan %.0f sort|tighten %.0f sums|final+sums %.0f finish %.0f "
                  "(queries %.0f, wave cycles summed over the kernel's waves)\n",
                  sum[8] / sum[0], sum[9] / sum[0], sum[10] / sum[0], sum[11] / sum[0], sum[0]);
+    std::fprintf(stderr, "[prof] k_lrf8 per query: tightenings %.3f (overflow %.3f, final %.3f), leaf scans %.3f\n",
+                 sum[2] / sum[0], sum[3] / sum[0], sum[7] / sum[0], sum[1] / sum[0]);
 #endif
     return 0;
 }

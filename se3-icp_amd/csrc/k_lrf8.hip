@@ -390,6 +390,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF8
     unsigned n_leaves = 0, n_sel = 0, n_cand = 0, n_q = 0;
 #ifdef SE3ICP_PROF
     unsigned long long c_scan = 0, c_tight = 0, c_sums = 0, c_epi = 0;
+    unsigned n_tover = 0, n_tend = 0;  // tightenings for an overflowing leaf / for the final <= 128
 #endif
     PROF8_NOW(t_a0);
 
@@ -577,6 +578,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF8
                 } else if (!retried && (int)nbq[0] >= Kw) {
                     do_tighten = true;
                     retried = true;
+#ifdef SE3ICP_PROF
+                    ++n_tover;
+#endif
                 } else if (part == 0) {
                     part = 1;
                     retried = false;
@@ -610,7 +614,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF8
                         unsigned nmax = 0;
 #pragma unroll
                         for (int j = 0; j < kQ; ++j) nmax = max(nmax, nbq[j]);
-                        if (nmax > 128 && !retried) { do_tighten = true; retried = true; continue; }
+                        if (nmax > 128 && !retried) {
+#ifdef SE3ICP_PROF
+                            ++n_tend;
+#endif
+                            do_tighten = true;
+                            retried = true;
+                            continue;
+                        }
                         if (nmax > 128) fb_wave = true;  // (ties at the bound)
                         break;
                     }
@@ -874,6 +885,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF8
         atomicAdd(ctr + 9, c_tight);
         atomicAdd(ctr + 10, c_sums);
         atomicAdd(ctr + 11, c_epi);
+        atomicAdd(ctr + 3, (unsigned long long)n_tover);
+        atomicAdd(ctr + 7, (unsigned long long)n_tend);
     }
 #endif
 }
