@@ -426,6 +426,13 @@ int Engine::read_lrf_stats() {
                  sum[8] / sum[0], sum[9] / sum[0], sum[10] / sum[0], sum[11] / sum[0], sum[0]);
     std::fprintf(stderr, "[prof] k_lrf8 per query: tightenings %.3f (overflow %.3f, final %.3f), leaf scans %.3f\n",
                  sum[2] / sum[0], sum[3] / sum[0], sum[7] / sum[0], sum[1] / sum[0]);
+    {
+        unsigned long long f = 0;  // (16-bit fields, summed as integers)
+        for (int i = 0; i < kStatSlots; ++i) f += h_lrf_stats_[kStatCols * i + 5];
+        std::fprintf(stderr, "[prof] k_lrf8 hand-overs: waves with the leaf table full %llu, no room %llu, > 128 at the end %llu; "
+                     "queries with f32-equal f64-distinct ranks %llu\n",
+                     f & 0xffff, (f >> 16) & 0xffff, (f >> 32) & 0xffff, f >> 48);
+    }
 #endif
     return 0;
 }

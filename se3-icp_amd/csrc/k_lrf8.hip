@@ -43,14 +43,20 @@ namespace {
 
 using namespace knn;
 
-constexpr int kW = 4;          // waves per block
+#ifndef SE3ICP_LRF8_KW
+#define SE3ICP_LRF8_KW 4
+#endif
+constexpr int kW = SE3ICP_LRF8_KW;  // waves per block
 constexpr int kQ = 8;          // queries per wave (eight lanes each in the group phases)
 #ifndef SE3ICP_LRF8_CAP
 #define SE3ICP_LRF8_CAP 192
 #endif
 constexpr int kCap = SE3ICP_LRF8_CAP;  // candidates buffered per query (u32: cut key | candidate id), <= 256
-constexpr int kLeaves = 64;    // leaves one wave may scan: candidate id = (list index << 6) | lane
-constexpr unsigned kIdBits = 0xfffu;     // low bits of a list entry: the candidate id
+#ifndef SE3ICP_LRF8_LEAF_BITS
+#define SE3ICP_LRF8_LEAF_BITS 6
+#endif
+constexpr int kLeaves = 1 << SE3ICP_LRF8_LEAF_BITS;  // leaves one wave may scan: candidate id = (list index << 6) | lane
+constexpr unsigned kIdBits = (1u << (SE3ICP_LRF8_LEAF_BITS + 6)) - 1u;  // low bits of a list entry: the candidate id
 constexpr unsigned kAll = 0xfffffffeu;   // bound of the accept-all phase (> every finite key)
 constexpr unsigned kPad = 0xffffffffu;   // sort padding (> every bound)
 
@@ -306,7 +312,7 @@ __device__ __forceinline__ unsigned rank_key64(const unsigned long long (&k)[16]
 // The final list of the group's query (nbg <= 128 entries): full keys recomputed from the
 // points (nanoflann arithmetic), sorted with the point index as tie-break, the rank-ordered
 // tree slots written back over the list; returns false when two of the ranks the sums use
-// share an f32 key (the query then goes to the exact kernel).
+// share an f32 key but not the f64 distance (the query then goes to the exact kernel).
 __device__ __forceinline__ bool final_group(unsigned* lists, const int* leaves, const double* __restrict__ TX,
                                             const double* __restrict__ TY, const double* __restrict__ TZ,
                                             const int32_t* __restrict__ perm, const int32_t* __restrict__ pos,
@@ -326,23 +332,24 @@ __device__ __forceinline__ bool final_group(unsigned* lists, const int* leaves, 
         k[s] = x;
     }
     net8_64<16, 128>(k, l);
-    // No two of the first lim = min(nbg, max(kk, kn) + 1) ranks may share an f32 key: then
-    // the (key, index) order is the exact (f64 d, index) order of the reference's kNN and of
-    // the exact kernel, whose sums this kernel then reproduces bit for bit.
+    // Two of the first lim = min(nbg, max(kk, kn) + 1) ranks sharing an f32 key must also
+    // share the f64 distance (then both orders fall back to the index): the (key, index)
+    // order is then the exact (f64 d, index) order of the reference's kNN and of the exact
+    // kernel, whose sums this kernel reproduces bit for bit.  Otherwise the query goes to
+    // the exact kernel.
     const int lim = min(nbg, max(kk, kn) + 1);
-    bool tie = false;
+    unsigned tied = 0u;  // bit s: ranks l*16+s and l*16+s+1 share an f32 key
 #pragma unroll
     for (int s = 0; s + 1 < 16; ++s) {
         const int e = l * 16 + s;
-        tie |= (bool)((int)(e + 1 < lim) & (int)((unsigned)(k[s] >> 32) == (unsigned)(k[s + 1] >> 32)));
+        if ((int)(e + 1 < lim) & (int)((unsigned)(k[s] >> 32) == (unsigned)(k[s + 1] >> 32))) tied |= 1u << s;
     }
     {
         // the next lane's first key (lane l + 1 of the group)
         const unsigned first_next = __shfl((unsigned)(k[0] >> 32), (int)(threadIdx.x & 63) + 1, 64);
         const int e = l * 16 + 15;
-        tie |= (bool)((int)(l < 7) & (int)(e + 1 < lim) & (int)((unsigned)(k[15] >> 32) == first_next));
+        if ((int)(l < 7) & (int)(e + 1 < lim) & (int)((unsigned)(k[15] >> 32) == first_next)) tied |= 1u << 15;
     }
-    const bool ok = !(bool)(unsigned)((__ballot(tie) >> (8 * g)) & 0xffull);
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
@@ -350,6 +357,14 @@ __device__ __forceinline__ bool final_group(unsigned* lists, const int* leaves, 
         if (e < nbg) list[e] = (unsigned)(off + pos[off + (int)(unsigned)k[s]]);
     }
     __builtin_amdgcn_wave_barrier();
+    bool bad = false;
+    while (tied) {  // rare: the tree slots of the tied ranks, now in rank order in the list
+        const int e = l * 16 + __builtin_ctz(tied);
+        tied &= tied - 1u;
+        const int a = (int)list[e], b = (int)list[e + 1];
+        bad |= l2_3(qx, qy, qz, TX[a], TY[a], TZ[a]) != l2_3(qx, qy, qz, TX[b], TY[b], TZ[b]);
+    }
+    const bool ok = !(bool)(unsigned)((__ballot(bad) >> (8 * g)) & 0xffull);
     return ok;
 }
 
@@ -362,11 +377,15 @@ __device__ __forceinline__ bool final_group(unsigned* lists, const int* leaves, 
 #define PROF8_ADD(acc, a, b) do {} while (0)
 #endif
 
+#ifndef SE3ICP_LRF8_EPI_WAVE
+#define SE3ICP_LRF8_EPI_WAVE 0  // eigen-solves and frames per wave (0: per block of kW waves)
+#endif
+static_assert(SE3ICP_LRF8_EPI_WAVE || (kW >= 2 && kW * kQ <= 64), "the per-block epilogue: waves 0 and 1, a lane per query");
 #ifndef SE3ICP_LRF8_WPE
 #define SE3ICP_LRF8_WPE 4
 #endif
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF8_WPE))) void k_lrf8(
+__global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF8_WPE))) void k_lrf8(
     View v, const int32_t* __restrict__ cloud_of, const CloudSetup* __restrict__ setup,
     const CloudDev* __restrict__ clouds, const float* __restrict__ tlo, const float* __restrict__ thi,
     const double* __restrict__ tx64, const int32_t* __restrict__ wave_base, int nwaves,
@@ -391,6 +410,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF8
 #ifdef SE3ICP_PROF
     unsigned long long c_scan = 0, c_tight = 0, c_sums = 0, c_epi = 0;
     unsigned n_tover = 0, n_tend = 0;  // tightenings for an overflowing leaf / for the final <= 128
+    unsigned long long fb_cause = 0;     // 16-bit fields: leaf table full, no room, > 128 at the end, f32/f64 ties
+#define PROF8_FB(field) fb_cause += 1ull << (16 * (field))
+#else
+#define PROF8_FB(field) do {} while (0)
 #endif
     PROF8_NOW(t_a0);
 
@@ -478,7 +501,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF8
     // id) <= Tq[j].  part: 0 the whole leaf, 1 / 2 its first / second 32 points (a leaf that
     // does not fit a list even after a tightening is appended in two halves).
     auto scan_leaf = [&](int i, int part) __attribute__((always_inline)) -> bool {
-        if (nlist >= kLeaves) { fb_wave = true; return true; }
+        if (nlist >= kLeaves) { fb_wave = true; PROF8_FB(0); return true; }
         const int li = nlist++;
         ++n_leaves;
         if (lane == 0) leaves[li] = i;
@@ -586,6 +609,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF8
                     retried = false;
                 } else {
                     fb_wave = true;
+                    PROF8_FB(1);
                 }
                 continue;
             }
@@ -622,7 +646,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF8
                             retried = true;
                             continue;
                         }
-                        if (nmax > 128) fb_wave = true;  // (ties at the bound)
+                        if (nmax > 128) { fb_wave = true; PROF8_FB(2); }  // (ties at the bound)
                         break;
                     }
                     const int ai = c0 + lane;
@@ -669,6 +693,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF8
                                        qv[4 * g + 2], cl.off, n, T.L, g, l, nbg, kk, kn, want_t, want_n);
         fb_q = (bool)((int)!exact | (int)(nTop < Kw));
         n_cand += (unsigned)nbg;
+#ifdef SE3ICP_PROF
+        fb_cause += (unsigned long long)__popcll(__ballot((int)fb_q & (int)(l == 0) & (int)(g < qn))) << 48;
+#endif
     }
     // queries for the exact kernel
     if ((int)(mode != 0) & (int)fb_q & (int)(l == 0) & (int)(g < qn)) {
@@ -753,67 +780,82 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF8
     }
 
     // ---------------------------------------------------------------- eigen-solves
+    // TOLDI: C about the quirk centroid cl = (S' - q) / rz (ISR.cpp:259-272, see k_knn.hip),
+    // its smallest eigenvector by cyclic Jacobi; normals: FastEigen3x3 of the kn-point
+    // covariance (Open3D EstimateNormals, ISR.cpp:643) and the GICP covariance from it.
+    auto toldi_eig = [&](double* pb) __attribute__((always_inline)) {
+        const int wb = (int)pb[P8_W];  // the query's tree slot
+        const double rz = (double)((int)pb[P8_KK] / 3);
+        const double q3[3] = {TX[wb], TY[wb], TZ[wb]};
+        double cq[3], S[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            cq[a] = (pb[P8_SUM + a] - q3[a]) / rz;
+            S[a] = pb[P8_SUM + 3 + a];
+        }
+        const double* M = pb + P8_SUM + 6;
+        const int ia[6] = {0, 0, 0, 1, 1, 2}, ib[6] = {0, 1, 2, 1, 2, 2};
+        double c6[6];
+#pragma unroll
+        for (int k = 0; k < 6; ++k)
+            c6[k] = M[k] - S[ia[k]] * cq[ib[k]] - cq[ia[k]] * S[ib[k]] + rz * cq[ia[k]] * cq[ib[k]];
+        const d3 zn = jacobi_smallest_evec(c6[0], c6[1], c6[2], c6[3], c6[4], c6[5]);
+        pb[P8_ZN] = zn.x;
+        pb[P8_ZN + 1] = zn.y;
+        pb[P8_ZN + 2] = zn.z;
+    };
+    auto normal_eig = [&](const double* pb) __attribute__((always_inline)) {
+        const int wb = (int)pb[P8_W];
+        const int cc = cloud_of[wb];
+        const int knb = min(setup[cc].k_nrm, (int)pb[P8_NTOP]);
+        double n6[6] = {1, 0, 0, 1, 0, 1};
+        if (knb >= 3) {
+            double cu[9];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) cu[i] = pb[P8_SUM + 12 + i] / (double)knb;
+            n6[0] = cu[3] - cu[0] * cu[0];
+            n6[1] = cu[4] - cu[0] * cu[1];
+            n6[2] = cu[5] - cu[0] * cu[2];
+            n6[3] = cu[6] - cu[1] * cu[1];
+            n6[4] = cu[7] - cu[1] * cu[2];
+            n6[5] = cu[8] - cu[2] * cu[2];
+        }
+        d3 nm = fast_eigen3x3(n6[0], n6[1], n6[2], n6[3], n6[4], n6[5]);
+        if (sqrt(dot3(nm, nm)) == 0.0) nm = d3{0, 0, 1};
+        const int gp = (int)pb[P8_GP];
+        v.nrm64[gp] = nm.x;
+        v.nrm64[v.ld + gp] = nm.y;
+        v.nrm64[2 * (size_t)v.ld + gp] = nm.z;
+        if (setup[cc].want_cov) {
+            double cv[6];
+            gicp_cov_from_normal(nm, 1e-3, cv);
+#pragma unroll
+            for (int r = 0; r < 6; ++r) v.cov64[(size_t)r * v.ld + gp] = cv[r];
+        }
+    };
+#if SE3ICP_LRF8_EPI_WAVE
+    // each wave its own eight queries (lanes 0-7 TOLDI, 8-15 normals): no block barrier,
+    // a wave that finished its traversal early retires without waiting for the others
+    __builtin_amdgcn_wave_barrier();
+    {
+        double* pb = park + (lane & 7) * P8_N;
+        const int b_flags = lane < 16 ? (int)pb[P8_FLAGS] : 0;
+        if ((int)(lane < 8) & (b_flags & 1)) toldi_eig(pb);
+        if ((int)(lane >= 8) & ((b_flags & 2) >> 1)) normal_eig(pb);
+    }
+    __builtin_amdgcn_wave_barrier();
+#else
     // The 3x3 problems of the block's 32 queries, one lane each: wave 0 the TOLDI ones
-    // (cyclic Jacobi), wave 1 the normals (FastEigen3x3) at the same time.
+    // (cyclic Jacobi), wave 1 the normals at the same time.
     __syncthreads();
-    if (wid <= 1) {  // wave 0: the TOLDI problems, wave 1 the normals, side by side
+    if (wid <= 1) {
         double* pb = &s_park[lane < kW * kQ ? lane / kQ : 0][lane % kQ][0];
         const int b_flags = lane < kW * kQ ? (int)pb[P8_FLAGS] : 0;
-        const int wb = b_flags ? (int)pb[P8_W] : 0;  // the query's tree slot
-        d3 zn{0, 0, 0};
-        if ((b_flags & 1) && wid == 0) {
-            // C about the quirk centroid cl = (S' - q) / rz (ISR.cpp:259-272), see k_knn.hip
-            const double rz = (double)((int)pb[P8_KK] / 3);
-            const double q3[3] = {TX[wb], TY[wb], TZ[wb]};
-            double cq[3], S[3];
-#pragma unroll
-            for (int a = 0; a < 3; ++a) {
-                cq[a] = (pb[P8_SUM + a] - q3[a]) / rz;
-                S[a] = pb[P8_SUM + 3 + a];
-            }
-            const double* M = pb + P8_SUM + 6;
-            const int ia[6] = {0, 0, 0, 1, 1, 2}, ib[6] = {0, 1, 2, 1, 2, 2};
-            double c6[6];
-#pragma unroll
-            for (int k = 0; k < 6; ++k)
-                c6[k] = M[k] - S[ia[k]] * cq[ib[k]] - cq[ia[k]] * S[ib[k]] + rz * cq[ia[k]] * cq[ib[k]];
-            zn = jacobi_smallest_evec(c6[0], c6[1], c6[2], c6[3], c6[4], c6[5]);
-        }
-        if ((b_flags & 2) && wid == 1) {
-            const int cc = cloud_of[wb];
-            const int knb = min(setup[cc].k_nrm, (int)pb[P8_NTOP]);
-            double n6[6] = {1, 0, 0, 1, 0, 1};
-            if (knb >= 3) {
-                double cu[9];
-#pragma unroll
-                for (int i = 0; i < 9; ++i) cu[i] = pb[P8_SUM + 12 + i] / (double)knb;
-                n6[0] = cu[3] - cu[0] * cu[0];
-                n6[1] = cu[4] - cu[0] * cu[1];
-                n6[2] = cu[5] - cu[0] * cu[2];
-                n6[3] = cu[6] - cu[1] * cu[1];
-                n6[4] = cu[7] - cu[1] * cu[2];
-                n6[5] = cu[8] - cu[2] * cu[2];
-            }
-            d3 nm = fast_eigen3x3(n6[0], n6[1], n6[2], n6[3], n6[4], n6[5]);
-            if (sqrt(dot3(nm, nm)) == 0.0) nm = d3{0, 0, 1};
-            const int gp = (int)pb[P8_GP];
-            v.nrm64[gp] = nm.x;
-            v.nrm64[v.ld + gp] = nm.y;
-            v.nrm64[2 * (size_t)v.ld + gp] = nm.z;
-            if (setup[cc].want_cov) {
-                double cv[6];
-                gicp_cov_from_normal(nm, 1e-3, cv);
-#pragma unroll
-                for (int r = 0; r < 6; ++r) v.cov64[(size_t)r * v.ld + gp] = cv[r];
-            }
-        }
-        if ((b_flags & 1) && wid == 0) {
-            pb[P8_ZN] = zn.x;
-            pb[P8_ZN + 1] = zn.y;
-            pb[P8_ZN + 2] = zn.z;
-        }
+        if ((b_flags & 1) && wid == 0) toldi_eig(pb);
+        if ((b_flags & 2) && wid == 1) normal_eig(pb);
     }
     __syncthreads();
+#endif
 
     // ---------------------------------------------------------------- TOLDI axes (ISR.cpp:286-306)
     {
@@ -848,35 +890,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF8
             for (int i = 0; i < 6; ++i) pj[P8_SUM + i] = x6[i];
         }
     }
-    // the frames, on wave 0 for the block's 32 queries
-    __syncthreads();
+    // the frames (ISR.cpp:298-307, 597-607)
+    auto frame_out = [&](const double* pb) __attribute__((always_inline)) {
+        const int w = (int)pb[P8_W];
+        const CloudSetup sw = setup[cloud_of[w]];
+        const double qgx = TX[w], qgy = TY[w], qgz = TZ[w];
+        d3 nrm{pb[P8_ZN], pb[P8_ZN + 1], pb[P8_ZN + 2]};
+        if (nrm.x * pb[P8_SUM] + nrm.y * pb[P8_SUM + 1] + nrm.z * pb[P8_SUM + 2] < 0.0)
+            nrm = d3{-nrm.x, -nrm.y, -nrm.z};  // ISR.cpp:298
+        const d3 zax = nrm;
+        const d3 accs{pb[P8_SUM + 3], pb[P8_SUM + 4], pb[P8_SUM + 5]};
+        d3 xax = accs - dot3(accs, zax) * zax;  // ISR.cpp:302-303 (no |x| = 0 guard, as the reference)
+        xax = (1.0 / sqrt(dot3(xax, xax))) * xax;
+        const d3 yax = cross3(zax, xax);  // ISR.cpp:306
+        const double al = sw.alpha, be = sw.beta;
+        const double f12[12] = {al * xax.x, al * xax.y, al * xax.z, al * yax.x, al * yax.y, al * yax.z,
+                                al * zax.x, al * zax.y, al * zax.z, be * qgx, be * qgy, be * qgz};
+        const int gp = (int)pb[P8_GP];
+#pragma unroll
+        for (int r = 0; r < 12; ++r) {
+            v.fr64[(size_t)r * v.ld + gp] = f12[r];
+            const double f32v = (sw.cf_target && r >= 9) ? (r == 9 ? qgx : (r == 10 ? qgy : qgz)) : f12[r];
+            v.fr32[(size_t)r * v.ld + gp] = (float)f32v;
+        }
+    };
+#if SE3ICP_LRF8_EPI_WAVE
+    __builtin_amdgcn_wave_barrier();
+    {
+        const double* pb = park + (lane & 7) * P8_N;
+        const int b_flags = lane < 8 ? (int)pb[P8_FLAGS] : 0;
+        if (b_flags & 1) frame_out(pb);
+    }
+#else
+    __syncthreads();  // on wave 0 for the block's 32 queries
     if (wid == 0) {
         const double* pb = &s_park[lane < kW * kQ ? lane / kQ : 0][lane % kQ][0];
         const int b_flags = lane < kW * kQ ? (int)pb[P8_FLAGS] : 0;
-        if (b_flags & 1) {
-            const int w = (int)pb[P8_W];
-            const CloudSetup sw = setup[cloud_of[w]];
-            const double qgx = TX[w], qgy = TY[w], qgz = TZ[w];
-            d3 nrm{pb[P8_ZN], pb[P8_ZN + 1], pb[P8_ZN + 2]};
-            if (nrm.x * pb[P8_SUM] + nrm.y * pb[P8_SUM + 1] + nrm.z * pb[P8_SUM + 2] < 0.0)
-                nrm = d3{-nrm.x, -nrm.y, -nrm.z};  // ISR.cpp:298
-            const d3 zax = nrm;
-            const d3 accs{pb[P8_SUM + 3], pb[P8_SUM + 4], pb[P8_SUM + 5]};
-            d3 xax = accs - dot3(accs, zax) * zax;  // ISR.cpp:302-303 (no |x| = 0 guard, as the reference)
-            xax = (1.0 / sqrt(dot3(xax, xax))) * xax;
-            const d3 yax = cross3(zax, xax);  // ISR.cpp:306
-            const double al = sw.alpha, be = sw.beta;
-            const double f12[12] = {al * xax.x, al * xax.y, al * xax.z, al * yax.x, al * yax.y, al * yax.z,
-                                    al * zax.x, al * zax.y, al * zax.z, be * qgx, be * qgy, be * qgz};
-            const int gp = (int)pb[P8_GP];
-#pragma unroll
-            for (int r = 0; r < 12; ++r) {
-                v.fr64[(size_t)r * v.ld + gp] = f12[r];
-                const double f32v = (sw.cf_target && r >= 9) ? (r == 9 ? qgx : (r == 10 ? qgy : qgz)) : f12[r];
-                v.fr32[(size_t)r * v.ld + gp] = (float)f32v;
-            }
-        }
+        if (b_flags & 1) frame_out(pb);
     }
+#endif
 #ifdef SE3ICP_PROF
     PROF8_NOW(t_a3);
     PROF8_ADD(c_epi, t_a2, t_a3);
@@ -887,6 +939,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF8
         atomicAdd(ctr + 11, c_epi);
         atomicAdd(ctr + 3, (unsigned long long)n_tover);
         atomicAdd(ctr + 7, (unsigned long long)n_tend);
+        atomicAdd(ctr + 5, fb_cause);
     }
 #endif
 }

@@ -379,14 +379,29 @@ def test_batch_independence_16_vs_two_8(se3icp_mod):
         assert (f.num_iterations, f.num_pure_se3_iterations) == (h.num_iterations, h.num_pure_se3_iterations)
 
 
+def _lrf_cloud(kind):
+    from se3icp import datasets
+    if kind == "kitti":
+        pairs, _ = datasets.kitti_like_pairs(1, seed=4, first=2, total_pairs=8)
+        return pairs[0][0]
+    # a lattice: ranks with exactly equal f64 distances everywhere (ties k_lrf8 resolves by
+    # the point index); jittered by ~1e-12, distances equal in f32 but not in f64 (the
+    # queries go to the exact kernel)
+    g = np.stack(np.meshgrid(np.arange(48), np.arange(40), np.arange(12), indexing="ij"), -1).reshape(-1, 3) * 0.05
+    if kind == "lattice_jitter":
+        g = g + np.random.default_rng(3).standard_normal(g.shape) * 1e-12
+    return g
+
+
+@pytest.mark.parametrize("kind", ["kitti", "lattice", "lattice_jitter"])
 @pytest.mark.parametrize("k", [90, 30])
-def test_lrf_fast_path_equals_exact_kernel(se3icp_mod, k):
+def test_lrf_fast_path_equals_exact_kernel(se3icp_mod, k, kind):
     """k_lrf8 (eight queries per wavefront) and the exact one-query-per-wavefront k_lrf
     give bitwise-identical TOLDI frames and normals (same neighbour sets in the same rank
-    order, same arithmetic), at C4 size: the fast path can never change a result."""
-    from se3icp import datasets, registration
-    pairs, _ = datasets.kitti_like_pairs(1, seed=4, first=2, total_pairs=8)
-    pts = pairs[0][0]
+    order, same arithmetic), at C4 size and on lattices full of distance ties: the fast path
+    can never change a result."""
+    from se3icp import registration
+    pts = _lrf_cloud(kind)
     fast_f = se3icp_mod.toldi_frames(pts, k)
     fast_n = se3icp_mod.estimate_normals(pts, k)
     registration.set_lrf_exact(True)
@@ -395,5 +410,6 @@ def test_lrf_fast_path_equals_exact_kernel(se3icp_mod, k):
         ex_n = se3icp_mod.estimate_normals(pts, k)
     finally:
         registration.set_lrf_exact(False)
-    assert np.array_equal(fast_f, ex_f), np.nonzero((fast_f != ex_f).reshape(len(pts), -1).any(axis=1))[0][:8]
-    assert np.array_equal(fast_n, ex_n)
+    same_f = (fast_f.view(np.uint64) == ex_f.view(np.uint64)).reshape(len(pts), -1).all(axis=1)
+    assert same_f.all(), np.nonzero(~same_f)[0][:8]
+    assert np.array_equal(fast_n.view(np.uint64), ex_n.view(np.uint64))
