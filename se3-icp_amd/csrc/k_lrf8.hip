@@ -68,6 +68,8 @@ enum Park8 {
     P8_N = 31
 };
 constexpr int kSums8 = 21;
+constexpr int kParkAt = 128;  // list entry where the park starts (8-byte aligned)
+static_assert(kCap >= kParkAt + 2 * P8_N, "the park overlays the list tail");
 
 // lane ^ m within a group of eight lanes (m = 1..7 as used by the networks)
 __device__ __forceinline__ unsigned gx(unsigned x, int m) {
@@ -382,7 +384,7 @@ __device__ __forceinline__ bool final_group(unsigned* lists, const int* leaves, 
 #endif
 static_assert(SE3ICP_LRF8_EPI_WAVE || (kW >= 2 && kW * kQ <= 64), "the per-block epilogue: waves 0 and 1, a lane per query");
 #ifndef SE3ICP_LRF8_WPE
-#define SE3ICP_LRF8_WPE 4
+#define SE3ICP_LRF8_WPE 6  // waves per SIMD: 6 = the LDS limit (26.6 KB per block); A/B 4 -> 5 -> 6: 6.73 -> 6.45 -> 6.38 ms
 #endif
 
 __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF8_WPE))) void k_lrf8(
@@ -390,9 +392,12 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
     const CloudDev* __restrict__ clouds, const float* __restrict__ tlo, const float* __restrict__ thi,
     const double* __restrict__ tx64, const int32_t* __restrict__ wave_base, int nwaves,
     int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_count) {
-    __shared__ unsigned s_list[kW][kQ][kCap];
+    // (a query's park overlays the tail of its list, free once the list is final: <= 128 entries)
+    __shared__ __attribute__((aligned(16))) unsigned s_list[kW][kQ][kCap];
+    auto park_of = [&](int w, int j) __attribute__((always_inline)) {
+        return reinterpret_cast<double*>(&s_list[w][j][kParkAt]);
+    };
     __shared__ int s_leaf[kW][kLeaves];
-    __shared__ double s_park[kW][kQ][P8_N];
     __shared__ double s_q[kW][kQ][4];  // the queries' f64 coordinates (read back per leaf: no registers held)
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int g = lane >> 3, l = lane & 7;  // query of the lane's group, lane within the group
@@ -402,10 +407,8 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
     const double* TY = tx64 + v.ld;
     const double* TZ = tx64 + 2 * (size_t)v.ld;
     const int first_leaf = (1 << T.L) - 1;
-    double* park = &s_park[wid][0][0];
     unsigned* lists = &s_list[wid][0][0];
     int* leaves = s_leaf[wid];
-    if (lane < kQ) park[lane * P8_N + P8_FLAGS] = 0.0;
     unsigned n_leaves = 0, n_sel = 0, n_cand = 0, n_q = 0;
 #ifdef SE3ICP_PROF
     unsigned long long c_scan = 0, c_tight = 0, c_sums = 0, c_epi = 0;
@@ -753,7 +756,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
         }
         __builtin_amdgcn_wave_barrier();
         if (l == 0) {
-            double* pj = park + g * P8_N;
+            double* pj = park_of(wid, g);
             const int flags = mine ? ((want_t ? 1 : 0) | (want_n ? 2 : 0)) : 0;
             pj[P8_FLAGS] = (double)flags;
             if (mine) {
@@ -838,7 +841,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
     // a wave that finished its traversal early retires without waiting for the others
     __builtin_amdgcn_wave_barrier();
     {
-        double* pb = park + (lane & 7) * P8_N;
+        double* pb = park_of(wid, lane & 7);
         const int b_flags = lane < 16 ? (int)pb[P8_FLAGS] : 0;
         if ((int)(lane < 8) & (b_flags & 1)) toldi_eig(pb);
         if ((int)(lane >= 8) & ((b_flags & 2) >> 1)) normal_eig(pb);
@@ -849,7 +852,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
     // (cyclic Jacobi), wave 1 the normals at the same time.
     __syncthreads();
     if (wid <= 1) {
-        double* pb = &s_park[lane < kW * kQ ? lane / kQ : 0][lane % kQ][0];
+        double* pb = park_of(lane < kW * kQ ? lane / kQ : 0, lane % kQ);
         const int b_flags = lane < kW * kQ ? (int)pb[P8_FLAGS] : 0;
         if ((b_flags & 1) && wid == 0) toldi_eig(pb);
         if ((b_flags & 2) && wid == 1) normal_eig(pb);
@@ -859,7 +862,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
 
     // ---------------------------------------------------------------- TOLDI axes (ISR.cpp:286-306)
     {
-        double* pj = park + g * P8_N;
+        double* pj = park_of(wid, g);
         const int flags = (int)pj[P8_FLAGS];
         double x6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         if (flags & 1) {
@@ -917,14 +920,14 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
 #if SE3ICP_LRF8_EPI_WAVE
     __builtin_amdgcn_wave_barrier();
     {
-        const double* pb = park + (lane & 7) * P8_N;
+        const double* pb = park_of(wid, lane & 7);
         const int b_flags = lane < 8 ? (int)pb[P8_FLAGS] : 0;
         if (b_flags & 1) frame_out(pb);
     }
 #else
     __syncthreads();  // on wave 0 for the block's 32 queries
     if (wid == 0) {
-        const double* pb = &s_park[lane < kW * kQ ? lane / kQ : 0][lane % kQ][0];
+        const double* pb = park_of(lane < kW * kQ ? lane / kQ : 0, lane % kQ);
         const int b_flags = lane < kW * kQ ? (int)pb[P8_FLAGS] : 0;
         if (b_flags & 1) frame_out(pb);
     }
