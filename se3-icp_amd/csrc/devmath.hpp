@@ -164,6 +164,21 @@ __device__ inline d3 fast_eigen3x3(double c00, double c01, double c02, double c1
     return d3{0, 0, 1};
 }
 
+// The SE(3) 12-vector of point gp as its rows of the frame buffers (fr64 [ld][12] f64,
+// fr32 [ld][12] f32; 16-byte stores).  f32 translation rows: the point itself for a cf
+// target (ISR.cpp:834-836), else the beta-weighted translation.
+__device__ __forceinline__ void store_frame_rows(double* fr64, float* fr32, int gp, const double* f12, bool cf_target,
+                                                 double qx, double qy, double qz) {
+    double2* r64 = reinterpret_cast<double2*>(fr64 + (size_t)gp * 12);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) r64[k] = make_double2(f12[2 * k], f12[2 * k + 1]);
+    float4* r32 = reinterpret_cast<float4*>(fr32 + (size_t)gp * 12);
+    r32[0] = make_float4((float)f12[0], (float)f12[1], (float)f12[2], (float)f12[3]);
+    r32[1] = make_float4((float)f12[4], (float)f12[5], (float)f12[6], (float)f12[7]);
+    r32[2] = cf_target ? make_float4((float)f12[8], (float)qx, (float)qy, (float)qz)
+                       : make_float4((float)f12[8], (float)f12[9], (float)f12[10], (float)f12[11]);
+}
+
 // GetRotationFromE1ToX (ISR.cpp:4-14) and Cov = Rx diag(eps,1,1) Rx^T (ISR.cpp:46-51),
 // returned as the 6 unique entries (xx xy xz yy yz zz).
 __device__ inline void gicp_cov_from_normal(d3 n, double eps, double out[6]) {

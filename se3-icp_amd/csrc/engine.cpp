@@ -740,8 +740,10 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         ktimes_.r3_queries = sum[6];
         ktimes_.r3_searched = sum[7];
 #ifdef SE3ICP_PROF
-        std::fprintf(stderr, "[prof] nn12: leaf visits %.0f, lanes wanting a visited leaf %.1f%% of valid lanes\n",
-                     sum[9], 100.0 * sum[8] / std::max(1.0, sum[10]));
+        std::fprintf(stderr, "[prof] nn12: leaf visits %.0f, lanes wanting a visited leaf %.1f%% of valid lanes; "
+                     "%.0f group waves, %.1f us each on average (100 MHz clock)\n",
+                     sum[9], 100.0 * sum[8] / std::max(1.0, sum[10]), std::floor(sum[11] / 17592186044416.0),
+                     std::fmod(sum[11], 17592186044416.0) / 100.0 / std::max(1.0, std::floor(sum[11] / 17592186044416.0)));
 #endif
     }
     float setup_ms = 0, loop_ms = 0;
@@ -869,8 +871,8 @@ int Engine::toldi_frames(const double* xyz, int64_t n, int k, double* frames) {
         double* F = frames + 16 * i;
         // packing [R00 R10 R20 R01 R11 R21 R02 R12 R22 t0 t1 t2] -> row-major 4x4
         for (int r = 0; r < 3; ++r) {
-            for (int c = 0; c < 3; ++c) F[r * 4 + c] = fr[(size_t)(c * 3 + r) * ld_ + i];
-            F[r * 4 + 3] = fr[(size_t)(9 + r) * ld_ + i];
+            for (int c = 0; c < 3; ++c) F[r * 4 + c] = fr[(size_t)i * 12 + c * 3 + r];
+            F[r * 4 + 3] = fr[(size_t)i * 12 + 9 + r];
         }
         F[12] = F[13] = F[14] = 0.0;
         F[15] = 1.0;
@@ -942,10 +944,11 @@ int Engine::nn(const double* query, int64_t nq, const double* data, int64_t nd, 
     for (int64_t i = 0; i < ntot; ++i) {
         const double* row = i < nq ? query + dim * i : data + dim * (i - nq);
         double n2 = 0;
-        for (int r = 0; r < dim; ++r) {
-            m64[(size_t)r * L + i] = row[r];
+        for (int r = 0; r < dim; ++r) {  // (12-D vectors as rows, 3-D points as columns: tree_in_ix)
+            const size_t at = dim == 12 ? (size_t)i * 12 + r : (size_t)r * L + i;
+            m64[at] = row[r];
             const double c = dim == 3 ? row[r] - cen[r] : row[r];
-            m32[(size_t)r * L + i] = (float)c;
+            m32[at] = (float)c;
             n2 += c * c;
         }
         if (i >= nq) nb = std::max(nb, std::sqrt(n2));

@@ -691,15 +691,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
             const double al = st.alpha, be = st.beta;
             const double f12[12] = {al * xax.x, al * xax.y, al * xax.z, al * yax.x, al * yax.y, al * yax.z,
                                     al * zax.x, al * zax.y, al * zax.z, be * qx, be * qy, be * qz};
-            const int gp = (int)pb[PK_GP];
-#pragma unroll
-            for (int r = 0; r < 12; ++r) {
-                v.fr64[(size_t)r * v.ld + gp] = f12[r];
-                // f32 copy: 12-D search vectors of targets (cf: translation rows = points,
-                // ISR.cpp:834-836) and the kd-tree grouping of sources
-                const double f32v = (st.cf_target && r >= 9) ? (r == 9 ? qx : (r == 10 ? qy : qz)) : f12[r];
-                v.fr32[(size_t)r * v.ld + gp] = (float)f32v;
-            }
+            // (f32 copy: 12-D search vectors of targets and the kd-tree grouping of sources)
+            store_frame_rows(v.fr64, v.fr32, (int)pb[PK_GP], f12, st.cf_target, qx, qy, qz);
         }
     }
 #ifdef SE3ICP_PROF

@@ -909,13 +909,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
         const double al = sw.alpha, be = sw.beta;
         const double f12[12] = {al * xax.x, al * xax.y, al * xax.z, al * yax.x, al * yax.y, al * yax.z,
                                 al * zax.x, al * zax.y, al * zax.z, be * qgx, be * qgy, be * qgz};
-        const int gp = (int)pb[P8_GP];
-#pragma unroll
-        for (int r = 0; r < 12; ++r) {
-            v.fr64[(size_t)r * v.ld + gp] = f12[r];
-            const double f32v = (sw.cf_target && r >= 9) ? (r == 9 ? qgx : (r == 10 ? qgy : qgz)) : f12[r];
-            v.fr32[(size_t)r * v.ld + gp] = (float)f32v;
-        }
+        store_frame_rows(v.fr64, v.fr32, (int)pb[P8_GP], f12, sw.cf_target, qgx, qgy, qgz);
     };
 #if SE3ICP_LRF8_EPI_WAVE
     __builtin_amdgcn_wave_barrier();

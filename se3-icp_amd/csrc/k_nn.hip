@@ -154,6 +154,15 @@ __device__ __forceinline__ void compact_sweep(const float4* tile, const float4* 
 // chunks with at least this many searched queries use k_nn_group, sparser ones k_nn_single
 // (measured: a 12-D wave-per-query search costs ~5x the lanes' share of a group's, a 3-D
 // one far more, but a group's latency bounds an iteration with few groups)
+#ifndef SE3ICP_NN_WPE
+#define SE3ICP_NN_WPE 4  // waves per SIMD of k_nn_group (4: its natural 128 VGPRs)
+#endif
+#ifndef SE3ICP_NN_XCD
+#define SE3ICP_NN_XCD 0  // XCD-aware chunk -> block mapping of k_nn_prep / k_nn_group (A/B: 1 slower, pairs load XCDs unevenly)
+#endif
+#ifndef SE3ICP_NN_SPLIT
+#define SE3ICP_NN_SPLIT 1
+#endif
 #ifndef SE3ICP_NN_DENSE
 #define SE3ICP_NN_DENSE 128
 #endif
@@ -269,7 +278,7 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
 __global__ __launch_bounds__(1024) void k_nn_prep(View v) {
     constexpr int NL = kChunkQ / 64;  // leaves (groups) per chunk
     __shared__ int s_cnt[NL], s_slot[NL], s_base[NL], s_wc[NL], s_single;
-    const int c = blockIdx.x;
+    const int c = SE3ICP_NN_XCD ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int pair = c >> v.chunk_level;
     const PairDev* P = v.pairs + pair;
     const int phase = P->phase;
@@ -374,7 +383,7 @@ __device__ __forceinline__ void nn_finish(const View& v, const PairDev* P, int p
 }
 
 template <int D>
-__global__ __launch_bounds__(256) void k_nn_group(View v) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_WPE))) void k_nn_group(View v) {
     constexpr int NV = (D + 3) / 4;
     __shared__ float4 s_tile[kWaves][kLeafMax * NV];
     // compacted leaf sweeps (12-D): the wave's query vectors, the list of lanes that want
@@ -386,19 +395,25 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     // wave-uniform work item: group jg (64 listed queries) of chunk c; the pair record,
     // node boxes and leaf ranges become scalar loads
-    const int gi = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + wid);
+    // (SE3ICP_NN_SPLIT waves per group of the 12-D search, 64 / split queries each: more,
+    // shorter waves for a launch whose time is set by its longest waves)
+    constexpr int kSplit = D == 12 ? SE3ICP_NN_SPLIT : 1;
+    // (blocks of one XCD take consecutive chunks: a pair's target tree stays in that XCD's L2)
+    const int bx = SE3ICP_NN_XCD ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int wi = __builtin_amdgcn_readfirstlane(bx * kWaves + wid);
+    const int gi = wi / kSplit, q_lo = (wi % kSplit) * (64 / kSplit);
     const int c = gi >> 4;
     if (c >= v.nchunks) return;
     const int pair = c >> v.chunk_level;
     const PairDev* P = v.pairs + pair;
     const int phase = P->phase;
     if (phase != (D == 12 ? PHASE_SE3 : PHASE_R3)) return;
-    const int cnt_q = __builtin_amdgcn_readfirstlane(v.qcount[gi]);
-    if (cnt_q == 0) return;
+    const int cnt_q = min(__builtin_amdgcn_readfirstlane(v.qcount[gi]) - q_lo, 64 / kSplit);
+    if (cnt_q <= 0) return;
     const CloudDev cs = v.clouds[P->src], ct = v.clouds[P->tgt];
     const TreeRef TR = (D == 12) ? v.t12 : v.t3;
     const bool valid = lane < cnt_q;
-    const int gx = cs.off + v.qlist[(size_t)gi * 64 + (valid ? lane : 0)];  // source tree slot
+    const int gx = cs.off + v.qlist[(size_t)gi * 64 + q_lo + (valid ? lane : 0)];  // source tree slot
     const int g = cs.off + TR.perm[gx];
     const float mrg = valid ? v.nn_margin[g] : 0.f;
 
@@ -467,6 +482,7 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
     unsigned n_eval = 0, n_box = 0;  // wave-uniform work counters (roofline accounting)
 #ifdef SE3ICP_PROF
     unsigned n_want = 0, n_leafv = 0, n_valid = __popcll(__ballot(valid));
+    const unsigned long long t_w0 = __builtin_amdgcn_s_memrealtime();
 #endif
     while (sp > 0) {
         const int h = __builtin_amdgcn_readlane(stk, sp - 1);
@@ -571,6 +587,7 @@ __global__ __launch_bounds__(256) void k_nn_group(View v) {
             atomicAdd(v.stats + kStatCols * (gi & 63) + 8, (unsigned long long)n_want);
             atomicAdd(v.stats + kStatCols * (gi & 63) + 9, (unsigned long long)n_leafv);
             atomicAdd(v.stats + kStatCols * (gi & 63) + 10, (unsigned long long)n_leafv * n_valid);
+            atomicAdd(v.stats + kStatCols * (gi & 63) + 11, (1ull << 44) + (__builtin_amdgcn_s_memrealtime() - t_w0));  // waves, wave time
         }
 #endif
     }
@@ -737,7 +754,8 @@ void launch_nn_prep(const View& v, hipStream_t s) {
 // 16 groups of 64 per chunk, kWaves groups per block
 // and the single-query kernel over a fixed grid (8192 waves)
 void launch_nn_se3(const View& v, hipStream_t s) {
-    hipLaunchKernelGGL(k_nn_group<12>, dim3(v.nchunks * (kChunkQ / 64) / kWaves), dim3(64 * kWaves), 0, s, v);
+    hipLaunchKernelGGL(k_nn_group<12>, dim3(v.nchunks * (kChunkQ / 64) * SE3ICP_NN_SPLIT / kWaves), dim3(64 * kWaves), 0,
+                       s, v);
     hipLaunchKernelGGL(k_nn_single<12>, dim3(2048), dim3(256), 0, s, v);
 }
 void launch_nn_r3(const View& v, hipStream_t s) {

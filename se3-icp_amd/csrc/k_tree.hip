@@ -63,7 +63,7 @@ __global__ __launch_bounds__(256) void k_tree_bbox(TreeView t, int level) {
         const int pt = cl.off + t.perm[g];
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            const uint32_t u = ord_bits(t.vec[(size_t)d * t.ld + pt]);
+            const uint32_t u = ord_bits(t.vec[tree_in_ix(t, d, pt)]);
             lo[d] = u;
             hi[d] = u;
         }
@@ -111,7 +111,7 @@ __global__ __launch_bounds__(256) void k_tree_keys(TreeView t, int level, unsign
         if (e > ext) { ext = e; best = d; }
     }
     const int p = t.perm[g];
-    const uint32_t u = ord_bits(t.vec[(size_t)best * t.ld + cl.off + p]);
+    const uint32_t u = ord_bits(t.vec[tree_in_ix(t, best, cl.off + p)]);
     const unsigned long long hiw = ((unsigned long long)c << t.L) | ((unsigned long long)node << (t.L - level));
     keys[g] = (hiw << 32) | u;
     vals[g] = p;
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(256) void k_tree_keys32(TreeView t, int level, int 
         if (e > ext) { ext = e; best = d; lo = l; }
     }
     const int p = t.perm[g];
-    const float x = t.vec[(size_t)best * t.ld + cl.off + p];
+    const float x = t.vec[tree_in_ix(t, best, cl.off + p)];
     const float qmax = (float)((1u << qbits) - 1u);
     float qf = (ext > 0.f && ext < INFINITY) ? (x - lo) * (qmax / ext) : 0.f;
     qf = fminf(fmaxf(qf, 0.f), qmax);  // NaN -> 0
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
                     ++cnt;
 #pragma unroll
                     for (int d = 0; d < D; ++d) {
-                        const float x = t.vec[(size_t)d * t.ld + cl.off + p];
+                        const float x = t.vec[tree_in_ix(t, d, cl.off + p)];
                         s1[d] += x;
                         s2[d] = fmaf(x, x, s2[d]);
                     }
@@ -230,7 +230,7 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
                     const int p = s_val[e];
 #pragma unroll
                     for (int d = 0; d < D; ++d) {
-                        const float x = t.vec[(size_t)d * t.ld + cl.off + p];
+                        const float x = t.vec[tree_in_ix(t, d, cl.off + p)];
                         lo[d] = fminf(lo[d], x);
                         hi[d] = fmaxf(hi[d], x);
                     }
@@ -259,7 +259,7 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
             const int lane = tid & 63, wv = tid >> 6;
             for (int k = wv; k < nsub; k += kLocalThreads / 64) {
                 const int a0 = tree_first(n, l, (i << r) + k) - A, a1 = tree_first(n, l, (i << r) + k + 1) - A;
-                const float* row = t.vec + (size_t)s_best[k] * t.ld + cl.off;
+                const int bd = s_best[k];
                 unsigned long long key[kWaveSortPer];
 #pragma unroll
                 for (int u = 0; u < kWaveSortPer; ++u) {
@@ -267,7 +267,7 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
                     key[u] = ~0ull;
                     if (e < a1) {
                         const int p = s_val[e];
-                        key[u] = ((unsigned long long)ord_bits(row[p]) << 32) | (unsigned)p;
+                        key[u] = ((unsigned long long)ord_bits(t.vec[tree_in_ix(t, bd, cl.off + p)]) << 32) | (unsigned)p;
                     }
                 }
                 wave_sort_keys<kWaveSortPer>(key);
@@ -292,8 +292,7 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
                 k[u] = ~0ull;
                 if (e < m) {
                     const int sub = tree_node_of(A + e, n, l) - (i << r);
-                    const float* row = t.vec + (size_t)s_best[sub] * t.ld;
-                    const uint32_t c = ord_bits(row[cl.off + s_val[e]]);
+                    const uint32_t c = ord_bits(t.vec[tree_in_ix(t, s_best[sub], cl.off + s_val[e])]);
                     k[u] = ((unsigned long long)(unsigned)sub << (32 + kLocalBits)) | ((unsigned long long)c << kLocalBits) |
                            (unsigned)e;
                 }
@@ -327,10 +326,33 @@ __global__ __launch_bounds__(256) void k_tree_finish(TreeView t) {
     if (g < t.npts) {
         const CloudDev cl = t.clouds[t.cloud_of[g]];
         const int p = t.perm[g];
-        t.pos[cl.off + p] = g - cl.off;
-        for (int d = 0; d < t.D; ++d) t.tvec[(size_t)d * t.ld + g] = t.vec[(size_t)d * t.ld + cl.off + p];
-        if ((t.tvec64 != nullptr) & !((t.vec64_sources_only != 0) & ((t.cloud_of[g] & 1) != 0)))
-            for (int d = 0; d < t.D; ++d) t.tvec64[(size_t)d * t.ld + g] = t.vec64[(size_t)d * t.ld + cl.off + p];
+        const int src = cl.off + p;
+        t.pos[src] = g - cl.off;
+        const bool want64 = (t.tvec64 != nullptr) & !((t.vec64_sources_only != 0) & ((t.cloud_of[g] & 1) != 0));
+        if (t.D == 12) {  // one 48-B and one 96-B row per point (16-B loads)
+            const float4* r32 = reinterpret_cast<const float4*>(t.vec + (size_t)src * 12);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const float4 x = r32[k];
+                t.tvec[(size_t)(4 * k) * t.ld + g] = x.x;
+                t.tvec[(size_t)(4 * k + 1) * t.ld + g] = x.y;
+                t.tvec[(size_t)(4 * k + 2) * t.ld + g] = x.z;
+                t.tvec[(size_t)(4 * k + 3) * t.ld + g] = x.w;
+            }
+            if (want64) {
+                const double2* r64 = reinterpret_cast<const double2*>(t.vec64 + (size_t)src * 12);
+#pragma unroll
+                for (int k = 0; k < 6; ++k) {
+                    const double2 x = r64[k];
+                    t.tvec64[(size_t)(2 * k) * t.ld + g] = x.x;
+                    t.tvec64[(size_t)(2 * k + 1) * t.ld + g] = x.y;
+                }
+            }
+        } else {
+            for (int d = 0; d < t.D; ++d) t.tvec[(size_t)d * t.ld + g] = t.vec[(size_t)d * t.ld + src];
+            if (want64)
+                for (int d = 0; d < t.D; ++d) t.tvec64[(size_t)d * t.ld + g] = t.vec64[(size_t)d * t.ld + src];
+        }
     }
 }
 

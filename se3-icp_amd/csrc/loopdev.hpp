@@ -40,7 +40,7 @@ __device__ __forceinline__ void query_f64(const View& v, const double* T, int g,
     if constexpr (D == 12) {
         double m[12];
 #pragma unroll
-        for (int r = 0; r < 12; ++r) m[r] = v.fr64[(size_t)r * v.ld + g];
+        for (int r = 0; r < 12; ++r) m[r] = v.fr64[(size_t)g * 12 + r];
         pose_frame(T, m, q);
     } else {
         pose_point(T, v.xyz64[g], v.xyz64[v.ld + g], v.xyz64[2 * (size_t)v.ld + g], q);
@@ -78,11 +78,11 @@ __device__ __forceinline__ double l2_nanoflann3(const double* a, const double* b
 __device__ __forceinline__ void target12(const View& v, const CloudDev& ct, bool cf, int j, double* b) {
     const int gt = ct.off + j;
 #pragma unroll
-    for (int r = 0; r < 9; ++r) b[r] = v.fr64[(size_t)r * v.ld + gt];
+    for (int r = 0; r < 9; ++r) b[r] = v.fr64[(size_t)gt * 12 + r];
     if (cf) {
         b[9] = v.xyz64[gt]; b[10] = v.xyz64[v.ld + gt]; b[11] = v.xyz64[2 * (size_t)v.ld + gt];
     } else {
-        b[9] = v.fr64[9 * (size_t)v.ld + gt]; b[10] = v.fr64[10 * (size_t)v.ld + gt]; b[11] = v.fr64[11 * (size_t)v.ld + gt];
+        b[9] = v.fr64[(size_t)gt * 12 + 9]; b[10] = v.fr64[(size_t)gt * 12 + 10]; b[11] = v.fr64[(size_t)gt * 12 + 11];
     }
 }
 
@@ -92,9 +92,9 @@ __device__ __forceinline__ void target12(const View& v, const CloudDev& ct, bool
 __device__ __forceinline__ float stored_dist(const View& v, int phase, const CloudDev& ct, const double* Q, int j) {
     const int gt = ct.off + j;
     if (phase == PHASE_SE3) {
-        const double dx = Q[9] - v.fr64[9 * (size_t)v.ld + gt];
-        const double dy = Q[10] - v.fr64[10 * (size_t)v.ld + gt];
-        const double dz = Q[11] - v.fr64[11 * (size_t)v.ld + gt];
+        const double dx = Q[9] - v.fr64[(size_t)gt * 12 + 9];
+        const double dy = Q[10] - v.fr64[(size_t)gt * 12 + 10];
+        const double dz = Q[11] - v.fr64[(size_t)gt * 12 + 11];
         return (float)sqrt((dx * dx + dy * dy) + dz * dz);
     }
     const double b[3] = {v.xyz64[gt], v.xyz64[v.ld + gt], v.xyz64[2 * (size_t)v.ld + gt]};

@@ -23,11 +23,11 @@ struct TreeView {
     int32_t ld;
     const CloudDev* clouds;
     const int32_t* cloud_of;
-    const float* vec;  // [D][ld] input vectors, original order
+    const float* vec;  // input vectors, original order: 12-D [ld][12] rows, 3-D [3][ld] columns
     int32_t* perm;     // [ld] tree position (global slot) -> local point index
     int32_t* pos;      // [ld] point (global slot) -> local tree position
     float* tvec;       // [D][ld] vectors in tree order
-    const double* vec64;  // optional [D][ld] f64 vectors (original order) ...
+    const double* vec64;  // optional f64 vectors (original order, the layout of vec) ...
     double* tvec64;       // ... copied into tree order (coalesced leaf / query-chunk loads)
     int32_t vec64_sources_only;  // copy the f64 vectors of even (source) clouds only
     uint32_t* blo;     // [nclouds][nnodes][D] build scratch (orderable bits)
@@ -46,6 +46,12 @@ __host__ __device__ __forceinline__ int tree_node_of(int x, int n, int level) {
     return (int)(v / n) - 1;
 }
 __host__ __device__ __forceinline__ int tree_heap(int level, int i) { return (1 << level) - 1 + i; }
+// element d of the input vector at global slot p: the 12-D vectors (SE(3) frames) are
+// rows (a gather by the permutation reads one or two cache lines, not twelve), the 3-D
+// points columns
+__device__ __forceinline__ size_t tree_in_ix(const TreeView& t, int d, int p) {
+    return t.D == 12 ? (size_t)p * 12 + d : (size_t)d * t.ld + p;
+}
 
 inline int tree_depth_for(int max_n) {
     int L = 0;

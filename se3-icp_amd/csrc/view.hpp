@@ -50,8 +50,8 @@ struct View {
     const double* const* in_ptr;  // per cloud: AoS xyz input (device)
     double* xyz64;
     float* xyz32;
-    double* fr64;
-    float* fr32;
+    double* fr64;  // [ld][12] SE(3) 12-vectors of every point (rows: gathered by point)
+    float* fr32;   // [ld][12] their f32 copies (the 12-D trees' input)
     double* nrm64;
     double* cov64;
     double* conf64;
