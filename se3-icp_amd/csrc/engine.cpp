@@ -107,7 +107,7 @@ Engine::~Engine() {
                      &d_fr64_, &d_fr32_, &d_nrm64_, &d_cov64_, &d_conf64_, &d_knn_,
                      &d_corr_idx_, &d_corr_dist_, &d_flag_list_, &d_flag_count_, &d_trim_key_, &d_red_partial_,
                      &d_red_out_, &d_work_, &d_wb_, &d_wn_, &d_chunks_, &d_partial_, &d_centers_,
-                     &d_rechecked_, &d_keys0_, &d_keys1_, &d_vals1_, &d_sort_tmp_, &d_stats_,
+                     &d_rechecked_, &d_keys0_, &d_vals1_, &d_sort_tmp_, &d_stats_,
                      &d_qlist_, &d_qcount_, &d_hist_, &d_cert_d1_, &d_cert_l2_, &d_cert_it_, &d_margin_, &d_sqlist_, &d_state_, &d_trim_cand_, &d_trim_ctr_, &d_scales_, &d_trim_hist_,
                      &d_lrf_fb_, &d_lrf_fbn_,
                      &t3_.perm, &t3_.pos, &t3_.vec, &t3_.blo, &t3_.bhi, &t3_.lo, &t3_.hi,
@@ -157,7 +157,7 @@ int Engine::alloc_points(int64_t ntot, int kmax, bool knn_list) {
               ensure<double>(d_nrm64_, 3 * L) && ensure<double>(d_cov64_, 6 * L) && ensure<double>(d_conf64_, L) &&
               (!knn_list || ensure<int32_t>(d_knn_, L * kmax_)) && ensure<int32_t>(d_corr_idx_, L) && ensure<float>(d_corr_dist_, L) &&
               ensure<int32_t>(d_flag_list_, L) && ensure<int32_t>(d_flag_count_, 4) &&
-              ensure<unsigned long long>(d_keys0_, L) && ensure<unsigned long long>(d_keys1_, L) &&
+              ensure<uint32_t>(d_keys0_, L) &&
               ensure<int32_t>(d_vals1_, L) && ensure<unsigned long long>(d_stats_, kStatCols * kStatSlots) &&
               ensure<float>(d_cert_d1_, L) && ensure<float>(d_cert_l2_, L) && ensure<int32_t>(d_cert_it_, L) &&
               ensure<float>(d_margin_, L) && ensure<int32_t>(d_sqlist_, L);
@@ -238,12 +238,11 @@ int Engine::build_tree(int D, const float* vec, hipStream_t s, const double* vec
     if (!ensure<uint32_t>(tb.blo, nb) || !ensure<uint32_t>(tb.bhi, nb) || !ensure<float>(tb.lo, nb) ||
         !ensure<float>(tb.hi, nb) || (vec64 && !ensure<double>(tb.vec64, (size_t)D * ld_)))
         return SE3ICP_ERR_OUT_OF_MEMORY;
-    int cbits = 0;
-    while ((1 << cbits) < nclouds_) ++cbits;
-    const size_t need = tree_sort_temp_bytes((int)ntot_, 32 + tb.L + cbits);
-    if (!ensure<char>(d_sort_tmp_, need)) return SE3ICP_ERR_OUT_OF_MEMORY;
     std::vector<int32_t> host_n(nclouds_);
-    for (int c = 0; c < nclouds_; ++c) host_n[c] = h_clouds_[c].n;
+    int max_n = 0;
+    for (int c = 0; c < nclouds_; ++c) max_n = std::max(max_n, host_n[c] = h_clouds_[c].n);
+    const size_t need = tree_build_temp_bytes((int)ntot_, nclouds_, max_n, tb.L);
+    if (!ensure<char>(d_sort_tmp_, std::max<size_t>(need, 256))) return SE3ICP_ERR_OUT_OF_MEMORY;
     TreeView t{};
     t.host_n = host_n.data();
     t.D = D;
@@ -265,8 +264,7 @@ int Engine::build_tree(int D, const float* vec, hipStream_t s, const double* vec
     t.bhi = (uint32_t*)tb.bhi.p;
     t.lo = (float*)tb.lo.p;
     t.hi = (float*)tb.hi.p;
-    if (build_trees(t, d_sort_tmp_.p, d_sort_tmp_.bytes, (unsigned long long*)d_keys0_.p,
-                    (unsigned long long*)d_keys1_.p, (int32_t*)d_vals1_.p, s) != 0)
+    if (build_trees(t, d_sort_tmp_.p, d_sort_tmp_.bytes, (uint32_t*)d_keys0_.p, (int32_t*)d_vals1_.p, s) != 0)
         return SE3ICP_ERR_HIP;
     return 0;
 }

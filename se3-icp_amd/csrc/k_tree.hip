@@ -14,7 +14,6 @@
 // order (coalesced leaf loads) and f32 AABBs of all 2^(L+1)-1 nodes (heap order),
 // inflated by a few ulps so the f32 boxes bound the f64 points they stand for.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include "tree.hpp"
 #include "wave.hpp"
@@ -31,11 +30,12 @@ __device__ __forceinline__ float ord_float(uint32_t u) {
     return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
 }
 
-__global__ __launch_bounds__(256) void k_tree_init(TreeView t) {
+__global__ __launch_bounds__(256) void k_tree_init(TreeView t, int32_t* perm2) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g < t.npts) {
         const CloudDev cl = t.clouds[t.cloud_of[g]];
         t.perm[g] = g - cl.off;
+        perm2[g] = g - cl.off;  // (both buffers hold valid point indices at all times)
     }
     const size_t nb = (size_t)t.nclouds * t.nnodes * t.D;
     for (size_t i = g; i < nb; i += (size_t)gridDim.x * blockDim.x) {
@@ -95,55 +95,320 @@ __global__ __launch_bounds__(256) void k_tree_bbox(TreeView t, int level) {
     }
 }
 
-// widest dimension of every node of the level, then the sort keys:
-//   key = (cloud << L | node << (L - level)) << 32 | orderable(coordinate along that dim)
-__global__ __launch_bounds__(256) void k_tree_keys(TreeView t, int level, unsigned long long* keys, int32_t* vals) {
-    const int g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= t.npts) return;
+// ---- global levels: a stable median partition of every node of the level, all clouds at
+// once, in five passes over the level's points (no device-wide sort).
+//   hist    the coordinate along the node's widest (sampled) dimension, quantised to
+//           kPartBins bins of the node's extent -> per-block histograms in LDS (q kept per point)
+//   select  per node: its histogram from its blocks', the bin holding the median position, and how many of its points
+//           go left (the rest of that bin goes right; any partition at the median
+//           position is a valid tree: the boxes are computed exactly afterwards)
+//   hist2 / select2  the same inside the median bin with the key's fine bits (a 22-bit split)
+//   count   per block of kPartElems consecutive tree positions: the (left, tie) counts of
+//           the points after the block's last node start (segmented carries)
+//   scan    the carries across blocks (one workgroup)
+//   scatter each point's rank among its node's points of the same class -> its new position
+// Ties keep their tree order, so the build is deterministic.
+constexpr int kPartBits = 11, kPartBins = 1 << kPartBits;  // bins per pass; keys of 2 * kPartBits bits
+constexpr int kPartThreads = 256, kPartPer = 4, kPartElems = kPartThreads * kPartPer;
+constexpr int kSelThreads = 1024, kSelPer = kPartBins / kSelThreads;
+
+struct PartSel {
+    int32_t bin;   // the median bin
+    int32_t tie_left;  // its points that go left (in tree order)
+    int32_t tie_n;     // its points
+    int32_t pad;
+};
+
+// node ids (cloud << level | node) grow with the tree position
+__device__ __forceinline__ int part_node_id(int c, int level, int node) { return (c << level) + node; }
+__device__ __forceinline__ int part_node_id_at(const TreeView& t, int level, int g) {
     const int c = t.cloud_of[g];
     const CloudDev cl = t.clouds[c];
-    const int node = tree_node_of(g - cl.off, cl.n, level);
-    const size_t base = ((size_t)c * t.nnodes + tree_heap(level, node)) * t.D;
-    int best = 0;
-    float ext = -1.f;
-    for (int d = 0; d < t.D; ++d) {
-        const float e = ord_float(t.bhi[base + d]) - ord_float(t.blo[base + d]);
-        if (e > ext) { ext = e; best = d; }
-    }
-    const int p = t.perm[g];
-    const uint32_t u = ord_bits(t.vec[tree_in_ix(t, best, cl.off + p)]);
-    const unsigned long long hiw = ((unsigned long long)c << t.L) | ((unsigned long long)node << (t.L - level));
-    keys[g] = (hiw << 32) | u;
-    vals[g] = p;
+    return part_node_id(c, level, tree_node_of(g - cl.off, cl.n, level));
 }
 
-// 32-bit variant: key = ((cloud << level) | node) << qbits | q, with q the coordinate
-// quantised to qbits over the node's (sampled) extent.  Any partition at the median
-// position yields a valid tree -- the boxes are computed exactly afterwards -- so ties
-// from the quantisation only cost split quality, and the sort needs 3-4 digit passes
-// of 4-byte keys instead of 5-6 of 8-byte keys.
-__global__ __launch_bounds__(256) void k_tree_keys32(TreeView t, int level, int qbits, uint32_t* keys, int32_t* vals) {
+// Per block of kPartElems tree positions: the histograms of the (at most) two nodes the
+// block starts in, in LDS, written out whole (dense[block][2][bins]); points of further
+// nodes (small clouds) go to the per-node overflow histograms by global atomics.
+__global__ __launch_bounds__(kPartThreads) void k_part_hist(TreeView t, int level, uint32_t* q_out, uint32_t* dense,
+                                                           int32_t* block_id0, uint32_t* overflow) {
+    __shared__ uint32_t s_h[2 * kPartBins];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 2 * kPartBins; i += kPartThreads) s_h[i] = 0u;
+    const int g0 = blockIdx.x * kPartElems;
+    const int id0 = part_node_id_at(t, level, g0);
+    if (tid == 0) block_id0[blockIdx.x] = id0;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kPartPer; ++u) {
+        const int g = g0 + u * kPartThreads + tid;
+        if (g < t.npts) {
+            const int c = t.cloud_of[g];
+            const CloudDev cl = t.clouds[c];
+            const int node = tree_node_of(g - cl.off, cl.n, level);
+            const size_t base = ((size_t)c * t.nnodes + tree_heap(level, node)) * t.D;
+            int best = 0;
+            float ext = -1.f, lo = 0.f;
+            for (int d = 0; d < t.D; ++d) {
+                const float l = ord_float(t.blo[base + d]);
+                const float e = ord_float(t.bhi[base + d]) - l;
+                if (e > ext) { ext = e; best = d; lo = l; }
+            }
+            const float x = t.vec[tree_in_ix(t, best, cl.off + t.perm[g])];
+            const float qmax = (float)((1 << (2 * kPartBits)) - 1);
+            float qf = (ext > 0.f && ext < INFINITY) ? (x - lo) * (qmax / ext) : 0.f;
+            qf = fminf(fmaxf(qf, 0.f), qmax);  // NaN -> 0
+            const uint32_t key = (uint32_t)qf;
+            q_out[g] = key;
+            const uint32_t q = key >> kPartBits;  // coarse bin
+            const int id = part_node_id(c, level, node), slot = id - id0;
+            if (slot < 2) atomicAdd(&s_h[slot * kPartBins + q], 1u);
+            else atomicAdd(&overflow[(size_t)id * kPartBins + q], 1u);
+        }
+    }
+    __syncthreads();
+    uint32_t* out = dense + (size_t)blockIdx.x * 2 * kPartBins;
+    for (int i = tid; i < 2 * kPartBins; i += kPartThreads) out[i] = s_h[i];
+}
+
+// one workgroup per node of the level: its histogram (the blocks' dense slots + overflow),
+// the median bin; the overflow histogram is cleared for the next level
+__global__ __launch_bounds__(kSelThreads) void k_part_select(TreeView t, int level, const uint32_t* dense,
+                                                            const int32_t* block_id0, uint32_t* overflow, PartSel* sel) {
+    __shared__ uint32_t s_sum[kSelThreads];
+    const int nl = 1 << level;
+    const int id = blockIdx.x;
+    const int c = id >> level, node = id & (nl - 1);
+    const CloudDev cl = t.clouds[c];
+    const int a = tree_first(cl.n, level, node), b = tree_first(cl.n, level, node + 1);
+    const int mL = tree_first(cl.n, level + 1, 2 * node + 1) - a;
+    const int tid = threadIdx.x;
+    uint32_t v[kSelPer];
+    uint32_t* ov = overflow + (size_t)id * kPartBins;
+#pragma unroll
+    for (int k = 0; k < kSelPer; ++k) {
+        v[k] = ov[tid * kSelPer + k];
+        ov[tid * kSelPer + k] = 0u;
+    }
+    if (b > a) {
+        const int kb0 = (cl.off + a) / kPartElems, kb1 = (cl.off + b - 1) / kPartElems;
+#pragma unroll 8
+        for (int kb = kb0; kb <= kb1; ++kb) {
+            const int slot = id - block_id0[kb];
+            if ((unsigned)slot < 2u) {
+                const uint32_t* h = dense + ((size_t)kb * 2 + slot) * kPartBins;
+#pragma unroll
+                for (int k = 0; k < kSelPer; ++k) v[k] += h[tid * kSelPer + k];
+            }
+        }
+    }
+    uint32_t tot = 0;
+#pragma unroll
+    for (int k = 0; k < kSelPer; ++k) tot += v[k];
+    s_sum[tid] = tot;
+    __syncthreads();
+    for (int o = 1; o < kSelThreads; o <<= 1) {  // inclusive scan of the threads' totals
+        const uint32_t add = tid >= o ? s_sum[tid - o] : 0u;
+        __syncthreads();
+        s_sum[tid] += add;
+        __syncthreads();
+    }
+    uint32_t cum = tid > 0 ? s_sum[tid - 1] : 0u;  // points in the bins before this thread's
+    // the first bin whose inclusive count reaches mL (bin 0 when mL = 0: everything goes right)
+#pragma unroll
+    for (int k = 0; k < kSelPer; ++k) {
+        const uint32_t nxt = cum + v[k];
+        if (((int)(cum < (uint32_t)mL) & (int)(nxt >= (uint32_t)mL)) | ((int)(mL == 0) & (int)(tid == 0) & (int)(k == 0))) {
+            PartSel r;
+            r.bin = tid * kSelPer + k;
+            r.tie_left = mL - (int)cum;
+            r.tie_n = (int)v[k];
+            r.pad = 0;
+            sel[id] = r;
+        }
+        cum = nxt;
+    }
+}
+
+// second pass inside the median bin: the fine bits of its points' keys
+__global__ __launch_bounds__(256) void k_part_hist2(TreeView t, int level, const uint32_t* key, const PartSel* sel,
+                                                   uint32_t* fine) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= t.npts) return;
+    const int id = part_node_id_at(t, level, g);
+    const uint32_t k = key[g];
+    if ((int)(k >> kPartBits) == sel[id].bin) atomicAdd(&fine[(size_t)id * kPartBins + (k & (kPartBins - 1))], 1u);
+}
+
+// the fine bin holding the median position; sel becomes the full-key threshold
+__global__ __launch_bounds__(256) void k_part_select2(TreeView t, uint32_t* fine, PartSel* sel) {
+    __shared__ uint32_t s_sum[256];
+    constexpr int kPer = kPartBins / 256;
+    const int id = blockIdx.x, tid = threadIdx.x;
+    const PartSel r = sel[id];
+    const int want = r.tie_left;  // points of the coarse bin that go left
+    uint32_t* h = fine + (size_t)id * kPartBins;
+    uint32_t v[kPer];
+    uint32_t tot = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        v[k] = h[tid * kPer + k];
+        h[tid * kPer + k] = 0u;
+        tot += v[k];
+    }
+    s_sum[tid] = tot;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {
+        const uint32_t add = tid >= o ? s_sum[tid - o] : 0u;
+        __syncthreads();
+        s_sum[tid] += add;
+        __syncthreads();
+    }
+    uint32_t cum = tid > 0 ? s_sum[tid - 1] : 0u;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const uint32_t nxt = cum + v[k];
+        if (((int)(cum < (uint32_t)want) & (int)(nxt >= (uint32_t)want)) | ((int)(want == 0) & (int)(tid == 0) & (int)(k == 0))) {
+            PartSel o;
+            o.bin = (r.bin << kPartBits) | (tid * kPer + k);
+            o.tie_left = want - (int)cum;
+            o.tie_n = (int)v[k];
+            o.pad = 0;
+            sel[id] = o;
+        }
+        cum = nxt;
+    }
+}
+
+// (flag, packed counts) segmented sums: flag = a node starts in the span; counts = points
+// of class left (low 32 bits) and tie (high 32 bits) since the span's last node start
+struct SegCnt {
+    unsigned long long v;
+    int f;
+};
+__device__ __forceinline__ SegCnt seg_add(SegCnt a, SegCnt b) { return SegCnt{b.f ? b.v : a.v + b.v, a.f | b.f}; }
+
+__device__ __forceinline__ SegCnt part_class(const TreeView& t, int level, const uint32_t* q, const PartSel* sel, int g,
+                                             int* cls, int* node_out, int* c_out) {
     const int c = t.cloud_of[g];
     const CloudDev cl = t.clouds[c];
-    const int node = tree_node_of(g - cl.off, cl.n, level);
-    const size_t base = ((size_t)c * t.nnodes + tree_heap(level, node)) * t.D;
-    int best = 0;
-    float ext = -1.f, lo = 0.f;
-    for (int d = 0; d < t.D; ++d) {
-        const float l = ord_float(t.blo[base + d]);
-        const float e = ord_float(t.bhi[base + d]) - l;
-        if (e > ext) { ext = e; best = d; lo = l; }
+    const int x = g - cl.off;
+    const int node = tree_node_of(x, cl.n, level);
+    const PartSel r = sel[part_node_id(c, level, node)];
+    const int qq = (int)q[g];  // (full key against the full-key threshold)
+    const int k = qq < r.bin ? 0 : (qq == r.bin ? 1 : 2);
+    *cls = k;
+    *node_out = node;
+    *c_out = c;
+    return SegCnt{k == 0 ? 1ull : (k == 1 ? (1ull << 32) : 0ull), x == tree_first(cl.n, level, node) ? 1 : 0};
+}
+
+// block-wide segmented scan of one SegCnt per thread (256 threads): the inclusive value
+// and the exclusive one (what precedes the thread in the block)
+__device__ __forceinline__ SegCnt block_seg_scan(SegCnt x, SegCnt* s_wave, SegCnt* excl) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        SegCnt y;
+        y.v = __shfl_up(x.v, o, 64);
+        y.f = __shfl_up(x.f, o, 64);
+        if (lane >= o) x = seg_add(y, x);
     }
-    const int p = t.perm[g];
-    const float x = t.vec[tree_in_ix(t, best, cl.off + p)];
-    const float qmax = (float)((1u << qbits) - 1u);
-    float qf = (ext > 0.f && ext < INFINITY) ? (x - lo) * (qmax / ext) : 0.f;
-    qf = fminf(fmaxf(qf, 0.f), qmax);  // NaN -> 0
-    const uint32_t q = (uint32_t)qf;
-    keys[g] = ((((uint32_t)c << level) | (uint32_t)node) << qbits) | q;
-    vals[g] = p;
+    SegCnt ex;
+    ex.v = __shfl_up(x.v, 1, 64);
+    ex.f = __shfl_up(x.f, 1, 64);
+    if (lane == 0) ex = SegCnt{0ull, 0};
+    if (lane == 63) s_wave[wv] = x;
+    __syncthreads();
+    SegCnt pre{0ull, 0};
+    for (int w = 0; w < wv; ++w) pre = seg_add(pre, s_wave[w]);
+    __syncthreads();
+    *excl = seg_add(pre, ex);
+    return seg_add(pre, x);
+}
+
+__global__ __launch_bounds__(kPartThreads) void k_part_count(TreeView t, int level, const uint32_t* q, const PartSel* sel,
+                                                            SegCnt* tails) {
+    __shared__ SegCnt s_wave[kPartThreads / 64];
+    const int g0 = blockIdx.x * kPartElems + threadIdx.x * kPartPer;
+    SegCnt acc{0ull, 0};
+#pragma unroll
+    for (int u = 0; u < kPartPer; ++u) {
+        const int g = g0 + u;
+        if (g < t.npts) {
+            int k, node, c;
+            acc = seg_add(acc, part_class(t, level, q, sel, g, &k, &node, &c));
+        }
+    }
+    SegCnt ex;
+    const SegCnt inc = block_seg_scan(acc, s_wave, &ex);
+    if (threadIdx.x == kPartThreads - 1) tails[blockIdx.x] = inc;
+}
+
+// exclusive segmented scan of the blocks' tails: carry[k] = the counts entering block k
+__global__ __launch_bounds__(1024) void k_part_scan(const SegCnt* tails, int nblk, SegCnt* carry) {
+    __shared__ SegCnt s_t[1024];
+    const int tid = threadIdx.x;
+    const int per = (nblk + 1023) / 1024;
+    const int k0 = tid * per, k1 = min(nblk, k0 + per);
+    SegCnt acc{0ull, 0};
+    for (int k = k0; k < k1; ++k) acc = seg_add(acc, tails[k]);
+    s_t[tid] = acc;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const SegCnt y = tid >= o ? s_t[tid - o] : SegCnt{0ull, 0};
+        __syncthreads();
+        if (tid >= o) s_t[tid] = seg_add(y, s_t[tid]);
+        __syncthreads();
+    }
+    SegCnt run = tid > 0 ? s_t[tid - 1] : SegCnt{0ull, 0};
+    for (int k = k0; k < k1; ++k) {
+        carry[k] = run;
+        run = seg_add(run, tails[k]);
+    }
+}
+
+__global__ __launch_bounds__(kPartThreads) void k_part_scatter(TreeView t, int level, const uint32_t* q, const PartSel* sel,
+                                                              const SegCnt* carry, int32_t* perm_out) {
+    __shared__ SegCnt s_wave[kPartThreads / 64];
+    const int g0 = blockIdx.x * kPartElems + threadIdx.x * kPartPer;
+    SegCnt self[kPartPer];
+    int cls[kPartPer], nodes[kPartPer], cs[kPartPer];
+    SegCnt acc{0ull, 0};
+#pragma unroll
+    for (int u = 0; u < kPartPer; ++u) {
+        const int g = g0 + u;
+        self[u] = SegCnt{0ull, 0};
+        cls[u] = 2;
+        nodes[u] = 0;
+        cs[u] = 0;
+        if (g < t.npts) self[u] = part_class(t, level, q, sel, g, &cls[u], &nodes[u], &cs[u]);
+        acc = seg_add(acc, self[u]);
+    }
+    SegCnt ex;
+    (void)block_seg_scan(acc, s_wave, &ex);
+    // the counts of this thread's node before its first point: the block's carry, then the
+    // threads before it in the block
+    SegCnt run = seg_add(carry[blockIdx.x], ex);
+#pragma unroll
+    for (int u = 0; u < kPartPer; ++u) {
+        const int g = g0 + u;
+        if (self[u].f) run = SegCnt{0ull, 0};
+        if (g < t.npts) {
+            const CloudDev cl = t.clouds[cs[u]];
+            const int a = tree_first(cl.n, level, nodes[u]);
+            const int mL = tree_first(cl.n, level + 1, 2 * nodes[u] + 1) - a;
+            const PartSel r = sel[part_node_id(cs[u], level, nodes[u])];
+            const int r0 = (int)(unsigned)run.v, r1 = (int)(unsigned)(run.v >> 32);
+            const int x = g - cl.off;
+            int dst;
+            if (cls[u] == 0) dst = a + r0;
+            else if (cls[u] == 1) dst = r1 < r.tie_left ? a + (mL - r.tie_left) + r1 : a + mL + (r1 - r.tie_left);
+            else dst = a + mL + (r.tie_n - r.tie_left) + ((x - a) - r0 - r1);
+            if ((unsigned)dst < (unsigned)cl.n) perm_out[cl.off + dst] = t.perm[g];  // (always, by construction)
+        }
+        run = seg_add(run, SegCnt{self[u].v, 0});
+    }
 }
 
 // The levels below G in one workgroup per level-G node (<= kLocalMax points): the node's
@@ -408,45 +673,91 @@ __global__ __launch_bounds__(1024) void k_tree_up(TreeView t) {
 
 }  // namespace
 
-int build_trees(TreeView t, void* sort_tmp, size_t sort_tmp_bytes, unsigned long long* keys0,
-                unsigned long long* keys1, int32_t* vals1, hipStream_t s) {
+int tree_global_levels(int max_n, int L) {
+    int G = 0;  // global levels until every node fits one workgroup's LDS sort (and <= 128 sub-nodes below)
+    while (G < L && (((long long)max_n + (1ll << G) - 1) >> G) > kLocalMax) ++G;
+    if (L - 1 - G > 7) G = L - 8;
+    return G;
+}
+
+namespace {
+struct PartScratch {
+    uint32_t* dense;
+    int32_t* block_id0;
+    uint32_t* overflow;
+    PartSel* sel;
+    SegCnt* tails;
+    SegCnt* carry;
+    size_t overflow_words;
+};
+size_t part_layout(int npts, int nclouds, int G, char* base, PartScratch* ps) {
+    const size_t nodes = G > 0 ? (size_t)nclouds << (G - 1) : 0;
+    const size_t nblk = ((size_t)npts + kPartElems - 1) / kPartElems;
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        const size_t at = off;
+        off += (bytes + 255) & ~(size_t)255;
+        return base ? base + at : nullptr;
+    };
+    char* dn = take(G > 0 ? nblk * 2 * kPartBins * sizeof(uint32_t) : 0);
+    char* b0 = take(nblk * sizeof(int32_t));
+    char* ov = take(nodes * kPartBins * sizeof(uint32_t));
+    char* sl = take(nodes * sizeof(PartSel));
+    char* tl = take(nblk * sizeof(SegCnt));
+    char* cr = take(nblk * sizeof(SegCnt));
+    if (ps) {
+        ps->dense = (uint32_t*)dn;
+        ps->block_id0 = (int32_t*)b0;
+        ps->overflow = (uint32_t*)ov;
+        ps->sel = (PartSel*)sl;
+        ps->tails = (SegCnt*)tl;
+        ps->carry = (SegCnt*)cr;
+        ps->overflow_words = nodes * kPartBins;
+    }
+    return off;
+}
+
+__global__ __launch_bounds__(256) void k_clear_words(uint32_t* p, size_t n) {
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = 0u;
+}
+}  // namespace
+
+int build_trees(TreeView t, void* tmp, size_t tmp_bytes, uint32_t* qbuf, int32_t* perm_alt, hipStream_t s) {
     const int nb = (t.npts + 255) / 256;
     const int nbs = (t.npts + 256 * kSplitSample - 1) / (256 * kSplitSample);
     const int gfill = std::max(nb, 64);
     auto bbox = (t.D == 12) ? k_tree_bbox<12> : k_tree_bbox<3>;
-    hipLaunchKernelGGL(k_tree_init, dim3(gfill), dim3(256), 0, s, t);
-    int cbits = 0;
-    while ((1 << cbits) < t.nclouds) ++cbits;
-    const int end_bit = 32 + t.L + cbits;
-    // global levels until every node fits one workgroup's LDS sort (and <= 128 sub-nodes below)
     int max_n = 0;
-    for (int c = 0; c < t.nclouds; ++c) max_n = std::max(max_n, t.host_n ? t.host_n[c] : 0);
-    int G = 0;
-    while (G < t.L && (((long long)max_n + (1ll << G) - 1) >> G) > kLocalMax) ++G;
-    if (t.L - 1 - G > 7) G = t.L - 8;
-    if (!t.host_n) G = t.L;
+    for (int c = 0; c < t.nclouds; ++c) max_n = std::max(max_n, t.host_n[c]);
+    const int G = tree_global_levels(max_n, t.L);
+    PartScratch ps;
+    if (part_layout(t.npts, t.nclouds, G, (char*)tmp, &ps) > tmp_bytes) return -1;
+    // the level scatters alternate between the two permutation buffers: start in the one
+    // that makes the last global level land in t.perm
+    int32_t* const final_perm = t.perm;
+    TreeView tc = t;
+    tc.perm = (G % 2 == 0) ? final_perm : perm_alt;
+    int32_t* other = (G % 2 == 0) ? perm_alt : final_perm;
+    hipLaunchKernelGGL(k_tree_init, dim3(gfill), dim3(256), 0, s, tc, other);
+    if (ps.overflow_words) hipLaunchKernelGGL(k_clear_words, dim3(256), dim3(256), 0, s, ps.overflow, ps.overflow_words);
+    const int nblk = (t.npts + kPartElems - 1) / kPartElems;
     for (int l = 0; l < G; ++l) {
-        hipLaunchKernelGGL(bbox, dim3(nbs), dim3(256), 0, s, t, l);
-        // 24-bit keys (3 passes) while >= 8 quantisation bits remain, then 32-bit keys,
-        // then the exact 64-bit keys (very large batches only)
-        const int q24 = 24 - cbits - l, q32 = 32 - cbits - l;
-        size_t bytes = sort_tmp_bytes;
-        if (q24 >= 8 || q32 >= 8) {
-            const int qb = q24 >= 8 ? q24 : q32;
-            const int eb = q24 >= 8 ? 24 : 32;
-            uint32_t* k0 = reinterpret_cast<uint32_t*>(keys0);
-            uint32_t* k1 = reinterpret_cast<uint32_t*>(keys1);
-            hipLaunchKernelGGL(k_tree_keys32, dim3(nb), dim3(256), 0, s, t, l, qb, k0, vals1);
-            if (hipcub::DeviceRadixSort::SortPairs(sort_tmp, bytes, k0, k1, vals1, t.perm, t.npts, 0, eb, s) !=
-                hipSuccess)
-                return -1;
-        } else {
-            hipLaunchKernelGGL(k_tree_keys, dim3(nb), dim3(256), 0, s, t, l, keys0, vals1);
-            if (hipcub::DeviceRadixSort::SortPairs(sort_tmp, bytes, keys0, keys1, vals1, t.perm, t.npts, 0, end_bit,
-                                                   s) != hipSuccess)
-                return -1;
-        }
+        hipLaunchKernelGGL(bbox, dim3(nbs), dim3(256), 0, s, tc, l);
+        hipLaunchKernelGGL(k_part_hist, dim3(nblk), dim3(kPartThreads), 0, s, tc, l, qbuf, ps.dense, ps.block_id0,
+                           ps.overflow);
+        hipLaunchKernelGGL(k_part_select, dim3(t.nclouds << l), dim3(kSelThreads), 0, s, tc, l, (const uint32_t*)ps.dense,
+                           (const int32_t*)ps.block_id0, ps.overflow, ps.sel);
+        hipLaunchKernelGGL(k_part_hist2, dim3(nb), dim3(256), 0, s, tc, l, (const uint32_t*)qbuf, (const PartSel*)ps.sel,
+                           ps.overflow);
+        hipLaunchKernelGGL(k_part_select2, dim3(t.nclouds << l), dim3(256), 0, s, tc, ps.overflow, ps.sel);
+        hipLaunchKernelGGL(k_part_count, dim3(nblk), dim3(kPartThreads), 0, s, tc, l, (const uint32_t*)qbuf,
+                           (const PartSel*)ps.sel, ps.tails);
+        hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, s, (const SegCnt*)ps.tails, nblk, ps.carry);
+        hipLaunchKernelGGL(k_part_scatter, dim3(nblk), dim3(kPartThreads), 0, s, tc, l, (const uint32_t*)qbuf,
+                           (const PartSel*)ps.sel, (const SegCnt*)ps.carry, other);
+        std::swap(tc.perm, other);
     }
+    t.perm = final_perm;
     if (G < t.L)
         hipLaunchKernelGGL(t.D == 12 ? k_tree_local<12> : k_tree_local<3>, dim3(t.nclouds << G), dim3(kLocalThreads), 0,
                            s, t, G);
@@ -457,13 +768,8 @@ int build_trees(TreeView t, void* sort_tmp, size_t sort_tmp_bytes, unsigned long
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-size_t tree_sort_temp_bytes(int npts, int end_bit) {
-    size_t b64 = 0, b32 = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b64, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
-                                             (int32_t*)nullptr, (int32_t*)nullptr, npts, 0, end_bit, (hipStream_t)0);
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, b32, (uint32_t*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr,
-                                             (int32_t*)nullptr, npts, 0, 32, (hipStream_t)0);
-    return std::max(b64, b32);
+size_t tree_build_temp_bytes(int npts, int nclouds, int max_n, int L) {
+    return part_layout(npts, nclouds, tree_global_levels(max_n, L), nullptr, nullptr);
 }
 
 }  // namespace se3icp

@@ -59,8 +59,9 @@ inline int tree_depth_for(int max_n) {
     return L;
 }
 
-int build_trees(TreeView t, void* sort_tmp, size_t sort_tmp_bytes, unsigned long long* keys0,
-                unsigned long long* keys1, int32_t* vals1, hipStream_t s);
-size_t tree_sort_temp_bytes(int npts, int end_bit);
+// qbuf: [npts] u32 scratch, perm_alt: [npts] the second permutation buffer of the global levels
+int build_trees(TreeView t, void* tmp, size_t tmp_bytes, uint32_t* qbuf, int32_t* perm_alt, hipStream_t s);
+size_t tree_build_temp_bytes(int npts, int nclouds, int max_n, int L);
+int tree_global_levels(int max_n, int L);
 
 }  // namespace se3icp
