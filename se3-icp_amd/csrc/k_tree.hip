@@ -111,6 +111,7 @@ __global__ __launch_bounds__(256) void k_tree_bbox(TreeView t, int level) {
 constexpr int kPartBits = 11, kPartBins = 1 << kPartBits;  // bins per pass; keys of 2 * kPartBits bits
 constexpr int kPartThreads = 256, kPartPer = 4, kPartElems = kPartThreads * kPartPer;
 constexpr int kSelThreads = 1024, kSelPer = kPartBins / kSelThreads;
+constexpr int kHistPer = 8, kHistElems = kPartThreads * kHistPer;  // tree positions per histogram block
 
 struct PartSel {
     int32_t bin;   // the median bin
@@ -118,6 +119,40 @@ struct PartSel {
     int32_t tie_n;     // its points
     int32_t pad;
 };
+
+// split of a node: its widest dimension and the quantisation of that coordinate
+struct PartDim {
+    int32_t best;
+    float lo, scale;  // key = (x - lo) * scale, clamped to [0, 2^(2 kPartBits) - 1]
+    int32_t pad;
+};
+constexpr float kKeyMax = (float)((1 << (2 * kPartBits)) - 1);
+
+// widest dimension of a box given as orderable bits (blo/bhi)
+__device__ __forceinline__ PartDim part_dim_of(const uint32_t* blo, const uint32_t* bhi, int D) {
+    int best = 0;
+    float ext = -1.f, lo = 0.f;
+    for (int d = 0; d < D; ++d) {
+        const float l = ord_float(blo[d]);
+        const float e = ord_float(bhi[d]) - l;
+        if (e > ext) { ext = e; best = d; lo = l; }
+    }
+    PartDim r;
+    r.best = best;
+    r.lo = lo;
+    r.scale = (ext > 0.f && ext < INFINITY) ? kKeyMax / ext : 0.f;
+    r.pad = 0;
+    return r;
+}
+
+// every node's split from its sampled box (k_tree_bbox); once per node, not per point
+__global__ __launch_bounds__(64) void k_part_dims(TreeView t, int level, PartDim* dims) {
+    const int id = blockIdx.x * 64 + threadIdx.x;
+    if (id >= (t.nclouds << level)) return;
+    const int c = id >> level, node = id & ((1 << level) - 1);
+    const size_t base = ((size_t)c * t.nnodes + tree_heap(level, node)) * t.D;
+    dims[id] = part_dim_of(t.blo + base, t.bhi + base, t.D);
+}
 
 // node ids (cloud << level | node) grow with the tree position
 __device__ __forceinline__ int part_node_id(int c, int level, int node) { return (c << level) + node; }
@@ -127,41 +162,33 @@ __device__ __forceinline__ int part_node_id_at(const TreeView& t, int level, int
     return part_node_id(c, level, tree_node_of(g - cl.off, cl.n, level));
 }
 
-// Per block of kPartElems tree positions: the histograms of the (at most) two nodes the
+// Per block of kHistElems tree positions: the histograms of the (at most) two nodes the
 // block starts in, in LDS, written out whole (dense[block][2][bins]); points of further
 // nodes (small clouds) go to the per-node overflow histograms by global atomics.
-__global__ __launch_bounds__(kPartThreads) void k_part_hist(TreeView t, int level, uint32_t* q_out, uint32_t* dense,
-                                                           int32_t* block_id0, uint32_t* overflow) {
+__global__ __launch_bounds__(kPartThreads) void k_part_hist(TreeView t, int level, const PartDim* dims, uint32_t* q_out,
+                                                           uint32_t* dense, int32_t* block_id0, uint32_t* overflow) {
     __shared__ uint32_t s_h[2 * kPartBins];
     const int tid = threadIdx.x;
     for (int i = tid; i < 2 * kPartBins; i += kPartThreads) s_h[i] = 0u;
-    const int g0 = blockIdx.x * kPartElems;
+    const int g0 = blockIdx.x * kHistElems;
     const int id0 = part_node_id_at(t, level, g0);
     if (tid == 0) block_id0[blockIdx.x] = id0;
     __syncthreads();
-#pragma unroll
-    for (int u = 0; u < kPartPer; ++u) {
+#pragma unroll 4
+    for (int u = 0; u < kHistPer; ++u) {
         const int g = g0 + u * kPartThreads + tid;
         if (g < t.npts) {
             const int c = t.cloud_of[g];
             const CloudDev cl = t.clouds[c];
             const int node = tree_node_of(g - cl.off, cl.n, level);
-            const size_t base = ((size_t)c * t.nnodes + tree_heap(level, node)) * t.D;
-            int best = 0;
-            float ext = -1.f, lo = 0.f;
-            for (int d = 0; d < t.D; ++d) {
-                const float l = ord_float(t.blo[base + d]);
-                const float e = ord_float(t.bhi[base + d]) - l;
-                if (e > ext) { ext = e; best = d; lo = l; }
-            }
-            const float x = t.vec[tree_in_ix(t, best, cl.off + t.perm[g])];
-            const float qmax = (float)((1 << (2 * kPartBits)) - 1);
-            float qf = (ext > 0.f && ext < INFINITY) ? (x - lo) * (qmax / ext) : 0.f;
-            qf = fminf(fmaxf(qf, 0.f), qmax);  // NaN -> 0
+            const int id = part_node_id(c, level, node), slot = id - id0;
+            const PartDim pd = dims[id];
+            const float x = t.vec[tree_in_ix(t, pd.best, cl.off + t.perm[g])];
+            float qf = (x - pd.lo) * pd.scale;
+            qf = fminf(fmaxf(qf, 0.f), kKeyMax);  // NaN -> 0
             const uint32_t key = (uint32_t)qf;
             q_out[g] = key;
             const uint32_t q = key >> kPartBits;  // coarse bin
-            const int id = part_node_id(c, level, node), slot = id - id0;
             if (slot < 2) atomicAdd(&s_h[slot * kPartBins + q], 1u);
             else atomicAdd(&overflow[(size_t)id * kPartBins + q], 1u);
         }
@@ -191,7 +218,7 @@ __global__ __launch_bounds__(kSelThreads) void k_part_select(TreeView t, int lev
         ov[tid * kSelPer + k] = 0u;
     }
     if (b > a) {
-        const int kb0 = (cl.off + a) / kPartElems, kb1 = (cl.off + b - 1) / kPartElems;
+        const int kb0 = (cl.off + a) / kHistElems, kb1 = (cl.off + b - 1) / kHistElems;
 #pragma unroll 8
         for (int kb = kb0; kb <= kb1; ++kb) {
             const int slot = id - block_id0[kb];
@@ -241,7 +268,7 @@ __global__ __launch_bounds__(256) void k_part_hist2(TreeView t, int level, const
 }
 
 // the fine bin holding the median position; sel becomes the full-key threshold
-__global__ __launch_bounds__(256) void k_part_select2(TreeView t, uint32_t* fine, PartSel* sel) {
+__global__ __launch_bounds__(256) void k_part_select2(uint32_t* fine, PartSel* sel) {
     __shared__ uint32_t s_sum[256];
     constexpr int kPer = kPartBins / 256;
     const int id = blockIdx.x, tid = threadIdx.x;
@@ -686,6 +713,7 @@ struct PartScratch {
     int32_t* block_id0;
     uint32_t* overflow;
     PartSel* sel;
+    PartDim* dims[1];
     SegCnt* tails;
     SegCnt* carry;
     size_t overflow_words;
@@ -693,16 +721,18 @@ struct PartScratch {
 size_t part_layout(int npts, int nclouds, int G, char* base, PartScratch* ps) {
     const size_t nodes = G > 0 ? (size_t)nclouds << (G - 1) : 0;
     const size_t nblk = ((size_t)npts + kPartElems - 1) / kPartElems;
+    const size_t nhist = ((size_t)npts + kHistElems - 1) / kHistElems;
     size_t off = 0;
     auto take = [&](size_t bytes) {
         const size_t at = off;
         off += (bytes + 255) & ~(size_t)255;
         return base ? base + at : nullptr;
     };
-    char* dn = take(G > 0 ? nblk * 2 * kPartBins * sizeof(uint32_t) : 0);
-    char* b0 = take(nblk * sizeof(int32_t));
+    char* dn = take(G > 0 ? nhist * 2 * kPartBins * sizeof(uint32_t) : 0);
+    char* b0 = take(nhist * sizeof(int32_t));
     char* ov = take(nodes * kPartBins * sizeof(uint32_t));
     char* sl = take(nodes * sizeof(PartSel));
+    char* d0 = take(nodes * sizeof(PartDim));
     char* tl = take(nblk * sizeof(SegCnt));
     char* cr = take(nblk * sizeof(SegCnt));
     if (ps) {
@@ -710,6 +740,7 @@ size_t part_layout(int npts, int nclouds, int G, char* base, PartScratch* ps) {
         ps->block_id0 = (int32_t*)b0;
         ps->overflow = (uint32_t*)ov;
         ps->sel = (PartSel*)sl;
+        ps->dims[0] = (PartDim*)d0;
         ps->tails = (SegCnt*)tl;
         ps->carry = (SegCnt*)cr;
         ps->overflow_words = nodes * kPartBins;
@@ -741,15 +772,20 @@ int build_trees(TreeView t, void* tmp, size_t tmp_bytes, uint32_t* qbuf, int32_t
     hipLaunchKernelGGL(k_tree_init, dim3(gfill), dim3(256), 0, s, tc, other);
     if (ps.overflow_words) hipLaunchKernelGGL(k_clear_words, dim3(256), dim3(256), 0, s, ps.overflow, ps.overflow_words);
     const int nblk = (t.npts + kPartElems - 1) / kPartElems;
+    const int nhist = (t.npts + kHistElems - 1) / kHistElems;
     for (int l = 0; l < G; ++l) {
+        PartDim* dims = ps.dims[0];
+        // (the split dimension from every kSplitSample-th point's box: estimating the
+        // children's boxes from the parent's cut was measured to give slower searches)
         hipLaunchKernelGGL(bbox, dim3(nbs), dim3(256), 0, s, tc, l);
-        hipLaunchKernelGGL(k_part_hist, dim3(nblk), dim3(kPartThreads), 0, s, tc, l, qbuf, ps.dense, ps.block_id0,
+        hipLaunchKernelGGL(k_part_dims, dim3(((t.nclouds << l) + 63) / 64), dim3(64), 0, s, tc, l, dims);
+        hipLaunchKernelGGL(k_part_hist, dim3(nhist), dim3(kPartThreads), 0, s, tc, l, dims, qbuf, ps.dense, ps.block_id0,
                            ps.overflow);
         hipLaunchKernelGGL(k_part_select, dim3(t.nclouds << l), dim3(kSelThreads), 0, s, tc, l, (const uint32_t*)ps.dense,
                            (const int32_t*)ps.block_id0, ps.overflow, ps.sel);
         hipLaunchKernelGGL(k_part_hist2, dim3(nb), dim3(256), 0, s, tc, l, (const uint32_t*)qbuf, (const PartSel*)ps.sel,
                            ps.overflow);
-        hipLaunchKernelGGL(k_part_select2, dim3(t.nclouds << l), dim3(256), 0, s, tc, ps.overflow, ps.sel);
+        hipLaunchKernelGGL(k_part_select2, dim3(t.nclouds << l), dim3(256), 0, s, ps.overflow, ps.sel);
         hipLaunchKernelGGL(k_part_count, dim3(nblk), dim3(kPartThreads), 0, s, tc, l, (const uint32_t*)qbuf,
                            (const PartSel*)ps.sel, ps.tails);
         hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, s, (const SegCnt*)ps.tails, nblk, ps.carry);
