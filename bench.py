@@ -315,12 +315,16 @@ def lrf_roofline(ktot, kms, steps, k):
     q = ktot.get("lrf_queries", 0.0) / steps
     bpp = 24.0 * k
     achieved = q * bpp / (t_ms / 1000.0) / 1e9 if t_ms > 0 else 0.0
-    traffic, src = pmc_traffic("k_lrf")
+    t8, src = pmc_traffic("k_lrf8")
+    tx, _ = pmc_traffic("k_lrf(")  # the exact kernel over the hand-over list
+    traffic = (t8 + tx) if (t8 is not None and tx is not None) else t8
     return {
-        "kernel": "k_lrf",
+        "kernel": "k_lrf8 + k_lrf (hand-overs)",
         "bound": "hbm",
-        "note": "fused exact kNN-k (f64) + TOLDI frame + normals/GICP covariance per point; algorithmic bytes = "
-                "k neighbour gathers x 24 B per point (SURVEY.md §8d); the kernel is VALU-issue bound (DESIGN.md §5)",
+        "note": "fused exact kNN-k (f64) + TOLDI frame + normals/GICP covariance per point: k_lrf8 (eight queries "
+                "per wavefront) and the exact one-query-per-wavefront k_lrf for the points it hands over, one HIP-event "
+                "bracket; algorithmic bytes = k neighbour gathers x 24 B per point (SURVEY.md §8d); the kernels are "
+                "issue / latency bound, not HBM bound (DESIGN.md §5)",
         "achieved": round(achieved, 2),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
