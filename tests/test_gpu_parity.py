@@ -96,25 +96,81 @@ def test_knn_self_matches_oracle(se3icp_mod, refcpu, fixture_clouds):
     assert (np.diff(d, axis=1) >= -1e-15).all()
 
 
-def test_toldi_frames_match_oracle(se3icp_mod, refcpu, fixture_clouds):
-    src, _ = fixture_clouds
-    g = se3icp_mod.toldi_frames(src, 90)
-    r = refcpu.toldi_frames(src, 90)
+def _eig_gap(cov):
+    """Relative gap between the two smallest eigenvalues of symmetric 3x3 matrices."""
+    w = np.linalg.eigvalsh(cov)
+    return (w[:, 1] - w[:, 0]) / np.maximum(np.abs(w[:, 2]), 1e-300)
+
+
+def _toldi_cov(pts, idx):
+    """ISR.cpp:259-272 restated: centroid of ranks 1 .. k/3-1 divided by k/3, covariance
+    over ranks 1 .. k/3 about it."""
+    rz = idx.shape[1] // 3
+    c = pts[idx[:, 1:rz]].sum(axis=1) / rz
+    v = pts[idx[:, 1:rz + 1]] - c[:, None, :]
+    return np.einsum("nki,nkj->nij", v, v)
+
+
+def _stage_cloud(kind, fixture_clouds):
+    if kind == "fixture":
+        return fixture_clouds[0]
+    from se3icp import datasets
+    pairs, _ = datasets.kitti_like_pairs(1, seed=4, first=2, total_pairs=8)  # ~120k points
+    return pairs[0][0]
+
+
+@pytest.mark.parametrize("kind", ["fixture", "kitti"])
+def test_toldi_frames_match_oracle(se3icp_mod, refcpu, fixture_clouds, kind):
+    """Frames agree to 1e-8 except where the frame is ill-conditioned, and every
+    disagreement must be one: a near-degenerate smallest eigenvalue of the TOLDI
+    covariance (the z axis, ISR.cpp:275-281) or a near-zero projected x axis
+    (ISR.cpp:302-303, normalised without a guard)."""
+    src = _stage_cloud(kind, fixture_clouds)
+    k = 90
+    g = se3icp_mod.toldi_frames(src, k)
+    r = refcpu.toldi_frames(src, k)
     diff = np.abs(g - r).reshape(len(src), -1).max(axis=1)
-    # frames are smooth functions of the neighbourhoods except where the covariance has a
-    # (near-)degenerate smallest eigenvalue; require 99.9 % agreement at 1e-8
-    assert np.mean(diff <= 1e-8) >= 0.999, np.sort(diff)[-10:]
+    bad = np.nonzero(diff > 1e-8)[0]
+    assert len(bad) <= 0.001 * len(src), np.sort(diff)[-10:]
+    if len(bad):
+        idx, _ = refcpu.knn_self(src, k)
+        gap = _eig_gap(_toldi_cov(src, idx[bad]))
+        # x axis before normalisation: sum of weighted neighbour vectors minus its z part
+        z = r[bad, :3, 2]
+        v = src[idx[bad, 1:]] - src[bad, None, :]
+        R = np.linalg.norm(src[idx[bad, -1]] - src[bad], axis=1)
+        w = (R[:, None] - np.linalg.norm(v, axis=2)) ** 2 * np.einsum("nki,ni->nk", v, z) ** 2
+        acc = np.einsum("nk,nki->ni", w, v)
+        xr = np.linalg.norm(acc - np.einsum("ni,ni->n", acc, z)[:, None] * z, axis=1)
+        xr = xr / np.maximum(np.linalg.norm(acc, axis=1), 1e-300)
+        ill = (gap < 1e-6) | (xr < 1e-6)
+        print(f"[toldi] {len(bad)} of {len(src)} frames differ > 1e-8: eigen-gaps {np.round(gap[:8], 9)}, "
+              f"x-axis ratios {np.round(xr[:8], 9)}")
+        assert ill.all(), (bad[~ill], diff[bad[~ill]], gap[~ill], xr[~ill])
     R = g[:, :3, :3]
     np.testing.assert_allclose(np.einsum("nij,nik->njk", R, R), np.broadcast_to(np.eye(3), R.shape), atol=1e-9)
 
 
-def test_estimate_normals_match_oracle(se3icp_mod, refcpu, fixture_clouds):
-    src, _ = fixture_clouds
-    g = se3icp_mod.estimate_normals(src, 30)
-    r = refcpu.estimate_normals(src, 30)
-    # sign included: FastEigen3x3 is deterministic given the covariance
+@pytest.mark.parametrize("kind", ["fixture", "kitti"])
+def test_estimate_normals_match_oracle(se3icp_mod, refcpu, fixture_clouds, kind):
+    """Normals (sign included: FastEigen3x3 is deterministic given the covariance) agree
+    to 1e-8 except at near-degenerate covariances (Open3D's cumulant covariance of the 30
+    nearest points, ISR.cpp:643), and every disagreement must be one."""
+    src = _stage_cloud(kind, fixture_clouds)
+    k = 30
+    g = se3icp_mod.estimate_normals(src, k)
+    r = refcpu.estimate_normals(src, k)
     diff = np.abs(g - r).max(axis=1)
-    assert np.mean(diff <= 1e-8) >= 0.999
+    bad = np.nonzero(diff > 1e-8)[0]
+    assert len(bad) <= 0.001 * len(src)
+    if len(bad):
+        idx, _ = refcpu.knn_self(src, k)
+        p = src[idx[bad]]
+        mu = p.mean(axis=1)
+        cov = np.einsum("nki,nkj->nij", p, p) / k - np.einsum("ni,nj->nij", mu, mu)
+        gap = _eig_gap(cov)
+        print(f"[normals] {len(bad)} of {len(src)} normals differ > 1e-8: eigen-gaps {np.round(gap[:8], 9)}")
+        assert (gap < 1e-6).all(), (bad[gap >= 1e-6], diff[bad[gap >= 1e-6]], gap[gap >= 1e-6])
 
 
 def _se3_vectors(frames, alpha=3.0, beta=1.0):
