@@ -160,6 +160,12 @@ __device__ __forceinline__ void compact_sweep(const float4* tile, const float4* 
 #ifndef SE3ICP_NN_XCD
 #define SE3ICP_NN_XCD 0  // XCD-aware chunk -> block mapping of k_nn_prep / k_nn_group (A/B: 1 slower, pairs load XCDs unevenly)
 #endif
+#ifndef SE3ICP_NN_SINGLE_BLOCKS
+#define SE3ICP_NN_SINGLE_BLOCKS 4096  // grid of the one-query-per-wave kernels (4 waves per block, grid-strided)
+#endif
+#ifndef SE3ICP_NN_BIN
+#define SE3ICP_NN_BIN 0  // 1: k_nn_prep groups the searched queries by their previous match's target position (A/B: NN +22 %, prep +65 %)
+#endif
 #ifndef SE3ICP_NN_SPLIT
 #define SE3ICP_NN_SPLIT 1
 #endif
@@ -287,6 +293,9 @@ __global__ __launch_bounds__(1024) void k_nn_prep(View v) {
     __syncthreads();
     bool active = false;
     int x = 0, l = 0;
+#if SE3ICP_NN_BIN
+    unsigned tkey = 0xffffffffu;  // tree position of the previous match
+#endif
     if (phase != PHASE_IDLE) {
         const CloudDev cs = v.clouds[P->src], ct = v.clouds[P->tgt];
         const TreeRef TR = (phase == PHASE_SE3) ? v.t12 : v.t3;
@@ -300,6 +309,12 @@ __global__ __launch_bounds__(1024) void k_nn_prep(View v) {
                                           : !prep_settle<3>(v, TR, P, pair, ct, gx, g, 0.0);
             l = tree_node_of(x, cs.n, TR.GL) - (ci << (TR.GL - v.chunk_level));
             if (active) atomicAdd(&s_cnt[l], 1);
+#if SE3ICP_NN_BIN
+            if (active) {
+                const int prev = v.corr_idx[g];
+                tkey = (prev >= 0 && prev < ct.n) ? (unsigned)TR.pos[ct.off + prev] : 0x7fffffffu;
+            }
+#endif
         }
     }
     const unsigned long long m = __ballot(active);
@@ -335,6 +350,33 @@ __global__ __launch_bounds__(1024) void k_nn_prep(View v) {
         }
     }
     __syncthreads();
+#if SE3ICP_NN_BIN
+    if (s_single < 0) {
+        // group the searched queries by the target tree position of their previous match:
+        // a wave's 64 lanes then want the same target leaves (bitonic sort of the chunk's
+        // (position, query) keys in LDS; groups of 64 consecutive keys)
+        __shared__ unsigned long long s_key[kChunkQ];
+        const int tid = threadIdx.x;
+        s_key[tid] = active ? (((unsigned long long)tkey << 32) | (unsigned)x) : ~0ull;
+        __syncthreads();
+        for (int kk = 2; kk <= kChunkQ; kk <<= 1) {
+            for (int j = kk >> 1; j > 0; j >>= 1) {
+                const int p = tid ^ j;
+                if (p > tid) {
+                    const unsigned long long a = s_key[tid], b = s_key[p];
+                    const bool up = (tid & kk) == 0;
+                    if ((a > b) == up) { s_key[tid] = b; s_key[p] = a; }
+                }
+                __syncthreads();
+            }
+        }
+        int total = 0;
+        for (int j = 0; j < NL; ++j) total += s_cnt[j];
+        if (tid < total) v.qlist[(size_t)c * kChunkQ + tid] = (int)(unsigned)s_key[tid];
+        if (tid < NL) v.qcount[c * NL + tid] = min(64, max(0, total - 64 * tid));
+        return;
+    }
+#endif
     if (active) {
         int r = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
         for (int w = 0; w < wid; ++w) r += s_wc[w];
@@ -752,15 +794,15 @@ void launch_nn_prep(const View& v, hipStream_t s) {
     hipLaunchKernelGGL(k_nn_prep, dim3(v.nchunks), dim3(kChunkQ), 0, s, v);
 }
 // 16 groups of 64 per chunk, kWaves groups per block
-// and the single-query kernel over a fixed grid (8192 waves)
+// and the single-query kernel over a fixed grid (SE3ICP_NN_SINGLE_BLOCKS x 4 waves)
 void launch_nn_se3(const View& v, hipStream_t s) {
     hipLaunchKernelGGL(k_nn_group<12>, dim3(v.nchunks * (kChunkQ / 64) * SE3ICP_NN_SPLIT / kWaves), dim3(64 * kWaves), 0,
                        s, v);
-    hipLaunchKernelGGL(k_nn_single<12>, dim3(2048), dim3(256), 0, s, v);
+    hipLaunchKernelGGL(k_nn_single<12>, dim3(SE3ICP_NN_SINGLE_BLOCKS), dim3(256), 0, s, v);
 }
 void launch_nn_r3(const View& v, hipStream_t s) {
     hipLaunchKernelGGL(k_nn_group<3>, dim3(v.nchunks * (kChunkQ / 64) / kWaves), dim3(64 * kWaves), 0, s, v);
-    hipLaunchKernelGGL(k_nn_single<3>, dim3(2048), dim3(256), 0, s, v);
+    hipLaunchKernelGGL(k_nn_single<3>, dim3(SE3ICP_NN_SINGLE_BLOCKS), dim3(256), 0, s, v);
 }
 
 }  // namespace se3icp
