@@ -52,6 +52,9 @@ constexpr int kQ = 8;          // queries per wave (eight lanes each in the grou
 #define SE3ICP_LRF8_CAP 192
 #endif
 constexpr int kCap = SE3ICP_LRF8_CAP;  // candidates buffered per query (u32: cut key | candidate id), <= 256
+#ifndef SE3ICP_LRF8_SELECT
+#define SE3ICP_LRF8_SELECT 0  // bound of a tightening: 0 sorts; 1 (lists over 128) / 2 (always) a counting select (A/B: +11 % / +10 % k_lrf8)
+#endif
 #ifndef SE3ICP_LRF8_LEAF_BITS
 #define SE3ICP_LRF8_LEAF_BITS 6
 #endif
@@ -205,10 +208,61 @@ __device__ __forceinline__ unsigned kth_of_two(const unsigned* A, int na, const 
     const int j = r + 1 - lo;
     return max(lo > 0 ? A[lo - 1] : 0u, j > 0 ? B[j - 1] : 0u);
 }
+// The want-th smallest cut key (20-bit value, entries' top bits) of the group's list
+// without a sort: each lane counts its entries at or below a trial value, the group adds
+// the counts; the trial values interpolate between the bracket's counts, with a bisection
+// step whenever an interpolation did not halve the bracket.  Exact: returns the smallest
+// value v with count(<= v) >= want.
+__device__ __forceinline__ unsigned select_kth(const unsigned* list, int nbg, int l, int want) {
+    constexpr int PER = kCap / 8;
+    unsigned k[PER];
+    unsigned kmax = 0u, kmin = 0xfffffu;
+#pragma unroll
+    for (int s = 0; s < PER; ++s) {
+        const int e = l + 8 * s;
+        const bool v = e < nbg;
+        k[s] = v ? (list[e] >> 12) : 0xfffffu;
+        kmax = v ? max(kmax, k[s]) : kmax;
+        kmin = min(kmin, k[s]);
+    }
+    kmax = max(kmax, gx(kmax, 1)); kmax = max(kmax, gx(kmax, 2)); kmax = max(kmax, gx(kmax, 4));
+    kmin = min(kmin, gx(kmin, 1)); kmin = min(kmin, gx(kmin, 2)); kmin = min(kmin, gx(kmin, 4));
+    // count(<= lo) < want <= count(<= hi)
+    int lo = (int)kmin - 1, hi = (int)kmax, clo = 0, chi = nbg;
+    bool bis = false;
+    for (;;) {
+        const bool open = hi - lo > 1;
+        if (__ballot(open) == 0ull) break;
+        int mid;
+        if (bis) {
+            mid = (lo + hi) >> 1;
+        } else {
+            const float f = (float)(want - clo) * __builtin_amdgcn_rcpf((float)max(chi - clo, 1));
+            mid = lo + (int)((float)(hi - lo) * f);
+            mid = min(max(mid, lo + 1), hi - 1);
+        }
+        unsigned c = 0u;
+#pragma unroll
+        for (int s = 0; s < PER; ++s) c += (k[s] <= (unsigned)mid) ? 1u : 0u;
+        c += gx(c, 1);
+        c += gx(c, 2);
+        c += gx(c, 4);
+        if (open) {
+            const int width = hi - lo;
+            if ((int)c >= want) { hi = mid; chi = (int)c; }
+            else { lo = mid; clo = (int)c; }
+            bis = !bis && 2 * (hi - lo) > width;
+        }
+    }
+    return (unsigned)hi << 12;
+}
+
 __device__ __forceinline__ uint2 tighten_group(unsigned* lists, int g, int l, int nbg, int nmax, int Kw) {
     unsigned* list = lists + g * kCap;
     unsigned tg;
-    if (nmax <= 128) {
+    if (SE3ICP_LRF8_SELECT >= 2 || (SE3ICP_LRF8_SELECT == 1 && nmax > 128)) {
+        tg = select_kth(list, nbg, l, Kw);
+    } else if (nmax <= 128) {
         tg = list_kth<16>(list, nbg, l, Kw - 1);
     } else {  // two sorted runs of <= 128 (a 256-entry network would need the kernel's registers)
         const int na = min(nbg, 128), nb = max(nbg - 128, 0);
