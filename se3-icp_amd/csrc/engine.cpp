@@ -685,6 +685,12 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
                          sum[1] - trace_prev_[1], sum[7] - trace_prev_[7], sum[6] - trace_prev_[6],
                          sum[2] - trace_prev_[2], sum[3] - trace_prev_[3], ms[0], ms[1], ms[2], ms[3]);
             for (int k = 0; k < kStatCols; ++k) trace_prev_[k] = sum[k];
+#ifdef SE3ICP_PROF
+            std::fprintf(stderr, "[nn] iter %d: longest SE(3) group wave %.1f us (%llu box-test steps, %llu leaf visits, "
+                         "%llu queries)\n", it, (double)(stats[10] >> 40) / 100.0, (stats[10] >> 20) & 0xfffffull,
+                         (stats[10] >> 6) & 0x3fffull, stats[10] & 63ull);
+            HIPCHK(hipMemset((unsigned long long*)d_stats_.p + 10, 0, sizeof(unsigned long long)));
+#endif
         }
         const volatile int32_t* ph = h_phase_ + (size_t)(it % kLoopRing) * npairs;
         n_se3 = n_r3 = 0;
@@ -738,10 +744,17 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         ktimes_.r3_queries = sum[6];
         ktimes_.r3_searched = sum[7];
 #ifdef SE3ICP_PROF
-        std::fprintf(stderr, "[prof] nn12: leaf visits %.0f, lanes wanting a visited leaf %.1f%% of valid lanes; "
-                     "%.0f group waves, %.1f us each on average (100 MHz clock)\n",
-                     sum[9], 100.0 * sum[8] / std::max(1.0, sum[10]), std::floor(sum[11] / 17592186044416.0),
-                     std::fmod(sum[11], 17592186044416.0) / 100.0 / std::max(1.0, std::floor(sum[11] / 17592186044416.0)));
+        {
+            const double nw = std::max(1.0, std::floor(sum[11] / 17592186044416.0));
+            const double mean = std::fmod(sum[11], 17592186044416.0) / nw;  // 100 MHz ticks
+            const double sq = (double)stats[kStatCols + 10] / nw;
+            std::fprintf(stderr, "[prof] nn12: leaf visits %.0f; %.0f group waves, %.1f us each on average (sd %.1f, "
+                         "longest %.1f us; 100 MHz clock)\n",
+                         sum[9], nw, mean / 100.0, std::sqrt(std::max(0.0, sq - mean * mean)) / 100.0,
+                         (double)(stats[10] >> 40) / 100.0);
+            std::fprintf(stderr, "[prof] nn12 longest wave: %llu box-test steps, %llu leaf visits, %llu queries\n",
+                         (stats[10] >> 20) & 0xfffffull, (stats[10] >> 6) & 0x3fffull, stats[10] & 63ull);
+        }
 #endif
     }
     float setup_ms = 0, loop_ms = 0;

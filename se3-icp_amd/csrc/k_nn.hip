@@ -160,6 +160,12 @@ __device__ __forceinline__ void compact_sweep(const float4* tile, const float4* 
 #ifndef SE3ICP_NN_XCD
 #define SE3ICP_NN_XCD 0  // XCD-aware chunk -> block mapping of k_nn_prep / k_nn_group (A/B: 1 slower, pairs load XCDs unevenly)
 #endif
+#ifndef SE3ICP_NN_EJECT
+#define SE3ICP_NN_EJECT 0  // node visits after which a group wave hands its widest-ball lanes to k_nn_single (0: never; A/B 64 / 128 / 256: NN +31 / +9 / +4 %: the long waves are uniformly hard groups)
+#endif
+#ifndef SE3ICP_NN_SMALL
+#define SE3ICP_NN_SMALL 4  // groups of at most this many queries are searched one query at a time
+#endif
 #ifndef SE3ICP_NN_SINGLE_BLOCKS
 #define SE3ICP_NN_SINGLE_BLOCKS 4096  // grid of the one-query-per-wave kernels (4 waves per block, grid-strided)
 #endif
@@ -425,6 +431,11 @@ __device__ __forceinline__ void nn_finish(const View& v, const PairDev* P, int p
 }
 
 template <int D>
+__device__ __forceinline__ void single_one(const View& v, const PairDev* P, int pair, const TreeRef& TR,
+                                           const CloudDev& ct, int gx, int g, int lane, unsigned* n_eval,
+                                           unsigned* n_box);
+
+template <int D>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_WPE))) void k_nn_group(View v) {
     constexpr int NV = (D + 3) / 4;
     __shared__ float4 s_tile[kWaves][kLeafMax * NV];
@@ -454,6 +465,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_W
     if (cnt_q <= 0) return;
     const CloudDev cs = v.clouds[P->src], ct = v.clouds[P->tgt];
     const TreeRef TR = (D == 12) ? v.t12 : v.t3;
+    if (cnt_q <= SE3ICP_NN_SMALL) {
+        // a group of a few queries (a chunk's leftovers): each searched by all 64 lanes in
+        // turn (k_nn_single's lane-parallel search) -- a lone query with a wide ball would
+        // otherwise walk the tree one node per step and set the launch's time
+        unsigned n_eval = 0, n_box = 0;
+        for (int q = 0; q < cnt_q; ++q) {
+            const int gxq = __builtin_amdgcn_readfirstlane(cs.off + v.qlist[(size_t)gi * 64 + q_lo + q]);
+            const int gq = __builtin_amdgcn_readfirstlane(cs.off + TR.perm[gxq]);
+            single_one<D>(v, P, pair, TR, ct, gxq, gq, lane, &n_eval, &n_box);
+        }
+        if (lane == 0) {
+            unsigned long long* st = v.stats + kStatCols * (gi & 63) + (D == 12 ? 0 : 2);
+            atomicAdd(st, 64ull * n_eval);
+            atomicAdd(st + 1, 64ull * n_box);
+        }
+        return;
+    }
     const bool valid = lane < cnt_q;
     const int gx = cs.off + v.qlist[(size_t)gi * 64 + q_lo + (valid ? lane : 0)];  // source tree slot
     const int g = cs.off + TR.perm[gx];
@@ -523,10 +551,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_W
     int sp = 1;
     unsigned n_eval = 0, n_box = 0;  // wave-uniform work counters (roofline accounting)
 #ifdef SE3ICP_PROF
-    unsigned n_want = 0, n_leafv = 0, n_valid = __popcll(__ballot(valid));
+    unsigned n_want = 0, n_leafv = 0;
+    const unsigned n_valid = (unsigned)__popcll(__ballot(valid));
     const unsigned long long t_w0 = __builtin_amdgcn_s_memrealtime();
 #endif
+#if SE3ICP_NN_EJECT
+    // A wave still walking after SE3ICP_NN_EJECT node visits usually carries a query or a
+    // few with a far wider ball than the rest (an SE(3) element no target frame resembles):
+    // those lanes leave the group walk and go to the one-query-per-wave search (k_nn_single,
+    // next in the stream), which tests 64 nodes per instruction instead of one per step.
+    bool ejected = false;
+    unsigned next_check = 2u * SE3ICP_NN_EJECT;
+#endif
     while (sp > 0) {
+#if SE3ICP_NN_EJECT
+        if (n_box >= next_check) {
+            next_check += 2u * SE3ICP_NN_EJECT;
+            const bool live = (int)valid & (int)!ejected;
+            const float tmax = -wave_minf(live ? -thr : 0.f);
+            const bool ej = (int)live & (int)(tmax > 0.f) & (int)(thr >= 0.25f * tmax);
+            const unsigned long long em = __ballot(ej);
+            const int ne = __popcll(em);
+            if ((int)(ne > 0) & (int)(ne <= 16)) {
+                int base = 0;
+                if (lane == 0) base = atomicAdd(&v.flag_count[D == 12 ? 1 : 2], ne);
+                base = __shfl(base, 0, 64);
+                if (ej) {
+                    const int r = base + __builtin_amdgcn_mbcnt_hi((unsigned)(em >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)em, 0u));
+                    if (D == 12) v.sq_list[r] = gx;
+                    else v.sq_list[v.ld - 1 - r] = gx;
+                    ejected = true;
+                    thr = -1.f;
+                }
+            }
+        }
+#endif
         const int h = __builtin_amdgcn_readlane(stk, sp - 1);
         --sp;
         if (h >= first_leaf) {
@@ -628,11 +687,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_W
         if (D == 12) {
             atomicAdd(v.stats + kStatCols * (gi & 63) + 8, (unsigned long long)n_want);
             atomicAdd(v.stats + kStatCols * (gi & 63) + 9, (unsigned long long)n_leafv);
-            atomicAdd(v.stats + kStatCols * (gi & 63) + 10, (unsigned long long)n_leafv * n_valid);
-            atomicAdd(v.stats + kStatCols * (gi & 63) + 11, (1ull << 44) + (__builtin_amdgcn_s_memrealtime() - t_w0));  // waves, wave time
+            const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t_w0;
+            // longest wave, with its leaf visits, box-test steps and valid queries
+            atomicMax(v.stats + 10, (dt << 40) | ((unsigned long long)min(n_box, 0xfffffu) << 20) |
+                                        ((unsigned long long)min(n_leafv, 0x3fffu) << 6) | (n_valid % 64u));
+            atomicAdd(v.stats + kStatCols + 10, dt * dt);                      // (spread)
+            atomicAdd(v.stats + kStatCols * (gi & 63) + 11, (1ull << 44) + dt);  // waves, wave time
         }
 #endif
     }
+#if SE3ICP_NN_EJECT
+    if (ejected) return;  // (searched again by k_nn_single)
+#endif
     if (!valid) return;
     // certification (see the header) and the stored distance
     const bool flag = (bool)((int)(i1 < 0) | (int)!(d2 - d1 > 2.f * f32_err(d2, na, nb, D)));
