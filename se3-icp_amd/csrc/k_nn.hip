@@ -39,6 +39,9 @@ using namespace loopdev;
 
 constexpr int kWaves = 4;
 // Leaves wanted by at most this many lanes take the compacted path (8 lanes per query)
+#ifndef SE3ICP_NN_TPL
+#define SE3ICP_NN_TPL 4  // targets per lane in the compacted leaf sweeps (held in registers across queries)
+#endif
 #ifndef SE3ICP_NN_COMPACT3
 #define SE3ICP_NN_COMPACT3 40  // R3 phase (0: broadcast sweeps only)
 #endif
@@ -95,7 +98,7 @@ __device__ __forceinline__ float dist12(const f32x2* q2, const float4* t) {
 // sub, sub+LPQ, sub+2LPQ, sub+3LPQ per lane (LPQ * 4 >= cnt), the group's top-2 into
 // r1/r2/rb[query].  The lane's 4 targets are loop-invariant over the queries: the
 // compiler keeps them in registers (4 waves/SIMD; measured faster than re-reading at 5).
-template <int D, int LPQ>
+template <int D, int LPQ, int TPL = SE3ICP_NN_TPL>
 __device__ __forceinline__ void compact_sweep(const float4* tile, const float4* sq, const int* wl, float* r1, float* r2,
                                               int* rb, int w, int cnt, int ta, int lane) {
     constexpr int NV = (D + 3) / 4;
@@ -116,7 +119,7 @@ __device__ __forceinline__ void compact_sweep(const float4* tile, const float4* 
         float a1 = INFINITY, a2 = INFINITY;
         int b1 = 0;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < TPL; ++u) {
             const int j = sub + LPQ * u;
             float acc;
             if constexpr (D == 12) {
@@ -643,8 +646,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_W
                 if ((W >> lane) & 1ull)
                     s_wl[wid][__builtin_amdgcn_mbcnt_hi((unsigned)(W >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)W, 0u))] = lane;
                 __builtin_amdgcn_wave_barrier();
-                if (cnt <= 32) compact_sweep<D, 8>(tile, s_q[wid], s_wl[wid], s_r1[wid], s_r2[wid], s_rb[wid], w, cnt, ta, lane);
-                else compact_sweep<D, 16>(tile, s_q[wid], s_wl[wid], s_r1[wid], s_r2[wid], s_rb[wid], w, cnt, ta, lane);
+                constexpr int kL32 = 32 / SE3ICP_NN_TPL, kL64 = 64 / SE3ICP_NN_TPL;  // lanes per query
+                if (cnt <= 32) compact_sweep<D, kL32>(tile, s_q[wid], s_wl[wid], s_r1[wid], s_r2[wid], s_rb[wid], w, cnt, ta, lane);
+                else compact_sweep<D, kL64>(tile, s_q[wid], s_wl[wid], s_r1[wid], s_r2[wid], s_rb[wid], w, cnt, ta, lane);
                 __builtin_amdgcn_wave_barrier();
                 if ((W >> lane) & 1ull) {
                     const float r1 = s_r1[wid][lane], r2 = s_r2[wid][lane];
@@ -654,7 +658,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_W
                     d1 = fminf(d1, r1);
                 }
                 __builtin_amdgcn_wave_barrier();
-                n_eval += 4 * ((w + (cnt <= 32 ? 7 : 3)) >> (cnt <= 32 ? 3 : 2));  // 64-lane evaluation slots issued
+                {  // 64-lane evaluation slots issued
+                    const int qpi = 64 / (cnt <= 32 ? 32 / SE3ICP_NN_TPL : 64 / SE3ICP_NN_TPL);
+                    n_eval += SE3ICP_NN_TPL * ((w + qpi - 1) / qpi);
+                }
             }
             if ((int)valid & (int)(d1 < INFINITY)) thr = fminf(thr, widen(d1, d2));
             continue;
