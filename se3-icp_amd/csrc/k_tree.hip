@@ -109,6 +109,9 @@ __global__ __launch_bounds__(256) void k_tree_bbox(TreeView t, int level) {
 //   scatter each point's rank among its node's points of the same class -> its new position
 // Ties keep their tree order, so the build is deterministic.
 constexpr int kPartBits = 11, kPartBins = 1 << kPartBits;  // bins per pass; keys of 2 * kPartBits bits
+#ifndef SE3ICP_TREE_GSPLIT
+#define SE3ICP_TREE_GSPLIT 0  // global levels' split dimension: 0 widest sampled extent, 1 largest sample variance (A/B: SE(3) NN +9 %, setup +0.2 ms)
+#endif
 constexpr int kPartThreads = 256, kPartPer = 4, kPartElems = kPartThreads * kPartPer;
 constexpr int kSelThreads = 1024, kSelPer = kPartBins / kSelThreads;
 constexpr int kHistPer = 8, kHistElems = kPartThreads * kHistPer;  // tree positions per histogram block
@@ -145,6 +148,117 @@ __device__ __forceinline__ PartDim part_dim_of(const uint32_t* blo, const uint32
     return r;
 }
 
+#if SE3ICP_TREE_GSPLIT == 1
+// Split dimension of the global levels by the largest sample variance, as the LDS levels
+// (k_tree_local) choose theirs: every kSplitSample-th point's coordinates, quantised to
+// kMomBits bits over its cloud's root box, summed in 64-bit integers (order-independent
+// atomics: the tree stays deterministic).  Per node: count, then (sum, sum of squares) per
+// dimension.
+constexpr int kMomBits = 20;
+struct PartRoot {
+    float lo[12], s[12];  // q = (x - lo) * s in [0, 2^kMomBits)
+};
+__global__ __launch_bounds__(64) void k_part_root(TreeView t, PartRoot* root) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    if (c >= t.nclouds) return;
+    const size_t base = (size_t)c * t.nnodes * t.D;  // the root's sampled box (k_tree_bbox, level 0)
+    PartRoot r;
+    for (int d = 0; d < 12; ++d) { r.lo[d] = 0.f; r.s[d] = 0.f; }
+    for (int d = 0; d < t.D; ++d) {
+        const float lo = ord_float(t.blo[base + d]), ext = ord_float(t.bhi[base + d]) - lo;
+        r.lo[d] = lo;
+        r.s[d] = (ext > 0.f && ext < INFINITY) ? (float)((1 << kMomBits) - 1) / ext : 0.f;
+    }
+    root[c] = r;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_part_moments(TreeView t, int level, const PartRoot* root,
+                                                      unsigned long long* mom) {
+    const int g = (blockIdx.x * blockDim.x + threadIdx.x) * kSplitSample;
+    const int lane = threadIdx.x & 63;
+    const bool valid = g < t.npts;
+    int c = -1, node = -1;
+    unsigned long long s1[D], s2[D];
+    if (valid) {
+        c = t.cloud_of[g];
+        const CloudDev cl = t.clouds[c];
+        node = tree_node_of(g - cl.off, cl.n, level);
+        const int pt = cl.off + t.perm[g];
+        const PartRoot& r = root[c];
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            float qf = (t.vec[tree_in_ix(t, d, pt)] - r.lo[d]) * r.s[d];
+            qf = fminf(fmaxf(qf, 0.f), (float)((1 << kMomBits) - 1));  // NaN -> 0
+            const unsigned long long q = (unsigned)qf;
+            s1[d] = q;
+            s2[d] = q * q;
+        }
+    } else {
+#pragma unroll
+        for (int d = 0; d < D; ++d) { s1[d] = 0ull; s2[d] = 0ull; }
+    }
+    unsigned cnt = valid ? 1u : 0u;
+    const long long key = valid ? ((long long)c << 32) | (unsigned)node : -1;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const long long ok = __shfl_down(key, o, 64);
+        const bool same = (lane + o < 64) && ok == key;
+        const unsigned oc = __shfl_down(cnt, o, 64);
+        if (same) cnt += oc;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const unsigned long long a = __shfl_down(s1[d], o, 64), b = __shfl_down(s2[d], o, 64);
+            if (same) { s1[d] += a; s2[d] += b; }
+        }
+    }
+    const long long prev = __shfl_up(key, 1, 64);
+    const bool head = valid && (lane == 0 || prev != key);
+    if (head) {
+        unsigned long long* m = mom + (size_t)((c << level) + node) * (1 + 2 * D);
+        atomicAdd(m, (unsigned long long)cnt);
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            atomicAdd(m + 1 + 2 * d, s1[d]);
+            atomicAdd(m + 2 + 2 * d, s2[d]);
+        }
+    }
+}
+
+// every node's split: the dimension of largest variance; the key quantises that
+// coordinate over mean +- 8 sd (points beyond clamp to the end bins).  Clears the moments.
+__global__ __launch_bounds__(64) void k_part_dims(TreeView t, int level, const PartRoot* root, unsigned long long* mom,
+                                                  PartDim* dims) {
+    const int id = blockIdx.x * 64 + threadIdx.x;
+    if (id >= (t.nclouds << level)) return;
+    const int c = id >> level;
+    const int D = t.D;
+    unsigned long long* m = mom + (size_t)id * (1 + 2 * D);
+    const PartRoot& r = root[c];
+    const double n = (double)m[0];
+    int best = 0;
+    double bvar = -1.0, bmean = 0.0;
+    for (int d = 0; d < D; ++d) {
+        double var = 0.0, mean = 0.0;
+        if (n > 0.0 && r.s[d] > 0.f) {
+            const double mq = (double)m[1 + 2 * d] / n;
+            const double vq = fmax((double)m[2 + 2 * d] / n - mq * mq, 0.0);
+            const double inv = 1.0 / (double)r.s[d];
+            var = vq * inv * inv;
+            mean = (double)r.lo[d] + mq * inv;
+        }
+        if (var > bvar) { bvar = var; best = d; bmean = mean; }
+    }
+    for (int k = 0; k < 1 + 2 * D; ++k) m[k] = 0ull;
+    const double sd = sqrt(bvar);
+    PartDim pd;
+    pd.best = best;
+    pd.lo = (float)(bmean - 8.0 * sd);
+    pd.scale = (sd > 0.0 && sd < 1e30) ? (float)((double)kKeyMax / (16.0 * sd)) : 0.f;
+    pd.pad = 0;
+    dims[id] = pd;
+}
+#else
 // every node's split from its sampled box (k_tree_bbox); once per node, not per point
 __global__ __launch_bounds__(64) void k_part_dims(TreeView t, int level, PartDim* dims) {
     const int id = blockIdx.x * 64 + threadIdx.x;
@@ -153,6 +267,7 @@ __global__ __launch_bounds__(64) void k_part_dims(TreeView t, int level, PartDim
     const size_t base = ((size_t)c * t.nnodes + tree_heap(level, node)) * t.D;
     dims[id] = part_dim_of(t.blo + base, t.bhi + base, t.D);
 }
+#endif
 
 // node ids (cloud << level | node) grow with the tree position
 __device__ __forceinline__ int part_node_id(int c, int level, int node) { return (c << level) + node; }
@@ -714,6 +829,8 @@ struct PartScratch {
     uint32_t* overflow;
     PartSel* sel;
     PartDim* dims[1];
+    void* root;               // PartRoot per cloud (variance splits)
+    unsigned long long* mom;  // per node: count, (sum, sum of squares) per dimension
     SegCnt* tails;
     SegCnt* carry;
     size_t overflow_words;
@@ -733,6 +850,8 @@ size_t part_layout(int npts, int nclouds, int G, char* base, PartScratch* ps) {
     char* ov = take(nodes * kPartBins * sizeof(uint32_t));
     char* sl = take(nodes * sizeof(PartSel));
     char* d0 = take(nodes * sizeof(PartDim));
+    char* rt = take((size_t)nclouds * 96);
+    char* mm = take(nodes * 25 * sizeof(unsigned long long));
     char* tl = take(nblk * sizeof(SegCnt));
     char* cr = take(nblk * sizeof(SegCnt));
     if (ps) {
@@ -741,6 +860,8 @@ size_t part_layout(int npts, int nclouds, int G, char* base, PartScratch* ps) {
         ps->overflow = (uint32_t*)ov;
         ps->sel = (PartSel*)sl;
         ps->dims[0] = (PartDim*)d0;
+        ps->root = rt;
+        ps->mom = (unsigned long long*)mm;
         ps->tails = (SegCnt*)tl;
         ps->carry = (SegCnt*)cr;
         ps->overflow_words = nodes * kPartBins;
@@ -773,12 +894,27 @@ int build_trees(TreeView t, void* tmp, size_t tmp_bytes, uint32_t* qbuf, int32_t
     if (ps.overflow_words) hipLaunchKernelGGL(k_clear_words, dim3(256), dim3(256), 0, s, ps.overflow, ps.overflow_words);
     const int nblk = (t.npts + kPartElems - 1) / kPartElems;
     const int nhist = (t.npts + kHistElems - 1) / kHistElems;
+#if SE3ICP_TREE_GSPLIT == 1
+    if (G > 0) {
+        hipLaunchKernelGGL(bbox, dim3(nbs), dim3(256), 0, s, tc, 0);  // the roots' boxes: the moments' scale
+        hipLaunchKernelGGL(k_part_root, dim3((t.nclouds + 63) / 64), dim3(64), 0, s, tc, (PartRoot*)ps.root);
+        hipLaunchKernelGGL(k_clear_words, dim3(64), dim3(256), 0, s, (uint32_t*)ps.mom,
+                           ((size_t)t.nclouds << (G - 1)) * 25 * 2);
+    }
+#endif
     for (int l = 0; l < G; ++l) {
         PartDim* dims = ps.dims[0];
+#if SE3ICP_TREE_GSPLIT == 1
+        hipLaunchKernelGGL(t.D == 12 ? k_part_moments<12> : k_part_moments<3>, dim3(nbs), dim3(256), 0, s, tc, l,
+                           (const PartRoot*)ps.root, ps.mom);
+        hipLaunchKernelGGL(k_part_dims, dim3(((t.nclouds << l) + 63) / 64), dim3(64), 0, s, tc, l,
+                           (const PartRoot*)ps.root, ps.mom, dims);
+#else
         // (the split dimension from every kSplitSample-th point's box: estimating the
         // children's boxes from the parent's cut was measured to give slower searches)
         hipLaunchKernelGGL(bbox, dim3(nbs), dim3(256), 0, s, tc, l);
         hipLaunchKernelGGL(k_part_dims, dim3(((t.nclouds << l) + 63) / 64), dim3(64), 0, s, tc, l, dims);
+#endif
         hipLaunchKernelGGL(k_part_hist, dim3(nhist), dim3(kPartThreads), 0, s, tc, l, dims, qbuf, ps.dense, ps.block_id0,
                            ps.overflow);
         hipLaunchKernelGGL(k_part_select, dim3(t.nclouds << l), dim3(kSelThreads), 0, s, tc, l, (const uint32_t*)ps.dense,
