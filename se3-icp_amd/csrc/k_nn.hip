@@ -179,7 +179,7 @@ __device__ __forceinline__ void compact_sweep(const float4* tile, const float4* 
 #define SE3ICP_NN_SPLIT 1
 #endif
 #ifndef SE3ICP_NN_DENSE
-#define SE3ICP_NN_DENSE 128
+#define SE3ICP_NN_DENSE 256  // (A/B 64 / 128 / 256: 256 best by ~1 % of the loop)
 #endif
 #ifndef SE3ICP_NN_DENSE3
 #define SE3ICP_NN_DENSE3 256
