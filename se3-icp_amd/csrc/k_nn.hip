@@ -160,8 +160,11 @@ __device__ __forceinline__ void compact_sweep(const float4* tile, const float4* 
 #ifndef SE3ICP_NN_WPE
 #define SE3ICP_NN_WPE 4  // waves per SIMD of k_nn_group (4: its natural 128 VGPRs)
 #endif
+#ifndef SE3ICP_NN_XCD_RUN
+#define SE3ICP_NN_XCD_RUN 64  // (SE3ICP_NN_XCD 2) group blocks per XCD run: 64 = 16 chunks (A/B 16 / 64 / 128 / 256: 64 best)
+#endif
 #ifndef SE3ICP_NN_XCD
-#define SE3ICP_NN_XCD 0  // XCD-aware chunk -> block mapping of k_nn_prep / k_nn_group (A/B: 1 slower, pairs load XCDs unevenly)
+#define SE3ICP_NN_XCD 2  // chunk -> block mapping of k_nn_prep / k_nn_group: 2 runs of chunks dealt round-robin over the XCDs (neighbouring chunks share target leaves in one L2; SE(3) NN -3 %), 1 one contiguous range per XCD (slower: the pairs load the XCDs unevenly), 0 none
 #endif
 #ifndef SE3ICP_NN_EJECT
 #define SE3ICP_NN_EJECT 0  // node visits after which a group wave hands its widest-ball lanes to k_nn_single (0: never; A/B 64 / 128 / 256: NN +31 / +9 / +4 %: the long waves are uniformly hard groups)
@@ -293,7 +296,8 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
 __global__ __launch_bounds__(1024) void k_nn_prep(View v) {
     constexpr int NL = kChunkQ / 64;  // leaves (groups) per chunk
     __shared__ int s_cnt[NL], s_slot[NL], s_base[NL], s_wc[NL], s_single;
-    const int c = SE3ICP_NN_XCD ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int c = SE3ICP_NN_XCD == 2 ? xcd_block_runs(blockIdx.x, gridDim.x, SE3ICP_NN_XCD_RUN / 4)
+                  : SE3ICP_NN_XCD ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int pair = c >> v.chunk_level;
     const PairDev* P = v.pairs + pair;
     const int phase = P->phase;
@@ -455,7 +459,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_W
     // shorter waves for a launch whose time is set by its longest waves)
     constexpr int kSplit = D == 12 ? SE3ICP_NN_SPLIT : 1;
     // (blocks of one XCD take consecutive chunks: a pair's target tree stays in that XCD's L2)
-    const int bx = SE3ICP_NN_XCD ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int bx = SE3ICP_NN_XCD == 2 ? xcd_block_runs(blockIdx.x, gridDim.x, SE3ICP_NN_XCD_RUN)
+                   : SE3ICP_NN_XCD ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int wi = __builtin_amdgcn_readfirstlane(bx * kWaves + wid);
     const int gi = wi / kSplit, q_lo = (wi % kSplit) * (64 / kSplit);
     const int c = gi >> 4;

@@ -191,6 +191,16 @@ __device__ __forceinline__ void wave_sort_keys(unsigned long long (&k)[PER]) {
 // Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, Workgroup
 // dispatch): relabel them so that each XCD runs one contiguous range of the grid and its
 // L2 keeps the data neighbouring blocks share (bijective for any grid size).
+// Finer variant: runs of S consecutive logical blocks share an XCD and the runs are dealt
+// round-robin over the 8 XCDs (locality within a run, balance across runs).  Bijective
+// when nb is a multiple of 8 * S; otherwise the blocks past the last whole round keep
+// their own index.
+__device__ __forceinline__ int xcd_block_runs(int b, int nb, int S) {
+    const int whole = nb / (8 * S) * (8 * S);
+    if (b >= whole) return b;
+    const int x = b & 7, i = b >> 3;
+    return ((i / S) * 8 + x) * S + (i % S);
+}
 __device__ __forceinline__ int xcd_block(int b, int nb) {
     const int q = nb >> 3, r = nb & 7, x = b & 7, i = b >> 3;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + i;
