@@ -561,10 +561,13 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(TreeView t, int l
 #define SE3ICP_LOCAL_MAX 4096
 #endif
 constexpr int kLocalMax = SE3ICP_LOCAL_MAX;  // power of two
-constexpr int kLocalBits = __builtin_ctz(kLocalMax);  // element field of the block sort keys
+[[maybe_unused]] constexpr int kLocalBits = __builtin_ctz(kLocalMax);  // element field of the block sort keys
 constexpr int kWaveSortPer = 8;  // sub-nodes of <= 512 points: register sort by one wave
 #ifndef SE3ICP_TREE_SPLIT
 #define SE3ICP_TREE_SPLIT 1
+#endif
+#ifndef SE3ICP_TREE_LPART
+#define SE3ICP_TREE_LPART 1  // LDS levels over 512 points: 1 median partition, 0 block bitonic sort
 #endif
 #ifndef SE3ICP_TREE_STRIDE
 #define SE3ICP_TREE_STRIDE 16
@@ -576,6 +579,7 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
     __shared__ unsigned long long s_key[kLocalMax];
     __shared__ int32_t s_val[kLocalMax];
     __shared__ int s_best[128];
+    __shared__ float s_mu[128], s_sd[128];  // the split coordinate's sample mean and sd (variance splits)
     const int nG = 1 << G;
     const int c = blockIdx.x / nG, i = blockIdx.x % nG;
     const CloudDev cl = t.clouds[c];
@@ -627,7 +631,7 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
                     }
                     const float mu = a * inv;
                     const float e = b * inv - mu * mu;
-                    if (e > ext) { ext = e; best = d; }
+                    if (e > ext) { ext = e; best = d; if (lane == 0) { s_mu[k] = mu; s_sd[k] = sqrtf(fmaxf(e, 0.f)); } }
                 }
 #else
                 float lo[D], hi[D];
@@ -687,6 +691,146 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
             __syncthreads();
             continue;
         }
+#if SE3ICP_TREE_LPART && SE3ICP_TREE_SPLIT == 1
+        // large sub-nodes (<= 4 of them): a stable median partition in LDS, as the global
+        // levels do -- the split coordinate quantised to 22 bits over the sub-node's sample
+        // mean +- 8 sd, the median bin by two 11-bit histogram passes, then each point's
+        // rank among its sub-node's points of the same class (left / tie / right) by a
+        // block scan; ties keep their order.  Thread t owns the points t*8 .. t*8+7.
+        {
+            constexpr int PER = kLocalMax / kLocalThreads;
+            constexpr int kB = 2048;  // bins per pass
+            uint32_t* s_h = reinterpret_cast<uint32_t*>(s_key);  // nsub x kB histogram words
+            __shared__ int s_sel[4][4];  // per sub-node: bin / threshold, tie_left, tie_n, cum
+            __shared__ uint32_t s_scan[kLocalThreads / 64][8];
+            for (int x = tid; x < nsub * kB; x += kLocalThreads) s_h[x] = 0u;
+            uint32_t q[PER];
+            int sb[PER];
+            int32_t val[PER];
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const int e = tid * PER + u;
+                q[u] = 0u;
+                sb[u] = 0;
+                val[u] = -1;
+                if (e < m) {
+                    const int sub = tree_node_of(A + e, n, l) - (i << r);
+                    const int p = s_val[e];
+                    const float sd = s_sd[sub];
+                    const float x = t.vec[tree_in_ix(t, s_best[sub], cl.off + p)];
+                    float qf = sd > 0.f ? (x - (s_mu[sub] - 8.f * sd)) * (4194303.f / (16.f * sd)) : 0.f;
+                    qf = fminf(fmaxf(qf, 0.f), 4194303.f);  // NaN -> 0
+                    q[u] = (uint32_t)qf;
+                    sb[u] = sub;
+                    val[u] = p;
+                    atomicAdd(&s_h[sub * kB + (q[u] >> 11)], 1u);
+                }
+            }
+            __syncthreads();
+            const int lane = tid & 63, wv = tid >> 6;
+            // a wave per sub-node: the bin where the count reaches the left child's size
+            auto find_bin = [&](int k, int want, int pass) {
+                const uint32_t* hk = s_h + k * kB + lane * (kB / 64);
+                uint32_t tot = 0;
+                for (int j = 0; j < kB / 64; ++j) tot += hk[j];
+                uint32_t inc = tot;  // inclusive wave scan of the lanes' totals
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = __shfl_up(inc, o, 64);
+                    if (lane >= o) inc += y;
+                }
+                uint32_t cum = inc - tot;
+                if ((int)(cum >= (uint32_t)want || inc < (uint32_t)want) & (int)!(want == 0 && lane == 0)) return;
+                for (int j = 0; j < kB / 64; ++j) {
+                    const uint32_t vj = hk[j], nxt = cum + vj;
+                    const int bin = lane * (kB / 64) + j;
+                    if (((int)(cum < (uint32_t)want) & (int)(nxt >= (uint32_t)want)) | ((int)(want == 0) & (int)(bin == 0))) {
+                        if (pass == 0) {
+                            s_sel[k][0] = bin;
+                        } else {
+                            s_sel[k][0] = (s_sel[k][0] << 11) | bin;
+                            s_sel[k][2] = (int)vj;
+                        }
+                        s_sel[k][1] = want - (int)cum;
+                        break;
+                    }
+                    cum = nxt;
+                }
+            };
+            if (wv < nsub) {
+                const int a0 = tree_first(n, l, (i << r) + wv) - A;
+                const int mL = tree_first(n, l + 1, 2 * ((i << r) + wv) + 1) - A - a0;
+                find_bin(wv, mL, 0);
+            }
+            __syncthreads();
+            for (int x = tid; x < nsub * kB; x += kLocalThreads) s_h[x] = 0u;
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const int e = tid * PER + u;
+                if ((int)(e < m) & (int)((int)(q[u] >> 11) == s_sel[sb[u]][0])) atomicAdd(&s_h[sb[u] * kB + (q[u] & 2047u)], 1u);
+            }
+            __syncthreads();
+            if (wv < nsub) find_bin(wv, s_sel[wv][1], 1);
+            __syncthreads();
+            // class counts per sub-node (16-bit left | 16-bit tie), thread-exclusive block scan
+            uint32_t cnt[4] = {0u, 0u, 0u, 0u};
+            int cls[PER];
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const int e = tid * PER + u;
+                cls[u] = 2;
+                if (e < m) {
+                    const int T = s_sel[sb[u]][0];
+                    cls[u] = (int)q[u] < T ? 0 : ((int)q[u] == T ? 1 : 2);
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    cnt[k] += (sb[u] == k && e < m) ? (cls[u] == 0 ? 1u : (cls[u] == 1 ? 65536u : 0u)) : 0u;
+            }
+            uint32_t pre[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                uint32_t inc = cnt[k];
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t y = __shfl_up(inc, o, 64);
+                    if (lane >= o) inc += y;
+                }
+                if (lane == 63) s_scan[wv][k] = inc;
+                pre[k] = inc - cnt[k];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                for (int w = 0; w < wv; ++w) pre[k] += s_scan[w][k];
+            int dst[PER];
+#pragma unroll
+            for (int u = 0; u < PER; ++u) {
+                const int e = tid * PER + u;
+                dst[u] = -1;
+                if (e < m) {
+                    const int k = sb[u];
+                    const uint32_t run = k == 0 ? pre[0] : (k == 1 ? pre[1] : (k == 2 ? pre[2] : pre[3]));
+                    const int r0 = (int)(run & 0xffffu), r1 = (int)(run >> 16);
+                    const int a0 = tree_first(n, l, (i << r) + k) - A;
+                    const int mL = tree_first(n, l + 1, 2 * ((i << r) + k) + 1) - A - a0;
+                    const int tl = s_sel[k][1], tn = s_sel[k][2];
+                    if (cls[u] == 0) dst[u] = a0 + r0;
+                    else if (cls[u] == 1) dst[u] = r1 < tl ? a0 + (mL - tl) + r1 : a0 + mL + (r1 - tl);
+                    else dst[u] = a0 + mL + (tn - tl) + ((e - a0) - r0 - r1);
+                    const uint32_t add = cls[u] == 0 ? 1u : (cls[u] == 1 ? 65536u : 0u);
+                    if (k == 0) pre[0] += add; else if (k == 1) pre[1] += add; else if (k == 2) pre[2] += add; else pre[3] += add;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < PER; ++u)
+                if ((unsigned)dst[u] < (unsigned)m) s_val[dst[u]] = val[u];
+            __syncthreads();
+        }
+#else
         // large sub-nodes: block-wide bitonic sort of (sub-node, coordinate, element) keys
         // (7 + 32 + log2(kLocalMax) bits), kLocalMax / 512 per thread in registers; only the stages with partners
         // in another wave go through LDS
@@ -724,6 +868,7 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
             }
             __syncthreads();
         }
+#endif
     }
     for (int e = tid; e < m; e += kLocalThreads) t.perm[cl.off + A + e] = s_val[e];
 }
