@@ -15,6 +15,8 @@
 // inflated by a few ulps so the f32 boxes bound the f64 points they stand for.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "tree.hpp"
 #include "wave.hpp"
 
@@ -72,25 +74,74 @@ __global__ __launch_bounds__(256) void k_tree_bbox(TreeView t, int level) {
         for (int d = 0; d < D; ++d) { lo[d] = 0xffffffffu; hi[d] = 0u; }
     }
     const long long key = valid ? ((long long)c << 32) | (unsigned)node : -1;
+    // a wave whose samples all fall in one node (the common case: nodes of the global
+    // levels span thousands of positions) reduces with DPP / permlane butterflies; a wave
+    // spanning several nodes, by a segmented shuffle reduction
+    const long long key0 = ((long long)__builtin_amdgcn_readfirstlane((int)(key >> 32)) << 32) |
+                           (unsigned)__builtin_amdgcn_readfirstlane((int)key);
+    const bool uniform = __ballot(key == key0) == ~0ull;
+    bool head;
+    if (uniform) {
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const long long ok = __shfl_down(key, o, 64);
-        const bool same = (lane + o < 64) && ok == key;
+        for (int o = 1; o < 64; o <<= 1) {
 #pragma unroll
-        for (int d = 0; d < D; ++d) {
-            const uint32_t ol = __shfl_down(lo[d], o, 64);
-            const uint32_t oh = __shfl_down(hi[d], o, 64);
-            if (same) { lo[d] = min(lo[d], ol); hi[d] = max(hi[d], oh); }
+            for (int d = 0; d < D; ++d) {
+                lo[d] = min(lo[d], xor_lane(lo[d], o));
+                hi[d] = max(hi[d], xor_lane(hi[d], o));
+            }
+        }
+        head = (int)valid & (int)(lane == 0);
+    } else {
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const long long ok = __shfl_down(key, o, 64);
+            const bool same = (lane + o < 64) && ok == key;
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                const uint32_t ol = __shfl_down(lo[d], o, 64);
+                const uint32_t oh = __shfl_down(hi[d], o, 64);
+                if (same) { lo[d] = min(lo[d], ol); hi[d] = max(hi[d], oh); }
+            }
+        }
+        const long long prev = __shfl_up(key, 1, 64);
+        head = valid && (lane == 0 || prev != key);
+    }
+    // the block's waves combine in LDS first (the block's samples span at most a few nodes):
+    // one global atomic per node, dimension and block instead of one per wave
+    __shared__ uint32_t s_lo[4][D], s_hi[4][D];
+    __shared__ long long s_key0;
+    if (threadIdx.x < 4 * D) {
+        s_lo[threadIdx.x / D][threadIdx.x % D] = 0xffffffffu;
+        s_hi[threadIdx.x / D][threadIdx.x % D] = 0u;
+    }
+    if (threadIdx.x == 0) s_key0 = key;  // (the block's first sample: the smallest key)
+    __syncthreads();
+    const long long k0 = s_key0;
+    const int slot = (k0 >= 0 && valid && (key >> 32) == (k0 >> 32)) ? node - (int)(unsigned)k0 : 4;
+    if (head) {
+        if ((unsigned)slot < 4u) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                atomicMin(&s_lo[slot][d], lo[d]);
+                atomicMax(&s_hi[slot][d], hi[d]);
+            }
+        } else {
+            const size_t base = ((size_t)c * t.nnodes + tree_heap(level, node)) * D;
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                atomicMin(&t.blo[base + d], lo[d]);
+                atomicMax(&t.bhi[base + d], hi[d]);
+            }
         }
     }
-    const long long prev = __shfl_up(key, 1, 64);
-    const bool head = valid && (lane == 0 || prev != key);
-    if (head) {
-        const size_t base = ((size_t)c * t.nnodes + tree_heap(level, node)) * D;
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            atomicMin(&t.blo[base + d], lo[d]);
-            atomicMax(&t.bhi[base + d], hi[d]);
+    __syncthreads();
+    if ((int)(threadIdx.x < 4 * D) & (int)(k0 >= 0)) {
+        const int sl = threadIdx.x / D, d = threadIdx.x % D;
+        if (s_lo[sl][d] <= s_hi[sl][d]) {
+            const int c0 = (int)(k0 >> 32), n0 = (int)(unsigned)k0 + sl;
+            const size_t base = ((size_t)c0 * t.nnodes + tree_heap(level, n0)) * D;
+            atomicMin(&t.blo[base + d], s_lo[sl][d]);
+            atomicMax(&t.bhi[base + d], s_hi[sl][d]);
         }
     }
 }
@@ -666,28 +717,35 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
         __syncthreads();
         const int max_sub = (m + nsub - 1) / nsub + 1;  // sub-node sizes differ by <= 1
         if (max_sub <= 64 * kWaveSortPer) {
-            // small sub-nodes: one wave sorts each in registers, (coordinate, point) keys
+            // small sub-nodes: one wave sorts each in registers, (coordinate, point) keys, in a
+            // network of the sub-node's size (128, 256 or 512 keys)
             const int lane = tid & 63, wv = tid >> 6;
-            for (int k = wv; k < nsub; k += kLocalThreads / 64) {
-                const int a0 = tree_first(n, l, (i << r) + k) - A, a1 = tree_first(n, l, (i << r) + k + 1) - A;
-                const int bd = s_best[k];
-                unsigned long long key[kWaveSortPer];
+            auto wave_level = [&](auto per_tag) {
+                constexpr int PER = decltype(per_tag)::value;
+                for (int k = wv; k < nsub; k += kLocalThreads / 64) {
+                    const int a0 = tree_first(n, l, (i << r) + k) - A, a1 = tree_first(n, l, (i << r) + k + 1) - A;
+                    const int bd = s_best[k];
+                    unsigned long long key[PER];
 #pragma unroll
-                for (int u = 0; u < kWaveSortPer; ++u) {
-                    const int e = a0 + lane * kWaveSortPer + u;
-                    key[u] = ~0ull;
-                    if (e < a1) {
-                        const int p = s_val[e];
-                        key[u] = ((unsigned long long)ord_bits(t.vec[tree_in_ix(t, bd, cl.off + p)]) << 32) | (unsigned)p;
+                    for (int u = 0; u < PER; ++u) {
+                        const int e = a0 + lane * PER + u;
+                        key[u] = ~0ull;
+                        if (e < a1) {
+                            const int p = s_val[e];
+                            key[u] = ((unsigned long long)ord_bits(t.vec[tree_in_ix(t, bd, cl.off + p)]) << 32) | (unsigned)p;
+                        }
+                    }
+                    wave_sort_keys<PER>(key);
+#pragma unroll
+                    for (int u = 0; u < PER; ++u) {
+                        const int e = a0 + lane * PER + u;
+                        if (e < a1) s_val[e] = (int32_t)(unsigned)key[u];
                     }
                 }
-                wave_sort_keys<kWaveSortPer>(key);
-#pragma unroll
-                for (int u = 0; u < kWaveSortPer; ++u) {
-                    const int e = a0 + lane * kWaveSortPer + u;
-                    if (e < a1) s_val[e] = (int32_t)(unsigned)key[u];
-                }
-            }
+            };
+            if (max_sub <= 128) wave_level(std::integral_constant<int, 2>{});
+            else if (max_sub <= 256) wave_level(std::integral_constant<int, 4>{});
+            else wave_level(std::integral_constant<int, kWaveSortPer>{});
             __syncthreads();
             continue;
         }
