@@ -21,6 +21,7 @@ def _port():
     return p
 
 
+@pytest.mark.timeout(900)  # (a fresh box's first `import torch` alone can take minutes)
 def test_two_rank_bench_equals_one_rank(tmp_path):
     common = ["--steps", "1", "--warmup", "0", "--workload", "C3", "--cpu-baseline", "off"]
     one = tmp_path / "one.npy"
