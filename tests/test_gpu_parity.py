@@ -469,3 +469,37 @@ def test_lrf_fast_path_equals_exact_kernel(se3icp_mod, k, kind):
     same_f = (fast_f.view(np.uint64) == ex_f.view(np.uint64)).reshape(len(pts), -1).all(axis=1)
     assert same_f.all(), np.nonzero(~same_f)[0][:8]
     assert np.array_equal(fast_n.view(np.uint64), ex_n.view(np.uint64))
+
+
+@pytest.mark.parametrize("kind", ["duplicates", "tiny", "collinear"])
+def test_degenerate_clouds_knn_and_frames(se3icp_mod, refcpu, kind):
+    """Tree build and kNN on degenerate inputs: many exactly repeated points (median splits
+    through runs of equal keys, zero-variance sub-nodes), a cloud smaller than one leaf,
+    and points on a line (two dimensions without extent).  kNN distances equal the oracle's
+    (sets may differ only inside exact-distance ties), and the fast kernel's frames and
+    normals equal the exact kernel's bit for bit."""
+    from se3icp import registration
+    rng = np.random.default_rng(11)
+    if kind == "duplicates":
+        base = rng.standard_normal((60, 3))
+        pts = base[rng.integers(0, 60, 3000)] + 0.0
+    elif kind == "tiny":
+        pts = rng.standard_normal((40, 3))
+    else:
+        t = np.sort(rng.random(5000))
+        pts = np.stack([t, 2.0 * t, -t], axis=1)
+    k = min(30, len(pts))
+    g = se3icp_mod.knn_self(pts, k)
+    ri, rd = refcpu.knn_self(pts, k)
+    dg = np.sum((pts[g] - pts[:, None, :]) ** 2, axis=2)
+    np.testing.assert_allclose(np.sort(dg, axis=1), rd, rtol=0, atol=1e-12)
+    fast_f = se3icp_mod.toldi_frames(pts, k)
+    fast_n = se3icp_mod.estimate_normals(pts, k)
+    registration.set_lrf_exact(True)
+    try:
+        ex_f = se3icp_mod.toldi_frames(pts, k)
+        ex_n = se3icp_mod.estimate_normals(pts, k)
+    finally:
+        registration.set_lrf_exact(False)
+    assert np.array_equal(fast_f.view(np.uint64), ex_f.view(np.uint64))
+    assert np.array_equal(fast_n.view(np.uint64), ex_n.view(np.uint64))
