@@ -174,7 +174,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
                                              const CloudSetup* __restrict__ setup,
                                              const CloudDev* __restrict__ clouds, const float* __restrict__ tlo,
                                              const float* __restrict__ thi, const int32_t* __restrict__ qlist,
-                                             const int32_t* __restrict__ qcount) {
+                                             const int32_t* __restrict__ qcount, int qpw) {
     __shared__ double s_d[kWaves][kBuf];
     __shared__ int s_i[kWaves][kBuf];
     // the queries' sorted neighbour lists: dynamic LDS, kQ x v.kmax ints per wave, sized to
@@ -197,8 +197,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
     // slots qlist[0 .. *qcount-1], the grid striding over them
     const int nvq = qlist ? *qcount : v.npts;
     auto qslot = [&](int i) __attribute__((always_inline)) { return qlist ? qlist[i] : i; };
-    for (int vb = bid; vb * kWaves * kQ < nvq; vb += (int)gridDim.x) {
-    const int w0 = __builtin_amdgcn_readfirstlane((vb * kWaves + wid) * kQ);
+    // (list mode: qpw <= kQ queries per wave, the slots j >= qpw of a wave left empty, so
+    // that the few handed-over queries spread over more waves)
+    for (int vb = bid; vb * kWaves * qpw < nvq; vb += (int)gridDim.x) {
+    const int w0 = __builtin_amdgcn_readfirstlane((vb * kWaves + wid) * qpw);
     const TreeRef T = v.t3;
     double* bd = s_d[wid];
     int* bi = s_i[wid];
@@ -223,7 +225,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
 #endif
 
     for (int j = 0; j < kQ; ++j) {
-        if (w0 + j >= nvq) break;
+        if ((j >= qpw) | (w0 + j >= nvq)) break;
         const int w = qslot(w0 + j);
         const int c = cloud_of[w];
         const CloudSetup st = setup[c];
@@ -576,7 +578,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
         static_assert(kWaves * kQ <= 64, "one lane per query of the block");
         double* pb = &s_park[lane < kWaves * kQ ? lane / kQ : 0][lane % kQ][0];
         const int b_flags = lane < kWaves * kQ ? (int)pb[PK_FLAGS] : 0;
-        const int wb = b_flags ? qslot(vb * kWaves * kQ + lane) : 0;  // the query's tree slot
+        const int wb = b_flags ? qslot((vb * kWaves + lane / kQ) * qpw + lane % kQ) : 0;  // the query's tree slot
         d3 zn{0, 0, 0};
         if ((b_flags & 1) && wid == 0) {
             // C = sum over ranks 1..rz of (v - cl)(v - cl)^T with the quirk centroid
@@ -677,7 +679,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
         const double* pb = &s_park[lane < kWaves * kQ ? lane / kQ : 0][lane % kQ][0];
         const int b_flags = lane < kWaves * kQ ? (int)pb[PK_FLAGS] : 0;
         if (b_flags & 1) {
-            const int w = qslot(vb * kWaves * kQ + lane);
+            const int w = qslot((vb * kWaves + lane / kQ) * qpw + lane % kQ);
             const CloudSetup st = v.setup[v.cloud_of[w]];
             const double qx = TX[w], qy = TY[w], qz = TZ[w];
             d3 nrm{pb[PK_ZN], pb[PK_ZN + 1], pb[PK_ZN + 2]};
@@ -716,14 +718,20 @@ void launch_lrf(const View& v, int write_knn, hipStream_t s) {
     const int nw = (v.npts + kQ - 1) / kQ;
     const size_t lds = sizeof(int) * (size_t)kWaves * kQ * v.kmax;
     hipLaunchKernelGGL(k_lrf, dim3((nw + kWaves - 1) / kWaves), dim3(64 * kWaves), lds, s, v, write_knn, v.cloud_of,
-                       v.setup, v.clouds, v.t3.lo, v.t3.hi, nullptr, nullptr);
+                       v.setup, v.clouds, v.t3.lo, v.t3.hi, nullptr, nullptr, kQ);
 }
 
+#ifndef SE3ICP_LRF_LIST_QPW
+#define SE3ICP_LRF_LIST_QPW 4  // queries per wave of the hand-over pass (measured: 1, 2, 4, 8)
+#endif
+#ifndef SE3ICP_LRF_LIST_BLOCKS
+#define SE3ICP_LRF_LIST_BLOCKS 1024
+#endif
 void launch_lrf_list(const View& v, const int32_t* qlist, const int32_t* qcount, hipStream_t s) {
     const size_t lds = sizeof(int) * (size_t)kWaves * kQ * v.kmax;
-    const int nblk = std::max(1, std::min(1024, (v.npts + kWaves * kQ - 1) / (kWaves * kQ)));
+    const int nblk = std::max(1, std::min(SE3ICP_LRF_LIST_BLOCKS, (v.npts + kWaves * kQ - 1) / (kWaves * kQ)));
     hipLaunchKernelGGL(k_lrf, dim3(nblk), dim3(64 * kWaves), lds, s, v, 0, v.cloud_of, v.setup, v.clouds, v.t3.lo,
-                       v.t3.hi, qlist, qcount);
+                       v.t3.hi, qlist, qcount, SE3ICP_LRF_LIST_QPW);
 }
 
 }  // namespace se3icp
