@@ -48,6 +48,9 @@ constexpr int kWaves = 4;
 #ifndef SE3ICP_NN_COMPACT
 #define SE3ICP_NN_COMPACT 40
 #endif
+#ifndef SE3ICP_NN_SEED
+#define SE3ICP_NN_SEED 1  // first searches seeded by a greedy tree descent (and this many leaf targets)
+#endif
 
 // packed f32 pairs: v_pk_add_f32 / v_pk_fma_f32 issue two lanes' worth of f32 math per
 // instruction (the f32 vector peak of gfx950 assumes them)
@@ -285,6 +288,48 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
         m = (float)(SE3ICP_NN_EXPAND * sqrt(a2 * rot_frob2(T, Tp) + dt * dt));
     }
     v.nn_margin[g] = m;
+#if SE3ICP_NN_SEED
+    // No previous match (a pair's first search): seed one from a greedy descent of the
+    // target tree (the child whose f32 box bound is smaller, down to a leaf; a target of
+    // that leaf).  The search only uses it for its first pruning threshold, so any target
+    // is valid; a near one spares the group walk the nodes an infinite threshold opens.
+    if ((int)(v.corr_idx[g] < 0) & (int)(ct.n > 0)) {
+        double m0[D], Q[D];
+        load_m0<D>(v, TR, gx, m0);
+        pose_m0<D>(T, m0, Q);
+        float qf[D];
+#pragma unroll
+        for (int r = 0; r < D; ++r) qf[r] = (float)((D == 3) ? Q[r] - P->f32_center[r] : Q[r]);
+        const float* lo = TR.lo + (size_t)P->tgt * TR.nnodes * D;
+        const float* hi = TR.hi + (size_t)P->tgt * TR.nnodes * D;
+        int h = 0;
+        for (int lv = 0; lv < TR.L; ++lv) {
+            const int a = 2 * h + 1;
+            const float la = box_lb<D>(lo + (size_t)a * D, hi + (size_t)a * D, qf);
+            const float lb = box_lb<D>(lo + (size_t)(a + 1) * D, hi + (size_t)(a + 1) * D, qf);
+            h = la <= lb ? a : a + 1;
+        }
+        const int li = h - ((1 << TR.L) - 1);
+        const int ta = min(tree_first(ct.n, TR.L, li), ct.n - 1);
+        const int cnt = max(tree_first(ct.n, TR.L, li + 1) - ta, 1);
+        // the nearest of SE3ICP_NN_SEED targets spread over the leaf
+        const float* tv = TR.tvec + ct.off;
+        int best = ta;
+        float bd = INFINITY;
+        for (int k = 0; k < SE3ICP_NN_SEED; ++k) {
+            const int t = ta + (2 * k + 1) * cnt / (2 * SE3ICP_NN_SEED);
+            float d = 0.f;
+#pragma unroll
+            for (int r = 0; r < D; ++r) {
+                const float e = qf[r] - tv[(size_t)r * v.ld + t];
+                d = fmaf(e, e, d);
+            }
+            best = d < bd ? t : best;
+            bd = fminf(d, bd);
+        }
+        v.corr_idx[g] = TR.perm[ct.off + best];
+    }
+#endif
     return false;
 }
 
