@@ -55,6 +55,12 @@ constexpr int kCap = SE3ICP_LRF8_CAP;  // candidates buffered per query (u32: cu
 #ifndef SE3ICP_LRF8_SELECT
 #define SE3ICP_LRF8_SELECT 0  // bound of a tightening: 0 sorts; 1 (lists over 128) / 2 (always) a counting select (A/B: +11 % / +10 % k_lrf8)
 #endif
+#ifndef SE3ICP_LRF8_MERGE
+#define SE3ICP_LRF8_MERGE 1  // tightenings keep the list sorted: sort only the tail appended since, merge (0: sort the whole list each time)
+#endif
+#ifndef SE3ICP_LRF8_FINAL32
+#define SE3ICP_LRF8_FINAL32 1  // final rank order: u32 entry sort + odd-even fix-up of the full keys (0: a 64-bit network)
+#endif
 #ifndef SE3ICP_LRF8_LEAF_BITS
 #define SE3ICP_LRF8_LEAF_BITS 6
 #endif
@@ -180,22 +186,32 @@ __device__ __forceinline__ unsigned list_kth(const unsigned* list, int nbg, int 
     sort8<PER>(k, l);
     return rank_key(k, l, r);
 }
-// sort the run list[0 .. len) (len <= 128) in place
+// sort the run list[0 .. len) (len <= 8 * PER) in place
+template <int PER = 16>
 __device__ __forceinline__ void sort_run(unsigned* list, int len, int l) {
-    unsigned k[16];
+    unsigned k[PER];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-        const int e = l * 16 + s;
+    for (int s = 0; s < PER; ++s) {
+        const int e = l * PER + s;
         k[s] = e < len ? list[e] : kPad;
     }
-    sort8<16>(k, l);
+    sort8<PER>(k, l);
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-        const int e = l * 16 + s;
+    for (int s = 0; s < PER; ++s) {
+        const int e = l * PER + s;
         if (e < len) list[e] = k[s];
     }
     __builtin_amdgcn_wave_barrier();
+}
+// number of entries <= t in the sorted run A[0 .. n)
+__device__ __forceinline__ int upper_count(const unsigned* A, int n, unsigned t) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (A[m] <= t) lo = m + 1; else hi = m;
+    }
+    return lo;
 }
 // entry of rank r of the union of two sorted runs A (na) and B (nb) (distinct entries):
 // i entries of A and r+1-i of B are the r+1 smallest; binary search on i
@@ -287,6 +303,69 @@ __device__ __forceinline__ uint2 tighten_group(unsigned* lists, int g, int l, in
     return make_uint2(tg, keep_n);
 }
 
+// Bound tightening over a list whose first mv entries are already sorted (the kept set of
+// the previous tightening): only the tail appended since is sorted, the Kw-th entry is
+// found by a merge-path search of the two runs, and the kept parts of both runs are merged
+// by a bitonic half-cleaner network (A ascending, padding, B descending: one bitonic
+// sequence of 128), so the kept list stays sorted for the next tightening.
+//   presort (wave-uniform): some list has no sorted prefix (the first tightening) or a
+//           tail over 128: list[0 .. min(nbg, 128)) is sorted first;
+//   tail_per (wave-uniform): 0 every tail empty, 8 every tail <= 64 entries, else 16.
+// Returns (bound, kept, new sorted prefix) for the group; kept sets over 128 entries (ties
+// at the bound) are compacted unmerged (prefix 0).
+__device__ __forceinline__ uint3 tighten_group_sorted(unsigned* lists, int g, int l, int nbg, int mv, int nmax, int Kw,
+                                                      bool presort, int tail_per) {
+    unsigned* list = lists + g * kCap;
+    if (presort) {
+        mv = min(nbg, 128);
+        sort_run<16>(list, mv, l);
+    }
+    const int nb = nbg - mv;
+    unsigned* B = list + mv;
+    if (tail_per == 8) sort_run<8>(B, nb, l);
+    else if (tail_per == 16) sort_run<16>(B, nb, l);
+    const unsigned tg = nbg >= Kw ? (kth_of_two(list, mv, B, nb, Kw - 1) | kIdBits) : kPad;
+    const int ka = upper_count(list, mv, tg), kb = upper_count(B, nb, tg);
+    const int kept = ka + kb;
+    if (__ballot(kept > 128) == 0ull) {
+        unsigned k[16];
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            const int e = l * 16 + s;
+            k[s] = e < ka ? list[e] : (e >= 128 - kb ? B[127 - e] : kPad);
+        }
+        __builtin_amdgcn_wave_barrier();
+        stage8<16, 128, 64>(k, l);
+        stage8<16, 128, 32>(k, l);
+        stage8<16, 128, 16>(k, l);
+        stage8<16, 128, 8>(k, l);
+        stage8<16, 128, 4>(k, l);
+        stage8<16, 128, 2>(k, l);
+        stage8<16, 128, 1>(k, l);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            const int e = l * 16 + s;
+            if (e < kept) list[e] = k[s];
+        }
+        __builtin_amdgcn_wave_barrier();
+        return make_uint3(tg, (unsigned)kept, (unsigned)kept);
+    }
+    // (rare) stable compaction in place, as tighten_group
+    unsigned keep_n = 0;
+    for (int r0 = 0; r0 < nmax; r0 += 8) {
+        const int e = r0 + l;
+        const unsigned ent = e < nbg ? list[e] : kPad;
+        const bool keep = ent <= tg;
+        const unsigned long long m = __ballot(keep);
+        const unsigned gm = (unsigned)(m >> (8 * g)) & 0xffu;
+        __builtin_amdgcn_wave_barrier();
+        if (keep) list[(int)keep_n + __popc(gm & ((1u << l) - 1u))] = ent;
+        keep_n += (unsigned)__popc(gm);
+        __builtin_amdgcn_wave_barrier();
+    }
+    return make_uint3(tg, keep_n, 0u);
+}
+
 // point of a list entry: the wave's leaf list holds leaf indices, the id (list index << 6 |
 // lane) picks the point
 __device__ __forceinline__ int entry_slot(unsigned ent, const int* leaves, int off, int n, int L) {
@@ -376,6 +455,64 @@ __device__ __forceinline__ bool final_group(unsigned* lists, const int* leaves, 
                                             int nbg, int kk, int kn, bool want_t, bool want_n) {
     unsigned* list = lists + g * kCap;
     unsigned long long k[16];
+#if SE3ICP_LRF8_FINAL32
+    // The list entries (cut key | id) sorted as u32 give the rank order up to runs whose
+    // full keys the cut does not separate; the (full key << 32 | point index) keys of that
+    // order are put right by three odd-even transposition passes, and the result is
+    // checked: a list still out of order goes to the exact kernel.
+    bool unsorted = false;
+    {
+        unsigned k32[16];
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            const int e = l * 16 + s;
+            k32[s] = e < nbg ? list[e] : kPad;
+        }
+        sort8<16>(k32, l);
+#pragma unroll
+        for (int s = 0; s < 16; ++s) {
+            const int e = l * 16 + s;
+            unsigned long long x = ~0ull;
+            if (e < nbg) {
+                const int slot = entry_slot(k32[s], leaves, off, n, L);
+                const unsigned key = f32_up_bits(l2_3(qx, qy, qz, TX[slot], TY[slot], TZ[slot]));
+                x = ((unsigned long long)key << 32) | (unsigned)perm[slot];
+            }
+            k[s] = x;
+        }
+    }
+    auto ce = [](unsigned long long& a, unsigned long long& b) __attribute__((always_inline)) {
+        const bool sw = b < a;
+        const unsigned long long lo = sw ? b : a, hi = sw ? a : b;
+        a = lo;
+        b = hi;
+    };
+    auto odd_pass = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int s = 1; s + 1 < 16; s += 2) ce(k[s], k[s + 1]);
+        // (lane l's last, lane l+1's first) within the group of eight
+        const int me = (int)(threadIdx.x & 63);
+        const unsigned long long nx = ((unsigned long long)(unsigned)__shfl((int)(unsigned)(k[0] >> 32), me + 1, 64) << 32) |
+                                      (unsigned)__shfl((int)(unsigned)k[0], me + 1, 64);
+        const unsigned long long pv = ((unsigned long long)(unsigned)__shfl((int)(unsigned)(k[15] >> 32), me - 1, 64) << 32) |
+                                      (unsigned)__shfl((int)(unsigned)k[15], me - 1, 64);
+        if (l < 7 && nx < k[15]) k[15] = nx;
+        if (l > 0 && k[0] < pv) k[0] = pv;
+    };
+#pragma unroll
+    for (int s = 0; s < 16; s += 2) ce(k[s], k[s + 1]);
+    odd_pass();
+#pragma unroll
+    for (int s = 0; s < 16; s += 2) ce(k[s], k[s + 1]);
+    {
+        const int me = (int)(threadIdx.x & 63);
+        const unsigned long long nx = ((unsigned long long)(unsigned)__shfl((int)(unsigned)(k[0] >> 32), me + 1, 64) << 32) |
+                                      (unsigned)__shfl((int)(unsigned)k[0], me + 1, 64);
+#pragma unroll
+        for (int s = 0; s + 1 < 16; ++s) unsorted |= k[s + 1] < k[s];
+        unsorted |= (l < 7) && nx < k[15];
+    }
+#else
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
         const int e = l * 16 + s;
@@ -388,6 +525,7 @@ __device__ __forceinline__ bool final_group(unsigned* lists, const int* leaves, 
         k[s] = x;
     }
     net8_64<16, 128>(k, l);
+#endif
     // Two of the first lim = min(nbg, max(kk, kn) + 1) ranks sharing an f32 key must also
     // share the f64 distance (then both orders fall back to the index): the (key, index)
     // order is then the exact (f64 d, index) order of the reference's kNN and of the exact
@@ -420,6 +558,9 @@ __device__ __forceinline__ bool final_group(unsigned* lists, const int* leaves, 
         const int a = (int)list[e], b = (int)list[e + 1];
         bad |= l2_3(qx, qy, qz, TX[a], TY[a], TZ[a]) != l2_3(qx, qy, qz, TX[b], TY[b], TZ[b]);
     }
+#if SE3ICP_LRF8_FINAL32
+    bad |= unsorted;
+#endif
     const bool ok = !(bool)(unsigned)((__ballot(bad) >> (8 * g)) & 0xffull);
     return ok;
 }
@@ -508,6 +649,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
     // the list length of the lane's own group g, kept alongside (picking nbq[g] at run time
     // would turn the register arrays into scratch memory)
     unsigned nbv = 0u;
+    int mvv = 0;  // (SE3ICP_LRF8_MERGE) sorted prefix of the group's list
     double* qv = &s_q[wid][0][0];
     float fqlo[3] = {0.f, 0.f, 0.f}, fqhi[3] = {0.f, 0.f, 0.f};
     int nlist = 0;
@@ -543,7 +685,23 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
 #pragma unroll
         for (int j = 0; j < kQ; ++j) nmax = max(nmax, nbq[j]);
         __builtin_amdgcn_wave_barrier();
+#if SE3ICP_LRF8_MERGE
+        int dmax = 0;
+        bool anyz = false;
+#pragma unroll
+        for (int j = 0; j < kQ; ++j) {
+            const int mj = __builtin_amdgcn_readlane(mvv, 8 * j);
+            dmax = max(dmax, (int)nbq[j] - mj);
+            anyz |= mj == 0;
+        }
+        const bool presort = anyz || dmax > 128;
+        const int tail_per = presort ? (nmax <= 128 ? 0 : 8) : (dmax == 0 ? 0 : dmax <= 64 ? 8 : 16);
+        const uint3 r3 = tighten_group_sorted(lists, g, l, (int)nbv, mvv, (int)nmax, Kw, presort, tail_per);
+        const uint2 r = make_uint2(r3.x, r3.y);
+        mvv = (int)r3.z;
+#else
         const uint2 r = tighten_group(lists, g, l, (int)nbv, (int)nmax, Kw);
+#endif
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int j = 0; j < kQ; ++j) {

@@ -175,6 +175,9 @@ __device__ __forceinline__ void compact_sweep(const float4* tile, const float4* 
 #ifndef SE3ICP_NN_SMALL
 #define SE3ICP_NN_SMALL 4  // groups of at most this many queries are searched one query at a time
 #endif
+#ifndef SE3ICP_NN_TWOLEVEL
+#define SE3ICP_NN_TWOLEVEL 0  // (A/B: SE(3) NN +1 %, kept off) k_nn_group: an interior node whose children are interior pushes its four grandchildren in one step (one box-load round trip per two levels)
+#endif
 #ifndef SE3ICP_NN_SINGLE_BLOCKS
 #define SE3ICP_NN_SINGLE_BLOCKS 4096  // grid of the one-query-per-wave kernels (4 waves per block, grid-strided)
 #endif
@@ -716,6 +719,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_W
             if ((int)valid & (int)(d1 < INFINITY)) thr = fminf(thr, widen(d1, d2));
             continue;
         }
+#if SE3ICP_NN_TWOLEVEL
+        if (2 * h + 2 < first_leaf) {
+            // Both children are interior: test the four grandchildren (4h+3 .. 4h+6, one
+            // contiguous box run) instead, so the wave's dependent chain of box loads is one
+            // round trip per two levels.  A child's box lies inside its parent's, so a
+            // grandchild that passes implies its parent would have; exactness is unchanged
+            // (pruning stays conservative, leaves are re-tested when popped).
+            n_box += 4;
+            const int g0 = 4 * h + 3;
+            float lg[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if constexpr (D == 12) lg[k] = box_lb12(box_lo + (size_t)(g0 + k) * D, box_hi + (size_t)(g0 + k) * D, q2);
+                else lg[k] = box_lb<D>(box_lo + (size_t)(g0 + k) * D, box_hi + (size_t)(g0 + k) * D, q);
+            }
+            bool vg[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) vg[k] = __ballot(lg[k] * (1.f - 2e-6f) < thr) != 0ull;
+            // near-first order by lane 0's bounds: the nearer child (min of its two
+            // grandchildren), within it the nearer grandchild; pushed far-first (LIFO)
+            const int o = __builtin_amdgcn_readfirstlane(((fminf(lg[0], lg[1]) <= fminf(lg[2], lg[3])) ? 0 : 2) |
+                                                         ((lg[0] <= lg[1]) ? 0 : 4) | ((lg[2] <= lg[3]) ? 0 : 8));
+            const int cn = o & 2, cf = 2 - cn;  // first grandchild index of the near / far child
+            const int fn = (cn == 0) ? ((o >> 2) & 1) : ((o >> 3) & 1);  // near child's nearer grandchild (0/1)
+            const int ff = (cf == 0) ? ((o >> 2) & 1) : ((o >> 3) & 1);
+            const int order[4] = {cf + 1 - ff, cf + ff, cn + 1 - fn, cn + fn};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int gk = order[k];
+                const bool vk = gk == 0 ? vg[0] : gk == 1 ? vg[1] : gk == 2 ? vg[2] : vg[3];
+                if (vk) { stk = (lane == sp) ? g0 + gk : stk; ++sp; }
+            }
+            continue;
+        }
+#endif
         n_box += 2;
         const int hl = 2 * h + 1, hr = 2 * h + 2;
         float ll, lr;
