@@ -92,6 +92,8 @@ int Engine::init() {
     if (hipGetDeviceCount(&n) != hipSuccess || dev_ < 0 || dev_ >= n) return SE3ICP_ERR_NO_DEVICE;
     HIPCHK(hipSetDevice(dev_));
     HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
+    if (const char* e = std::getenv("SE3ICP_LRF_SPLIT")) lrf_split_ = std::max(0, std::min(99, std::atoi(e)));
     for (auto& e : ev_) HIPCHK(hipEventCreate(&e));
     for (auto& e : loop_ev_) HIPCHK(hipEventCreate(&e));
     if (const char* e = std::getenv("SE3ICP_L12_EXTRA")) l12_extra_ = std::max(0, std::min(2, std::atoi(e)));
@@ -108,7 +110,7 @@ Engine::~Engine() {
                      &d_corr_idx_, &d_corr_dist_, &d_flag_list_, &d_flag_count_, &d_trim_key_, &d_red_partial_,
                      &d_red_out_, &d_work_, &d_wb_, &d_wn_, &d_chunks_, &d_partial_, &d_centers_,
                      &d_rechecked_, &d_keys0_, &d_vals1_, &d_sort_tmp_, &d_stats_,
-                     &d_qlist_, &d_qcount_, &d_hist_, &d_cert_d1_, &d_cert_l2_, &d_cert_it_, &d_margin_, &d_sqlist_, &d_state_, &d_trim_cand_, &d_trim_ctr_, &d_scales_, &d_trim_hist_,
+                     &d_qlist_, &d_qcount_, &d_chunk_cost_, &d_chunk_order_, &d_hist_, &d_cert_d1_, &d_cert_l2_, &d_cert_it_, &d_margin_, &d_sqlist_, &d_state_, &d_trim_cand_, &d_trim_ctr_, &d_scales_, &d_trim_hist_,
                      &d_lrf_fb_, &d_lrf_fbn_,
                      &t3_.perm, &t3_.pos, &t3_.vec, &t3_.blo, &t3_.bhi, &t3_.lo, &t3_.hi,
                      &t12_.perm, &t12_.pos, &t12_.vec, &t12_.blo, &t12_.bhi, &t12_.lo, &t12_.hi};
@@ -126,6 +128,7 @@ Engine::~Engine() {
         if (e) (void)hipEventDestroy(e);
     if (h_state_) (void)hipHostFree(h_state_);
     if (h_phase_) (void)hipHostFree(h_phase_);
+    if (side_) (void)hipStreamDestroy(side_);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -220,6 +223,8 @@ View Engine::view() const {
     v.nchunks = nchunks_;
     v.qlist = (int32_t*)d_qlist_.p;
     v.qcount = (int32_t*)d_qcount_.p;
+    v.chunk_cost = (uint32_t*)d_chunk_cost_.p;
+    v.chunk_order = (int32_t*)d_chunk_order_.p;
     v.sq_list = (int32_t*)d_sqlist_.p;
     v.hist = (const double*)d_hist_.p;
     v.cert_d1 = (float*)d_cert_d1_.p;
@@ -376,13 +381,32 @@ int Engine::setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool nor
             // waves aligned to each cloud's first point (results independent of the batch)
             std::vector<int32_t> wb(nclouds_ + 1, 0);
             for (int c = 0; c < nclouds_; ++c) wb[c + 1] = wb[c] + (h_clouds_[c].n + 7) / 8;
-            if (!ensure<int32_t>(d_lrf_fb_, (size_t)ld_) || !ensure<int32_t>(d_lrf_fbn_, 2 + nclouds_ + 1))
+            const int nw = wb[nclouds_];
+            if (!ensure<int32_t>(d_lrf_fb_, (size_t)8 * nw + 64) || !ensure<int32_t>(d_lrf_fbn_, 2 + nclouds_ + 1))
                 return SE3ICP_ERR_OUT_OF_MEMORY;
             int32_t* d_wb = (int32_t*)d_lrf_fbn_.p + 2;
-            HIPCHK(hipMemsetAsync(d_lrf_fbn_.p, 0, sizeof(int32_t), s));
+            int32_t* fb = (int32_t*)d_lrf_fb_.p;
+            int32_t* fbn = (int32_t*)d_lrf_fbn_.p;
+            HIPCHK(hipMemsetAsync(fbn, 0, 2 * sizeof(int32_t), s));
             HIPCHK(hipMemcpyAsync(d_wb, wb.data(), sizeof(int32_t) * (nclouds_ + 1), hipMemcpyHostToDevice, s));
-            launch_lrf8(v, d_wb, wb[nclouds_], (int32_t*)d_lrf_fb_.p, (int32_t*)d_lrf_fbn_.p, s);
-            launch_lrf_list(v, (const int32_t*)d_lrf_fb_.p, (const int32_t*)d_lrf_fbn_.p, s);
+            // The exact pass is latency-bound (a few thousand queries, one wave each) and
+            // k_lrf8 issue-bound: the first lrf_split_ % of the waves' hand-overs are
+            // resolved on the side stream while k_lrf8 runs the rest; the last part's
+            // hand-overs (one query per wave) close the setup's kNN on the main stream.
+            const int nwa = lrf_split_ > 0 ? (int)((long long)nw * lrf_split_ / 100) : nw;
+            launch_lrf8(v, d_wb, 0, nwa, fb, fbn, s);
+            if (nwa < nw && nwa > 0) {
+                HIPCHK(hipEventRecord(ev_[8], s));
+                HIPCHK(hipStreamWaitEvent(side_, ev_[8], 0));
+                launch_lrf_list(v, fb, fbn, side_);
+                HIPCHK(hipEventRecord(ev_[9], side_));
+                launch_lrf8(v, d_wb, nwa, nw, fb + (size_t)8 * nwa, fbn + 1, s);
+                launch_lrf_list(v, fb + (size_t)8 * nwa, fbn + 1, s, 1);
+                HIPCHK(hipStreamWaitEvent(s, ev_[9], 0));
+            } else {
+                launch_lrf8(v, d_wb, nwa, nw, fb, fbn, s);
+                launch_lrf_list(v, fb, fbn, s);
+            }
         }
         HIPCHK(hipEventRecord(ev_[7], s));
         HIPCHK(hipGetLastError());
@@ -448,8 +472,10 @@ int Engine::setup_chunks(int npairs, hipStream_t s) {
     chunk_level_ = std::max(0, tree_L_ - 4);
     nchunks_ = npairs << chunk_level_;
     if (!ensure<int32_t>(d_qlist_, (size_t)nchunks_ * kChunkQ) || !ensure<int32_t>(d_qcount_, (size_t)nchunks_ * (kChunkQ / 64)) ||
+        !ensure<uint32_t>(d_chunk_cost_, (size_t)nchunks_) || !ensure<int32_t>(d_chunk_order_, (size_t)nchunks_) ||
         !ensure<double>(d_hist_, (size_t)kHist * npairs * 12))
         return SE3ICP_ERR_OUT_OF_MEMORY;
+    HIPCHK(hipMemsetAsync(d_chunk_cost_.p, 0, sizeof(uint32_t) * nchunks_, s));
     if (pinned(h_hist_, h_hist_cap_, (size_t)npairs * 12)) return SE3ICP_ERR_OUT_OF_MEMORY;
     HIPCHK(hipMemsetAsync(d_cert_it_.p, 0xff, sizeof(int32_t) * ld_, s));
     return 0;

@@ -96,6 +96,7 @@ class Engine {
     bool profile_ = false;
     std::mutex mu_;
     hipStream_t stream_ = nullptr;
+    hipStream_t side_ = nullptr;  // the exact hand-over pass of the setup, beside k_lrf8
     KernelTimes ktimes_;
 
     // geometry of the current batch
@@ -106,6 +107,7 @@ class Engine {
     bool have12_ = false, knn_list_ = false;
     bool nn_trace_ = false;              // SE3ICP_NN_TRACE=1: per-iteration NN work on stderr
     bool lrf_exact_only_ = false;        // SE3ICP_LRF_EXACT=1: the one-query-per-wavefront k_lrf for every point
+    int lrf_split_ = 0;                  // SE3ICP_LRF_SPLIT: % of k_lrf8 waves whose hand-overs run beside the rest (0: after all; A/B 80 / 88 / 93: k_lrf +3-5 %)
     se3icp_trace* trace_ = nullptr;      // armed per-iteration record of one pair (se3icp_set_trace)
     int record_trace(se3icp_trace* tr, int it, int& phase_of_it, hipStream_t s);
     double trace_prev_[kStatCols] = {};
@@ -121,7 +123,7 @@ class Engine {
     DevBuf d_clouds_, d_setup_, d_pairs_, d_cloud_of_, d_inptr_, d_in_, d_xyz64_, d_xyz32_, d_fr64_, d_fr32_, d_nrm64_,
         d_cov64_, d_conf64_, d_knn_, d_corr_idx_, d_corr_dist_, d_flag_list_, d_flag_count_,
         d_trim_key_, d_red_partial_, d_red_out_, d_work_, d_wb_, d_wn_, d_chunks_, d_partial_, d_centers_,
-        d_rechecked_, d_keys0_, d_vals1_, d_sort_tmp_, d_stats_, d_qlist_, d_qcount_, d_hist_, d_cert_d1_,
+        d_rechecked_, d_keys0_, d_vals1_, d_sort_tmp_, d_stats_, d_qlist_, d_qcount_, d_chunk_cost_, d_chunk_order_, d_hist_, d_cert_d1_,
         d_cert_l2_, d_cert_it_, d_margin_, d_sqlist_, d_state_, d_trim_cand_, d_trim_ctr_, d_scales_, d_trim_hist_,
         d_lrf_fb_, d_lrf_fbn_;  // k_lrf8 -> exact k_lrf hand-over list and its count
     TreeBufs t3_, t12_;

@@ -727,11 +727,11 @@ void launch_lrf(const View& v, int write_knn, hipStream_t s) {
 #ifndef SE3ICP_LRF_LIST_BLOCKS
 #define SE3ICP_LRF_LIST_BLOCKS 1024
 #endif
-void launch_lrf_list(const View& v, const int32_t* qlist, const int32_t* qcount, hipStream_t s) {
+void launch_lrf_list(const View& v, const int32_t* qlist, const int32_t* qcount, hipStream_t s, int qpw) {
     const size_t lds = sizeof(int) * (size_t)kWaves * kQ * v.kmax;
     const int nblk = std::max(1, std::min(SE3ICP_LRF_LIST_BLOCKS, (v.npts + kWaves * kQ - 1) / (kWaves * kQ)));
     hipLaunchKernelGGL(k_lrf, dim3(nblk), dim3(64 * kWaves), lds, s, v, 0, v.cloud_of, v.setup, v.clouds, v.t3.lo,
-                       v.t3.hi, qlist, qcount, SE3ICP_LRF_LIST_QPW);
+                       v.t3.hi, qlist, qcount, qpw > 0 ? std::min(qpw, kQ) : SE3ICP_LRF_LIST_QPW);
 }
 
 }  // namespace se3icp

@@ -585,7 +585,7 @@ static_assert(SE3ICP_LRF8_EPI_WAVE || (kW >= 2 && kW * kQ <= 64), "the per-block
 __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF8_WPE))) void k_lrf8(
     View v, const int32_t* __restrict__ cloud_of, const CloudSetup* __restrict__ setup,
     const CloudDev* __restrict__ clouds, const float* __restrict__ tlo, const float* __restrict__ thi,
-    const double* __restrict__ tx64, const int32_t* __restrict__ wave_base, int nwaves,
+    const double* __restrict__ tx64, const int32_t* __restrict__ wave_base, int w_lo, int nwaves,
     int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_count) {
     // (a query's park overlays the tail of its list, free once the list is final: <= 128 entries)
     __shared__ __attribute__((aligned(16))) unsigned s_list[kW][kQ][kCap];
@@ -619,7 +619,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
     // Wave wv covers local points 8*(wv - wave_base[c]) .. +7 of cloud c (waves aligned to
     // each cloud's start).  mode 0: nothing to do (no kNN wanted, past the end); 1: this
     // kernel; 2: its queries go to the exact kernel (partial wave, k too large for the lists).
-    const int wv = __builtin_amdgcn_readfirstlane(bid * kW + wid);
+    const int wv = __builtin_amdgcn_readfirstlane(w_lo + bid * kW + wid);
     int mode = 0, c = 0, w0 = 0, qn = 0;
     CloudSetup st{};
     CloudDev cl{0, 0};
@@ -1155,12 +1155,12 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
 
 }  // namespace
 
-void launch_lrf8(const View& v, const int32_t* wave_base, int nwaves, int32_t* fb_list, int32_t* fb_count,
+void launch_lrf8(const View& v, const int32_t* wave_base, int w_lo, int w_hi, int32_t* fb_list, int32_t* fb_count,
                  hipStream_t s) {
-    const int nb = (nwaves + kW - 1) / kW;
-    if (nb == 0) return;
+    const int nb = (w_hi - w_lo + kW - 1) / kW;
+    if (nb <= 0) return;
     hipLaunchKernelGGL(k_lrf8, dim3(nb), dim3(64 * kW), 0, s, v, v.cloud_of, v.setup, v.clouds, v.t3.lo, v.t3.hi,
-                       v.t3.tvec64, wave_base, nwaves, fb_list, fb_count);
+                       v.t3.tvec64, wave_base, w_lo, w_hi, fb_list, fb_count);
 }
 
 }  // namespace se3icp

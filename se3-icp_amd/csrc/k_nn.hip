@@ -175,6 +175,9 @@ __device__ __forceinline__ void compact_sweep(const float4* tile, const float4* 
 #ifndef SE3ICP_NN_SMALL
 #define SE3ICP_NN_SMALL 4  // groups of at most this many queries are searched one query at a time
 #endif
+#ifndef SE3ICP_NN_ORDER
+#define SE3ICP_NN_ORDER 0  // (A/B 4 / 8 / 16 classes: SE(3) NN -2 %, but the ordering launch costs as much; off) k_nn_group dispatches chunks in this many cost classes, costliest first (by the chunk's longest group wave of its last search); 0: tree order
+#endif
 #ifndef SE3ICP_NN_TWOLEVEL
 #define SE3ICP_NN_TWOLEVEL 0  // (A/B: SE(3) NN +1 %, kept off) k_nn_group: an interior node whose children are interior pushes its four grandchildren in one step (one box-load round trip per two levels)
 #endif
@@ -452,6 +455,63 @@ __global__ __launch_bounds__(1024) void k_nn_prep(View v) {
     }
 }
 
+// Dispatch order of k_nn_group's chunks (one 1024-thread block): a stable partition into
+// SE3ICP_NN_ORDER classes by the cost each chunk's longest group wave had in the last
+// search (costliest class first, tree order within a class, so neighbouring chunks still
+// share target leaves in one L2).  A launch's time is set by its longest waves; started
+// first, they overlap the many short ones.  Costs are cleared for the next search; with
+// none recorded (a first search) the order is the tree order.  Results never depend on it.
+__global__ __launch_bounds__(1024) void k_nn_order(uint32_t* __restrict__ cost, int32_t* __restrict__ order, int n) {
+    constexpr int NC = SE3ICP_NN_ORDER > 0 ? SE3ICP_NN_ORDER : 1;
+    __shared__ unsigned s_max;
+    __shared__ int s_base[NC], s_wcnt[16][NC];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    if (t == 0) s_max = 0u;
+    if (t < NC) s_base[t] = 0;
+    __syncthreads();
+    unsigned m = 0u;
+    for (int c = t; c < n; c += 1024) m = max(m, cost[c]);
+    atomicMax(&s_max, m);
+    __syncthreads();
+    const unsigned long long cmax = s_max;
+    auto cls_of = [&](unsigned x) __attribute__((always_inline)) {
+        return (int)min((unsigned long long)(NC - 1), ((cmax - x) * NC) / (cmax + 1));
+    };
+    for (int c = t; c < n; c += 1024) atomicAdd(&s_base[cls_of(cost[c])], 1);
+    __syncthreads();
+    if (t == 0) {
+        int acc = 0;
+        for (int k = 0; k < NC; ++k) { const int x = s_base[k]; s_base[k] = acc; acc += x; }
+    }
+    __syncthreads();
+    for (int c0 = 0; c0 < n; c0 += 1024) {
+        const int c = c0 + t;
+        const bool in = c < n;
+        int k = NC;
+        if (in) { k = cls_of(cost[c]); cost[c] = 0u; }
+        int rank = 0;
+#pragma unroll
+        for (int j = 0; j < NC; ++j) {
+            const unsigned long long b = __ballot(k == j);
+            if (lane == 0) s_wcnt[w][j] = __popcll(b);
+            if (k == j) rank = __builtin_amdgcn_mbcnt_hi((unsigned)(b >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b, 0u));
+        }
+        __syncthreads();
+        if (in) {
+            int pos = s_base[k] + rank;
+            for (int u = 0; u < w; ++u) pos += s_wcnt[u][k];
+            order[pos] = c;
+        }
+        __syncthreads();
+        if (t < NC) {
+            int tot = 0;
+            for (int u = 0; u < 16; ++u) tot += s_wcnt[u][t];
+            s_base[t] += tot;
+        }
+        __syncthreads();
+    }
+}
+
 // Results of a searched query (one lane): the recheck flag, the certificate, the
 // correspondence and its stored distance.
 template <int D>
@@ -510,9 +570,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_W
     const int bx = SE3ICP_NN_XCD == 2 ? xcd_block_runs(blockIdx.x, gridDim.x, SE3ICP_NN_XCD_RUN)
                    : SE3ICP_NN_XCD ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int wi = __builtin_amdgcn_readfirstlane(bx * kWaves + wid);
-    const int gi = wi / kSplit, q_lo = (wi % kSplit) * (64 / kSplit);
-    const int c = gi >> 4;
-    if (c >= v.nchunks) return;
+    const int gq = wi / kSplit, q_lo = (wi % kSplit) * (64 / kSplit);
+    if ((gq >> 4) >= v.nchunks) return;
+    // chunk at dispatch position gq >> 4 (k_nn_order: the costliest chunks start first, so
+    // the launch does not end on a long wave that started late)
+    const int c = SE3ICP_NN_ORDER ? __builtin_amdgcn_readfirstlane(v.chunk_order[gq >> 4]) : (gq >> 4);
+    const int gi = (c << 4) | (gq & 15);
     const int pair = c >> v.chunk_level;
     const PairDev* P = v.pairs + pair;
     const int phase = P->phase;
@@ -535,6 +598,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_W
             unsigned long long* st = v.stats + kStatCols * (gi & 63) + (D == 12 ? 0 : 2);
             atomicAdd(st, 64ull * n_eval);
             atomicAdd(st + 1, 64ull * n_box);
+            if (SE3ICP_NN_ORDER) atomicMax(v.chunk_cost + c, n_box / 2u + n_eval / 8u);
         }
         return;
     }
@@ -606,6 +670,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_W
     int stk = 0;  // DFS stack in a VGPR: lane i holds entry i (depth <= 2L+1 < 64)
     int sp = 1;
     unsigned n_eval = 0, n_box = 0;  // wave-uniform work counters (roofline accounting)
+    unsigned n_leaf = 0;             // leaves swept (the chunk cost)
 #ifdef SE3ICP_PROF
     unsigned n_want = 0, n_leafv = 0;
     const unsigned n_valid = (unsigned)__popcll(__ballot(valid));
@@ -660,6 +725,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_W
                 if (W == 0ull) continue;
                 w = __popcll(W);
             }
+            ++n_leaf;
 #ifdef SE3ICP_PROF
             n_want += __popcll(W & __ballot(valid));
             ++n_leafv;
@@ -778,6 +844,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_W
         unsigned long long* st = v.stats + kStatCols * (gi & 63) + (D == 12 ? 0 : 2);
         atomicAdd(st, 64ull * n_eval);
         atomicAdd(st + 1, 64ull * n_box);
+        // the wave's work (box-test steps + leaf sweeps): the chunk's cost for k_nn_order
+        if (SE3ICP_NN_ORDER) atomicMax(v.chunk_cost + c, n_box / 2u + 4u * n_leaf);
 #ifdef SE3ICP_PROF
         if (D == 12) {
             atomicAdd(v.stats + kStatCols * (gi & 63) + 8, (unsigned long long)n_want);
@@ -953,6 +1021,7 @@ __global__ __launch_bounds__(256) void k_nn_single(View v) {
 
 void launch_nn_prep(const View& v, hipStream_t s) {
     hipLaunchKernelGGL(k_nn_prep, dim3(v.nchunks), dim3(kChunkQ), 0, s, v);
+    if (SE3ICP_NN_ORDER) hipLaunchKernelGGL(k_nn_order, dim3(1), dim3(1024), 0, s, v.chunk_cost, v.chunk_order, v.nchunks);
 }
 // 16 groups of 64 per chunk, kWaves groups per block
 // and the single-query kernel over a fixed grid (SE3ICP_NN_SINGLE_BLOCKS x 4 waves)

@@ -81,6 +81,8 @@ struct View {
     int32_t nchunks;      // npairs << CL
     int32_t* qlist;       // [nchunks * kChunkQ] global slots of the searched queries, tree order
     int32_t* qcount;      // [nchunks][16] lanes of each group (0: none)
+    uint32_t* chunk_cost; // [nchunks] work of the chunk's longest group wave in its last search (k_nn_group)
+    int32_t* chunk_order; // [nchunks] dispatch order of k_nn_group: costliest chunks first (k_nn_order)
     int32_t* sq_list;     // [ld] queries of sparse chunks (global source tree slots) for k_nn_single:
                           // SE(3) phase from the front (count flag_count[1]), R3 from the back ([2])
     const double* hist;   // [kHist][npairs][12] pose T used at iteration k, row k % kHist
@@ -116,11 +118,13 @@ void launch_pair_norms(const View& v, int nnodes3, int nnodes12, const double* s
 // fused kNN + TOLDI frame + normals/GICP covariance (k_knn.hip); knn list only if v.knn
 void launch_lrf(const View& v, int write_knn, hipStream_t s);
 // the same for the listed tree slots qlist[0 .. *qcount) (device count; grid-strided)
-void launch_lrf_list(const View& v, const int32_t* qlist, const int32_t* qcount, hipStream_t s);
+// (qpw: queries per wave, 0 = the default)
+void launch_lrf_list(const View& v, const int32_t* qlist, const int32_t* qcount, hipStream_t s, int qpw = 0);
 // eight queries per wavefront (k_lrf8.hip); wave_base[c] = first wave of cloud c (waves
-// aligned to each cloud, nwaves in all); the queries it cannot resolve exactly from f32
-// keys are appended to fb_list (count fb_count, zeroed by the caller) for launch_lrf_list
-void launch_lrf8(const View& v, const int32_t* wave_base, int nwaves, int32_t* fb_list, int32_t* fb_count,
+// aligned to each cloud); this launch runs waves w_lo .. w_hi-1; the queries it cannot
+// resolve exactly from f32 keys are appended to fb_list (count fb_count, zeroed by the
+// caller) for launch_lrf_list
+void launch_lrf8(const View& v, const int32_t* wave_base, int w_lo, int w_hi, int32_t* fb_list, int32_t* fb_count,
                  hipStream_t s);
 
 // ---- k_loop.hip

@@ -1,7 +1,11 @@
 #!/bin/bash
-cd "${GRAFT_REPO_ROOT:-/root/repo}"
-for E in ${AB_EXTRAS:-1 0 1 0}; do
-  SE3ICP_L12_EXTRA=$E timeout -k 10 240 python bench.py --steps 3 --cpu-baseline off > gpurun_out/env_$E.json 2>/dev/null || exit 1
+# A/B of one run-time knob on the GPU box: AB_VAR=SE3ICP_LRF_SPLIT AB_VALS="88 0 88 0" tools/ab_env.sh
+# prints per run: value, iter/s, ms/step, the kernel split and the setup / loop phases
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
+mkdir -p gpurun_out
+VAR=${AB_VAR:-SE3ICP_LRF_SPLIT}
+for E in ${AB_VALS:-1 0 1 0}; do
+  env "$VAR=$E" timeout -k 10 240 python bench.py --steps ${AB_STEPS:-3} --cpu-baseline off > gpurun_out/env_$E.json 2> gpurun_out/env_$E.err || exit 1
   python -c "
-import json; d=json.loads(open('gpurun_out/env_$E.json').read().strip().splitlines()[-1]); print('extra $E', d['value'], d['ms_per_step'], d['kernel_ms_per_step'], d['roofline']['units_per_launch'])"
+import json; d=json.loads(open('gpurun_out/env_$E.json').read().strip().splitlines()[-1]); print('$VAR=$E', d['value'], d['ms_per_step'], d['kernel_ms_per_step'], d['phase_ms_per_step'])"
 done
