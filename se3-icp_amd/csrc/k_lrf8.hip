@@ -61,6 +61,9 @@ constexpr int kCap = SE3ICP_LRF8_CAP;  // candidates buffered per query (u32: cu
 #ifndef SE3ICP_LRF8_FINAL32
 #define SE3ICP_LRF8_FINAL32 1  // final rank order: u32 entry sort + odd-even fix-up of the full keys (0: a 64-bit network)
 #endif
+#ifndef SE3ICP_LRF8_F32SCAN
+#define SE3ICP_LRF8_F32SCAN 1  // leaf scans on the f32 coordinates (packed, two queries per instruction), bounds widened by the f32 error; 0: f64 distances
+#endif
 #ifndef SE3ICP_LRF8_LEAF_BITS
 #define SE3ICP_LRF8_LEAF_BITS 6
 #endif
@@ -204,6 +207,24 @@ __device__ __forceinline__ void sort_run(unsigned* list, int len, int l) {
     }
     __builtin_amdgcn_wave_barrier();
 }
+// |f32 squared distance of the f32-rounded points - exact squared distance of the f64
+// points| for distances <= d (loopdev.hpp f32_err, D = 3); S bounds the sum of the norms
+__device__ __forceinline__ float f32_err3(float d, float S) {
+    const float u = 5.9604645e-08f;
+    return 1.25f * (2.f * u * S * sqrtf(fmaxf(d, 0.f)) + 6.f * u * d + 4.f * u * u * S * S) + 1e-30f;
+}
+// the list bound from the Kw-th smallest entry t (f32 keys): every point whose exact
+// distance is within the Kw-th smallest exact distance has an f32 key <= the value of t
+// plus two errors (SE3ICP_LRF8_F32SCAN; identity for f64 keys, whose order is exact)
+__device__ __forceinline__ unsigned widen_bound(unsigned t, float S) {
+#if SE3ICP_LRF8_F32SCAN
+    if (t >= 0x7f800000u) return t;
+    const float b = __uint_as_float(t);
+    return (__float_as_uint(fmaf(2.02f, f32_err3(b, S), b)) + 2u) | kIdBits;
+#else
+    return t;
+#endif
+}
 // number of entries <= t in the sorted run A[0 .. n)
 __device__ __forceinline__ int upper_count(const unsigned* A, int n, unsigned t) {
     int lo = 0, hi = n;
@@ -273,7 +294,7 @@ __device__ __forceinline__ unsigned select_kth(const unsigned* list, int nbg, in
     return (unsigned)hi << 12;
 }
 
-__device__ __forceinline__ uint2 tighten_group(unsigned* lists, int g, int l, int nbg, int nmax, int Kw) {
+__device__ __forceinline__ uint2 tighten_group(unsigned* lists, int g, int l, int nbg, int nmax, int Kw, float S) {
     unsigned* list = lists + g * kCap;
     unsigned tg;
     if (SE3ICP_LRF8_SELECT >= 2 || (SE3ICP_LRF8_SELECT == 1 && nmax > 128)) {
@@ -286,7 +307,7 @@ __device__ __forceinline__ uint2 tighten_group(unsigned* lists, int g, int l, in
         sort_run(list + 128, nb, l);
         tg = kth_of_two(list, na, list + 128, nb, Kw - 1);
     }
-    tg |= kIdBits;
+    tg = widen_bound(tg | kIdBits, S);
     // compaction in place (reads of a round precede its writes, positions only move down)
     unsigned keep_n = 0;
     for (int r0 = 0; r0 < nmax; r0 += 8) {
@@ -314,7 +335,7 @@ __device__ __forceinline__ uint2 tighten_group(unsigned* lists, int g, int l, in
 // Returns (bound, kept, new sorted prefix) for the group; kept sets over 128 entries (ties
 // at the bound) are compacted unmerged (prefix 0).
 __device__ __forceinline__ uint3 tighten_group_sorted(unsigned* lists, int g, int l, int nbg, int mv, int nmax, int Kw,
-                                                      bool presort, int tail_per) {
+                                                      bool presort, int tail_per, float S) {
     unsigned* list = lists + g * kCap;
     if (presort) {
         mv = min(nbg, 128);
@@ -324,7 +345,7 @@ __device__ __forceinline__ uint3 tighten_group_sorted(unsigned* lists, int g, in
     unsigned* B = list + mv;
     if (tail_per == 8) sort_run<8>(B, nb, l);
     else if (tail_per == 16) sort_run<16>(B, nb, l);
-    const unsigned tg = nbg >= Kw ? (kth_of_two(list, mv, B, nb, Kw - 1) | kIdBits) : kPad;
+    const unsigned tg = nbg >= Kw ? widen_bound(kth_of_two(list, mv, B, nb, Kw - 1) | kIdBits, S) : kPad;
     const int ka = upper_count(list, mv, tg), kb = upper_count(B, nb, tg);
     const int kept = ka + kb;
     if (__ballot(kept > 128) == 0ull) {
@@ -654,17 +675,35 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
     float fqlo[3] = {0.f, 0.f, 0.f}, fqhi[3] = {0.f, 0.f, 0.f};
     int nlist = 0;
     const int n = cl.n;
+    float s_norm = 0.f;  // (f32 scans) bound on |q| + |p| over the cloud, from its root box
     if (mode == 1) {
+        // f32 box of the eight queries (the node boxes' frame)
+        const float fx = lane < kQ ? T.tvec[w0 + lane] : 0.f;
+        const float fy = lane < kQ ? T.tvec[v.ld + w0 + lane] : 0.f;
+        const float fz = lane < kQ ? T.tvec[2 * (size_t)v.ld + w0 + lane] : 0.f;
+#if SE3ICP_LRF8_F32SCAN
+        {  // the queries' f32 coordinates, x[8] y[8] z[8] (over the f64 query slots)
+            float* qf = reinterpret_cast<float*>(qv);
+            if (lane < kQ) {
+                qf[lane] = fx;
+                qf[kQ + lane] = fy;
+                qf[2 * kQ + lane] = fz;
+            }
+            const float* rlo = tlo + (size_t)c * T.nnodes * 3;
+            const float* rhi = thi + (size_t)c * T.nnodes * 3;
+            float r2 = 0.f;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) r2 += fmaxf(rlo[a] * rlo[a], rhi[a] * rhi[a]);
+            s_norm = 2.f * sqrtf(r2) * 1.0001f;
+        }
+#else
         if (lane < kQ) {
             qv[4 * lane] = TX[w0 + lane];
             qv[4 * lane + 1] = TY[w0 + lane];
             qv[4 * lane + 2] = TZ[w0 + lane];
         }
+#endif
         __builtin_amdgcn_wave_barrier();
-        // f32 box of the eight queries (the node boxes' frame)
-        const float fx = lane < kQ ? T.tvec[w0 + lane] : 0.f;
-        const float fy = lane < kQ ? T.tvec[v.ld + w0 + lane] : 0.f;
-        const float fz = lane < kQ ? T.tvec[2 * (size_t)v.ld + w0 + lane] : 0.f;
         fqlo[0] = fqhi[0] = __shfl(fx, 0, 64);
         fqlo[1] = fqhi[1] = __shfl(fy, 0, 64);
         fqlo[2] = fqhi[2] = __shfl(fz, 0, 64);
@@ -696,11 +735,11 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
         }
         const bool presort = anyz || dmax > 128;
         const int tail_per = presort ? (nmax <= 128 ? 0 : 8) : (dmax == 0 ? 0 : dmax <= 64 ? 8 : 16);
-        const uint3 r3 = tighten_group_sorted(lists, g, l, (int)nbv, mvv, (int)nmax, Kw, presort, tail_per);
+        const uint3 r3 = tighten_group_sorted(lists, g, l, (int)nbv, mvv, (int)nmax, Kw, presort, tail_per, s_norm);
         const uint2 r = make_uint2(r3.x, r3.y);
         mvv = (int)r3.z;
 #else
-        const uint2 r = tighten_group(lists, g, l, (int)nbv, (int)nmax, Kw);
+        const uint2 r = tighten_group(lists, g, l, (int)nbv, (int)nmax, Kw, s_norm);
 #endif
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -724,17 +763,41 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
         const int b = __builtin_amdgcn_readfirstlane(tree_first(n, T.L, i + 1));
         const bool valid = (bool)((int)(lane < b - a) & (int)(part == 0 || (part == 1) == (lane < 32)));
         const int slot = cl.off + a + (valid ? lane : 0);
-        const double px = TX[slot], py = TY[slot], pz = TZ[slot];
         const unsigned id = (unsigned)((li << 6) | lane);
-        // the list key: the f32 bits of the rounded-to-nearest distance plus one ulp (>= the
-        // distance: an upper bound, all that the bounds need; the final order uses exact keys)
         unsigned ent[kQ];
         unsigned long long m[kQ];
         bool over = false;
+#if SE3ICP_LRF8_F32SCAN
+        // the list key: the f32 squared distance of the f32 points (two queries per packed
+        // instruction); the bounds carry its error (widen_bound), the final order uses exact keys
+        float dq[kQ];
+        {
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            const float px = T.tvec[slot], py = T.tvec[v.ld + slot], pz = T.tvec[2 * (size_t)v.ld + slot];
+            const f2* qf2 = reinterpret_cast<const f2*>(qv);
+#pragma unroll
+            for (int jp = 0; jp < kQ / 2; ++jp) {
+                const f2 ex = qf2[jp] - f2{px, px}, ey = qf2[kQ / 2 + jp] - f2{py, py}, ez = qf2[kQ + jp] - f2{pz, pz};
+                f2 s2 = ex * ex;
+                s2 = __builtin_elementwise_fma(ey, ey, s2);
+                s2 = __builtin_elementwise_fma(ez, ez, s2);
+                dq[2 * jp] = s2.x;
+                dq[2 * jp + 1] = s2.y;
+            }
+        }
+#else
+        const double px = TX[slot], py = TY[slot], pz = TZ[slot];
+#endif
 #pragma unroll
         for (int j = 0; j < kQ; ++j) {
+#if SE3ICP_LRF8_F32SCAN
+            ent[j] = valid ? ((__float_as_uint(dq[j]) & ~kIdBits) | id) : kPad;
+#else
+            // the list key: the f32 bits of the rounded-to-nearest distance plus one ulp (>= the
+            // distance: an upper bound, all that the bounds need; the final order uses exact keys)
             const double d = l2_3(qv[4 * j], qv[4 * j + 1], qv[4 * j + 2], px, py, pz);
             ent[j] = valid ? (((__float_as_uint((float)d) + 1u) & ~kIdBits) | id) : kPad;
+#endif
             m[j] = __ballot(ent[j] <= Tq[j]);
             over |= nbq[j] + (unsigned)__popcll(m[j]) > (unsigned)kCap;
         }
@@ -902,10 +965,12 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
     const int nTop = min(Kw, nbg);
     const int kk = min(kl, nTop), kn = min(kn_want, nTop);
     const int wq = w0 + g;
+    // the group's f64 query (final order, sums)
+    const double qg64x = mode == 1 ? TX[wq] : 0.0, qg64y = mode == 1 ? TY[wq] : 0.0, qg64z = mode == 1 ? TZ[wq] : 0.0;
     if (mode == 1 && !fb_wave) {
         __builtin_amdgcn_wave_barrier();
-        const bool exact = final_group(lists, leaves, TX, TY, TZ, T.perm, T.pos, qv[4 * g], qv[4 * g + 1],
-                                       qv[4 * g + 2], cl.off, n, T.L, g, l, nbg, kk, kn, want_t, want_n);
+        const bool exact = final_group(lists, leaves, TX, TY, TZ, T.perm, T.pos, qg64x, qg64y, qg64z, cl.off, n, T.L,
+                                       g, l, nbg, kk, kn, want_t, want_n);
         fb_q = (bool)((int)!exact | (int)(nTop < Kw));
         n_cand += (unsigned)nbg;
 #ifdef SE3ICP_PROF
@@ -928,10 +993,14 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
 #pragma unroll
         for (int i = 0; i < kSums8; ++i) x[i] = 0.0;
         double Rf = 0.0;
+        #ifndef SE3ICP_LRF8_SKIP_SUMS  // (measurement build: the neighbour sums' share; wrong frames)
         if (mine) {
+#else
+        if (false) {
+#endif
             // the same loops, lane assignment and arithmetic as k_knn.hip's sums pass, over
             // the same rank order: the two kernels' frames agree bit for bit
-            const double qgx = qv[4 * g], qgy = qv[4 * g + 1], qgz = qv[4 * g + 2];
+            const double qgx = qg64x, qgy = qg64y, qgz = qg64z;
             const unsigned* rl = lists + g * kCap;
             if (want_t) {
                 const int rz = kk / 3;
@@ -1014,7 +1083,11 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
 #pragma unroll
         for (int k = 0; k < 6; ++k)
             c6[k] = M[k] - S[ia[k]] * cq[ib[k]] - cq[ia[k]] * S[ib[k]] + rz * cq[ia[k]] * cq[ib[k]];
+#ifdef SE3ICP_LRF8_SKIP_EIG  // (measurement build: the epilogue's share of the kernel; wrong frames)
+        const d3 zn = d3{c6[0], c6[1], c6[2]};
+#else
         const d3 zn = jacobi_smallest_evec(c6[0], c6[1], c6[2], c6[3], c6[4], c6[5]);
+#endif
         pb[P8_ZN] = zn.x;
         pb[P8_ZN + 1] = zn.y;
         pb[P8_ZN + 2] = zn.z;
@@ -1035,7 +1108,11 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
             n6[4] = cu[7] - cu[1] * cu[2];
             n6[5] = cu[8] - cu[2] * cu[2];
         }
+#ifdef SE3ICP_LRF8_SKIP_EIG
+        d3 nm = d3{n6[0], n6[1], n6[2]};
+#else
         d3 nm = fast_eigen3x3(n6[0], n6[1], n6[2], n6[3], n6[4], n6[5]);
+#endif
         if (sqrt(dot3(nm, nm)) == 0.0) nm = d3{0, 0, 1};
         const int gp = (int)pb[P8_GP];
         v.nrm64[gp] = nm.x;
@@ -1079,7 +1156,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
         double x6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         if (flags & 1) {
             const double nx = pj[P8_ZN], ny = pj[P8_ZN + 1], nz = pj[P8_ZN + 2];
-            const double qgx = qv[4 * g], qgy = qv[4 * g + 1], qgz = qv[4 * g + 2];
+            const double qgx = qg64x, qgy = qg64y, qgz = qg64z;
             const double R = pj[P8_R];
             const int kkq = (int)pj[P8_KK];
             const unsigned* rl = lists + g * kCap;
