@@ -615,7 +615,8 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
     };
     __shared__ int s_leaf[kW][kLeaves];
     __shared__ double s_q[kW][kQ][4];  // the queries' f64 coordinates (read back per leaf: no registers held)
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    // (wid through readfirstlane: the wave's LDS bases become scalar, not per-lane registers)
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = lane >> 3, l = lane & 7;  // query of the lane's group, lane within the group
     const int bid = xcd_block(blockIdx.x, gridDim.x);
     const TreeRef T = v.t3;
@@ -775,9 +776,16 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
             typedef float f2 __attribute__((ext_vector_type(2)));
             const float px = T.tvec[slot], py = T.tvec[v.ld + slot], pz = T.tvec[2 * (size_t)v.ld + slot];
             const f2* qf2 = reinterpret_cast<const f2*>(qv);
+            const f2 pxx = f2{px, px}, pyy = f2{py, py}, pzz = f2{pz, pz};
+            // a - b as one v_pk_add_f32 (the compiler splits a broadcast operand into two v_sub_f32)
+            auto pk_sub = [](f2 a, f2 b) __attribute__((always_inline)) {
+                f2 r;
+                asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+                return r;
+            };
 #pragma unroll
             for (int jp = 0; jp < kQ / 2; ++jp) {
-                const f2 ex = qf2[jp] - f2{px, px}, ey = qf2[kQ / 2 + jp] - f2{py, py}, ez = qf2[kQ + jp] - f2{pz, pz};
+                const f2 ex = pk_sub(qf2[jp], pxx), ey = pk_sub(qf2[kQ / 2 + jp], pyy), ez = pk_sub(qf2[kQ + jp], pzz);
                 f2 s2 = ex * ex;
                 s2 = __builtin_elementwise_fma(ey, ey, s2);
                 s2 = __builtin_elementwise_fma(ez, ez, s2);
@@ -808,7 +816,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
         }
 #pragma unroll
         for (int j = 0; j < kQ; ++j) {
-            if ((m[j] >> lane) & 1ull) {
+            if (ent[j] <= Tq[j]) {  // (the ballot's own compare: the exec mask, no bit test of m)
                 const int at = (int)nbq[j] + __builtin_amdgcn_mbcnt_hi((unsigned)(m[j] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m[j], 0u));
                 lists[j * kCap + at] = ent[j];
             }
