@@ -181,7 +181,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
     // the batch's largest k so that five 4-wave blocks fit a CU's 160 KB
     extern __shared__ int s_dyn[];
     __shared__ double s_park[kWaves][kQ][PK_N];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
 #ifdef SE3ICP_LRF_LDSPAD  // occupancy experiment: unused LDS
     __shared__ int s_pad[SE3ICP_LRF_LDSPAD / 4];
     if (v.npts < 0) s_pad[threadIdx.x] = 0;

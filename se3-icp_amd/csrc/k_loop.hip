@@ -292,7 +292,7 @@ __global__ __launch_bounds__(1024) void k_trim(View v) {
         if (threadIdx.x == 0) v.trim_key[pair] = 0ull;  // keep none (handled by reduce)
         return;
     }
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const unsigned* dist = reinterpret_cast<const unsigned*>(v.corr_dist) + cs.off;
     constexpr int U = 8;  // independent loads in flight per thread
     uint64_t* win = v.trim_key + v.npairs + pair;
@@ -604,7 +604,7 @@ __global__ __launch_bounds__(256) void k_reduce(View v) {
             }
         }
     }
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     {  // the 28 sums over the wave by recursive halving (wave.hpp)
         double x[32];
 #pragma unroll

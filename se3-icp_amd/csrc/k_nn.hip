@@ -352,7 +352,7 @@ __global__ __launch_bounds__(1024) void k_nn_prep(View v) {
     const int pair = c >> v.chunk_level;
     const PairDev* P = v.pairs + pair;
     const int phase = P->phase;
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (threadIdx.x < NL) s_cnt[threadIdx.x] = 0;
     __syncthreads();
     bool active = false;
@@ -560,7 +560,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_W
     __shared__ int s_wl[kWaves][64];
     __shared__ float s_r1[kWaves][64], s_r2[kWaves][64];
     __shared__ int s_rb[kWaves][64];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // wave-uniform work item: group jg (64 listed queries) of chunk c; the pair record,
     // node boxes and leaf ranges become scalar loads
     // (SE3ICP_NN_SPLIT waves per group of the 12-D search, 64 / split queries each: more,
