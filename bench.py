@@ -32,6 +32,8 @@ sys.path[:0] = [os.path.join(ROOT, "se3-icp_amd"), ROOT]
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X vector (= f32 MFMA) peak, /opt/skills/guides/MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak, same guide
+N_SIMDS = 1024             # 256 CUs x 4 SIMDs (same guide)
+CLOCK_GHZ = 2.4            # peak engine clock (same guide)
 
 METRIC = "ICP iterations/sec + pairs/sec, ~120k-pt KITTI clouds, 1/2/4/8 GPU"
 
@@ -84,6 +86,21 @@ def pmc_traffic(kernel_substr: str):
             if kernel_substr in k and v.get("hbm_bytes_per_launch") is not None:
                 return float(v["hbm_bytes_per_launch"]), os.path.relpath(f, ROOT)
     return None, None
+
+
+def pmc_counter(kernel_substr: str, counter: str):
+    """One PMC counter per dispatch of a kernel from the newest committed PMC summary."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        for k, v in d.get("kernels", {}).items():
+            c = v.get("counters_per_dispatch", {})
+            if kernel_substr in k and counter in c:
+                return float(c[counter])
+    return None
 
 
 def make_pairs(wl: str, total: int, first: int, count: int, n_az: int):
@@ -318,13 +335,19 @@ def lrf_roofline(ktot, kms, steps, k):
     t8, src = pmc_traffic("k_lrf8")
     tx, _ = pmc_traffic("k_lrf(")  # the exact kernel over the hand-over list
     traffic = (t8 + tx) if (t8 is not None and tx is not None) else t8
+    # what does bound it: the VALU issue of k_lrf8 (SQ_ACTIVE_INST_VALU counts quad-cycles per
+    # SIMD, summed over the chip's 1,024 SIMDs) over this launch pair's measured time
+    av = pmc_counter("k_lrf8", "SQ_ACTIVE_INST_VALU")
+    valu_busy = round(av * 4.0 / (N_SIMDS * CLOCK_GHZ * 1e6 * t_ms), 3) if (av and t_ms > 0) else None
     return {
         "kernel": "k_lrf8 + k_lrf (hand-overs)",
         "bound": "hbm",
         "note": "fused exact kNN-k (f64) + TOLDI frame + normals/GICP covariance per point: k_lrf8 (eight queries "
                 "per wavefront) and the exact one-query-per-wavefront k_lrf for the points it hands over, one HIP-event "
                 "bracket; algorithmic bytes = k neighbour gathers x 24 B per point (SURVEY.md §8d); the kernels are "
-                "issue / latency bound, not HBM bound (DESIGN.md §5)",
+                "VALU-issue bound, not HBM bound (valu_issue_busy: the fraction of the launch the SIMDs spend issuing "
+                "VALU, from the committed PMC pass; DESIGN.md §5)",
+        "valu_issue_busy": valu_busy,
         "achieved": round(achieved, 2),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
