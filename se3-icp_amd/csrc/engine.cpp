@@ -110,7 +110,7 @@ Engine::~Engine() {
                      &d_corr_idx_, &d_corr_dist_, &d_flag_list_, &d_flag_count_, &d_trim_key_, &d_red_partial_,
                      &d_red_out_, &d_work_, &d_wb_, &d_wn_, &d_chunks_, &d_partial_, &d_centers_,
                      &d_rechecked_, &d_keys0_, &d_vals1_, &d_sort_tmp_, &d_stats_,
-                     &d_qlist_, &d_qcount_, &d_chunk_cost_, &d_chunk_order_, &d_hist_, &d_cert_d1_, &d_cert_l2_, &d_cert_it_, &d_margin_, &d_sqlist_, &d_state_, &d_trim_cand_, &d_trim_ctr_, &d_scales_, &d_trim_hist_,
+                     &d_qlist_, &d_qcount_, &d_chunk_cost_, &d_chunk_order_, &d_hist_, &d_cert_, &d_sqlist_, &d_state_, &d_trim_cand_, &d_trim_ctr_, &d_scales_, &d_trim_hist_,
                      &d_lrf_fb_, &d_lrf_fbn_,
                      &t3_.perm, &t3_.pos, &t3_.vec, &t3_.blo, &t3_.bhi, &t3_.lo, &t3_.hi,
                      &t12_.perm, &t12_.pos, &t12_.vec, &t12_.blo, &t12_.bhi, &t12_.lo, &t12_.hi};
@@ -162,8 +162,8 @@ int Engine::alloc_points(int64_t ntot, int kmax, bool knn_list) {
               ensure<int32_t>(d_flag_list_, L) && ensure<int32_t>(d_flag_count_, 4) &&
               ensure<uint32_t>(d_keys0_, L) &&
               ensure<int32_t>(d_vals1_, L) && ensure<unsigned long long>(d_stats_, kStatCols * kStatSlots) &&
-              ensure<float>(d_cert_d1_, L) && ensure<float>(d_cert_l2_, L) && ensure<int32_t>(d_cert_it_, L) &&
-              ensure<float>(d_margin_, L) && ensure<int32_t>(d_sqlist_, L);
+              ensure<float4>(d_cert_, L) &&
+              ensure<int32_t>(d_sqlist_, L);
     for (TreeBufs* t : {&t3_, &t12_})
         ok = ok && ensure<int32_t>(t->perm, L) && ensure<int32_t>(t->pos, L);
     ok = ok && ensure<float>(t3_.vec, 3 * L) && ensure<float>(t12_.vec, 12 * L);
@@ -227,10 +227,7 @@ View Engine::view() const {
     v.chunk_order = (int32_t*)d_chunk_order_.p;
     v.sq_list = (int32_t*)d_sqlist_.p;
     v.hist = (const double*)d_hist_.p;
-    v.cert_d1 = (float*)d_cert_d1_.p;
-    v.cert_l2 = (float*)d_cert_l2_.p;
-    v.cert_it = (int32_t*)d_cert_it_.p;
-    v.nn_margin = (float*)d_margin_.p;
+    v.cert = (float4*)d_cert_.p;
     return v;
 }
 
@@ -477,7 +474,7 @@ int Engine::setup_chunks(int npairs, hipStream_t s) {
         return SE3ICP_ERR_OUT_OF_MEMORY;
     HIPCHK(hipMemsetAsync(d_chunk_cost_.p, 0, sizeof(uint32_t) * nchunks_, s));
     if (pinned(h_hist_, h_hist_cap_, (size_t)npairs * 12)) return SE3ICP_ERR_OUT_OF_MEMORY;
-    HIPCHK(hipMemsetAsync(d_cert_it_.p, 0xff, sizeof(int32_t) * ld_, s));
+    HIPCHK(hipMemsetAsync(d_cert_.p, 0xff, sizeof(float4) * ld_, s));  // iteration -1: no certificate
     return 0;
 }
 

@@ -263,7 +263,8 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
     pose_point(T, mt[0], mt[1], mt[2], Qt);
     const double rot2 = 3.0 * a2 * (1.0 + 1e-12);  // |rotation columns|^2 (12-D), 0 (3-D)
     const int it = P->iter;
-    const int ci = v.cert_it[g];
+    const float4 cr = v.cert[g];
+    const int ci = __float_as_int(cr.z);
     const double qn = sqrt(rot2 + Qt[0] * Qt[0] + Qt[1] * Qt[1] + Qt[2] * Qt[2]);
     if ((int)(ci >= P->phase_start) & (int)(ci < it) & (int)(it - ci < kHist)) {
         double Tr[12], Qr[3];
@@ -274,7 +275,7 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
         // |q_now - q_then|, padded for the frame's orthonormality and the rounding of the
         // two f64 queries the searches used
         const double dl = sqrt(a2 * rot_frob2(T, Tr) * (1.0 + 1e-12) + dt * dt) * (1.0 + 1e-12) + 2e-15 * (qn + qr);
-        const double a = (double)v.cert_l2[g] - dl, b = (double)v.cert_d1[g] + dl;
+        const double a = (double)cr.y - dl, b = (double)cr.x + dl;
         // margin for the f64 rounding of the reference's own squared distances (|q| + |target| <= M)
         const double M = 2.0 * qn + b;
         if ((int)(a > b) & (int)((a - b) * (a + b) > 1e-14 * M * M)) {
@@ -293,7 +294,7 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
         const double dt = dist3_f64(Qt, Qp);
         m = (float)(SE3ICP_NN_EXPAND * sqrt(a2 * rot_frob2(T, Tp) + dt * dt));
     }
-    v.nn_margin[g] = m;
+    v.cert[g].w = m;
 #if SE3ICP_NN_SEED
     // No previous match (a pair's first search): seed one from a greedy descent of the
     // target tree (the child whose f32 box bound is smaller, down to a leaf; a target of
@@ -344,7 +345,10 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
 // for k_nn_group: consecutive leaves' remaining queries share a 64-lane group as long as
 // they fit, a leaf is never split (with every query searched, a group is one leaf).
 // qlist[c][j][lane] = local tree position, qcount[c][j] = lanes of group j.
-__global__ __launch_bounds__(1024) void k_nn_prep(View v) {
+#ifndef SE3ICP_NN_PREP_WPE
+#define SE3ICP_NN_PREP_WPE 8  // waves per SIMD of k_nn_prep: 8 = two 1024-thread blocks per CU (<= 64 VGPRs)
+#endif
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_PREP_WPE))) void k_nn_prep(View v) {
     constexpr int NL = kChunkQ / 64;  // leaves (groups) per chunk
     __shared__ int s_cnt[NL], s_slot[NL], s_base[NL], s_wc[NL], s_single;
     const int c = SE3ICP_NN_XCD == 2 ? xcd_block_runs(blockIdx.x, gridDim.x, SE3ICP_NN_XCD_RUN / 4)
@@ -526,13 +530,13 @@ __device__ __forceinline__ void nn_finish(const View& v, const PairDev* P, int p
     // certificate for the next iterations (k_nn_prep): exact match distance <= sqrt(d1 + err),
     // every other target >= min(d2 - err(d2), thr): visited ones by the top-2, unvisited
     // ones because every box skipped had a bound >= thr at the time (thr only decreases)
+    // (one 16-B store; the margin slot w is dead once the search has read it)
     if ((int)flag | (int)(i1 < 0)) {
-        v.cert_it[g] = -1;
+        v.cert[g] = make_float4(0.f, 0.f, __int_as_float(-1), 0.f);
     } else {
         const float l2 = fminf(d2 - f32_err(d2, na, nb, D), thr * (1.f - 4e-6f));
-        v.cert_d1[g] = sqrtf(d1 + f32_err(d1, na, nb, D)) * (1.f + 1e-6f);
-        v.cert_l2[g] = sqrtf(fmaxf(l2, 0.f)) * (1.f - 1e-6f);
-        v.cert_it[g] = P->iter;
+        v.cert[g] = make_float4(sqrtf(d1 + f32_err(d1, na, nb, D)) * (1.f + 1e-6f),
+                                sqrtf(fmaxf(l2, 0.f)) * (1.f - 1e-6f), __int_as_float(P->iter), 0.f);
     }
     // tree position -> target index; a NaN query keeps the reference's zero-initialised index
     i1 = (i1 < 0) ? 0 : TR.perm[ct.off + i1];
@@ -605,7 +609,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_W
     const bool valid = lane < cnt_q;
     const int gx = cs.off + v.qlist[(size_t)gi * 64 + q_lo + (valid ? lane : 0)];  // source tree slot
     const int g = cs.off + TR.perm[gx];
-    const float mrg = valid ? v.nn_margin[g] : 0.f;
+    const float mrg = valid ? v.cert[g].w : 0.f;
 
     // query: f64 pose applied to the source element, rounded to f32
     float q[D];
@@ -898,7 +902,7 @@ __device__ __forceinline__ void single_one(const View& v, const PairDev* P, int 
     f32x2 q2[(D + 1) / 2];
 #pragma unroll
     for (int r = 0; r < D / 2; ++r) q2[r] = f32x2{q[2 * r], q[2 * r + 1]};
-    const float mrg = v.nn_margin[g];
+    const float mrg = v.cert[g].w;
     auto widen = [&](float a1, float a2) __attribute__((always_inline)) {
         const float e = sqrtf(a1) + 2.f * mrg;
         const float t = fmaxf(a1, fminf(e * e, a2));

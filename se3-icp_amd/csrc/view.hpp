@@ -86,13 +86,13 @@ struct View {
     int32_t* sq_list;     // [ld] queries of sparse chunks (global source tree slots) for k_nn_single:
                           // SE(3) phase from the front (count flag_count[1]), R3 from the back ([2])
     const double* hist;   // [kHist][npairs][12] pose T used at iteration k, row k % kHist
-    // NN certificate of each source point from its last search (iteration cert_it):
-    // every target other than the match is at least cert_l2 away from that query, the
-    // match at most cert_d1 (exact distances, conservatively rounded)
-    float* cert_d1;
-    float* cert_l2;
-    int32_t* cert_it;     // -1: none
-    float* nn_margin;     // [ld] search-radius expansion of the searched queries
+    // NN certificate of each source point from its last search, one 16-B record per point
+    // (k_nn_prep gathers it through the tree permutation: one cache line, not four):
+    //   x = d1: the match is at most d1 away (exact distance, conservatively rounded),
+    //   y = l2: every other target at least l2,
+    //   z = the iteration of that search (int bits; -1: none),
+    //   w = the search-radius expansion of a query searched in this iteration
+    float4* cert;
 };
 
 // ---- k_setup.hip
