@@ -328,6 +328,9 @@ __device__ __forceinline__ int part_node_id_at(const TreeView& t, int level, int
     return part_node_id(c, level, tree_node_of(g - cl.off, cl.n, level));
 }
 
+#ifndef SE3ICP_TREE_HIST_ATOMIC
+#define SE3ICP_TREE_HIST_ATOMIC 1  // block histograms added into per-node histograms (0: written whole, summed by k_part_select)
+#endif
 // Per block of kHistElems tree positions: the histograms of the (at most) two nodes the
 // block starts in, in LDS, written out whole (dense[block][2][bins]); points of further
 // nodes (small clouds) go to the per-node overflow histograms by global atomics.
@@ -360,8 +363,17 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(TreeView t, int leve
         }
     }
     __syncthreads();
+#if SE3ICP_TREE_HIST_ATOMIC
+    // the block's two node histograms added into the per-node histograms (its non-zero bins;
+    // integer adds: the order does not matter), so k_part_select reads one histogram per node
+    for (int i = tid; i < 2 * kPartBins; i += kPartThreads) {
+        const uint32_t x = s_h[i];
+        if (x) atomicAdd(&overflow[(size_t)(id0 + i / kPartBins) * kPartBins + (i & (kPartBins - 1))], x);
+    }
+#else
     uint32_t* out = dense + (size_t)blockIdx.x * 2 * kPartBins;
     for (int i = tid; i < 2 * kPartBins; i += kPartThreads) out[i] = s_h[i];
+#endif
 }
 
 // one workgroup per node of the level: its histogram (the blocks' dense slots + overflow),
@@ -383,7 +395,7 @@ __global__ __launch_bounds__(kSelThreads) void k_part_select(TreeView t, int lev
         v[k] = ov[tid * kSelPer + k];
         ov[tid * kSelPer + k] = 0u;
     }
-    if (b > a) {
+    if ((int)!SE3ICP_TREE_HIST_ATOMIC & (int)(b > a)) {
         const int kb0 = (cl.off + a) / kHistElems, kb1 = (cl.off + b - 1) / kHistElems;
 #pragma unroll 8
         for (int kb = kb0; kb <= kb1; ++kb) {
