@@ -122,6 +122,7 @@ Engine::~Engine() {
     if (h_rechecked_) (void)hipHostFree(h_rechecked_);
     if (h_hist_) (void)hipHostFree(h_hist_);
     if (h_lrf_stats_) (void)hipHostFree(h_lrf_stats_);
+    if (h_loop_stats_) (void)hipHostFree(h_loop_stats_);
     for (auto& e : ev_)
         if (e) (void)hipEventDestroy(e);
     for (auto& e : loop_ev_)
@@ -752,8 +753,10 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         HIPCHK(hipMemcpyAsync(h_partial_, d_centers_.p, sizeof(double) * 3 * nclouds_, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(h_rechecked_, d_rechecked_.p, sizeof(int32_t) * npairs, hipMemcpyDeviceToHost, s));
     {
-        unsigned long long stats[kStatCols * kStatSlots];
-        HIPCHK(hipMemcpyAsync(stats, d_stats_.p, sizeof(stats), hipMemcpyDeviceToHost, s));
+        if (pinned(h_loop_stats_, h_loop_stats_cap_, (size_t)kStatCols * kStatSlots)) return SE3ICP_ERR_OUT_OF_MEMORY;
+        const unsigned long long* stats = h_loop_stats_;
+        HIPCHK(hipMemcpyAsync(h_loop_stats_, d_stats_.p, sizeof(unsigned long long) * kStatCols * kStatSlots,
+                              hipMemcpyDeviceToHost, s));
         SYNC_STREAM(s);
         double sum[kStatCols] = {};
         for (int i = 0; i < kStatSlots; ++i)

@@ -142,6 +142,8 @@ class Engine {
     size_t h_state_cap_ = 0, h_phase_cap_ = 0;
     unsigned long long* h_lrf_stats_ = nullptr;  // k_lrf work counters (read at the next sync)
     size_t h_lrf_stats_cap_ = 0;
+    unsigned long long* h_loop_stats_ = nullptr;  // loop NN work counters (pinned: an async copy, not a staged one)
+    size_t h_loop_stats_cap_ = 0;
     bool lrf_stats_pending_ = false;
     // 6/7: k_lrf time; 12/13/14: batch begin / setup done / loop done (GPU-timeline phase
     // times); 15: sync_stream; the rest unused

@@ -234,6 +234,46 @@ def register_batch_device(src_ptr: int, src_off, tgt_ptr: int, tgt_off, method: 
     return _results(res, n)
 
 
+class DeviceBatchRunner:
+    """``register_batch_device`` for repeated calls on the same clouds (benchmark loops):
+    the ctypes arguments are built once, each ``run(slot)`` is one C-ABI call writing into
+    preallocated result / kernel-time buffers, and the conversion to ``PairResult`` happens
+    later (``results(slot)``, ``kernel_times(slot)``), outside the caller's timed region."""
+
+    _KT_KEYS = ["nn_se3_ms", "nn_r3_ms", "recheck_ms", "trim_ms", "reduce_ms", "setup_ms", "nn_se3_launches",
+                "nn_r3_launches", "se3_dist_evals", "se3_box_tests", "r3_dist_evals", "r3_box_tests",
+                "lrf_ms", "lrf_queries", "lrf_leaves", "lrf_merges", "lrf_box_tests", "lrf_candidates",
+                "nn_prep_ms", "se3_queries", "se3_searched", "r3_queries", "r3_searched", "lrf_fallback"]
+
+    def __init__(self, src_ptr: int, src_off, tgt_ptr: int, tgt_off, method: str,
+                 params: _lib.Params | None = None, device: int = 0, slots: int = 1):
+        self._L = _lib.load()
+        self.n = len(src_off) - 1
+        self._dev = device
+        self._so = (C.c_int64 * (self.n + 1))(*[int(x) for x in src_off])
+        self._to = (C.c_int64 * (self.n + 1))(*[int(x) for x in tgt_off])
+        self._src = C.c_void_p(src_ptr)
+        self._tgt = C.c_void_p(tgt_ptr)
+        self._mid = _lib.method_id(method)
+        self._params = params or _lib.default_params()
+        self._pref = C.byref(self._params)
+        self._res = [(_lib.Result * self.n)() for _ in range(max(1, slots))]
+        self._kt = [(C.c_double * 24)() for _ in range(max(1, slots))]
+
+    def run(self, slot: int = 0) -> None:
+        rc = self._L.se3icp_register_batch_device(self._dev, self.n, self._src, self._so, self._tgt, self._to,
+                                                  self._mid, self._pref, self._res[slot], None)
+        if rc not in (_lib.OK, _lib.ERR_NONFINITE):
+            raise _lib.Se3IcpError(rc, "register_batch_device")
+        self._L.se3icp_last_kernel_times(self._dev, self._kt[slot])
+
+    def results(self, slot: int = 0) -> list[PairResult]:
+        return _results(self._res[slot], self.n)
+
+    def kernel_times(self, slot: int = 0) -> dict:
+        return dict(zip(self._KT_KEYS, list(self._kt[slot])))
+
+
 def register_batch_traced(pairs, method: str, params: _lib.Params | None = None, pair: int = 0,
                           max_iters: int = 160, device: int = 0):
     """register_batch with the per-iteration record of one pair (se3icp_set_trace): the
