@@ -99,6 +99,7 @@ int Engine::init() {
     if (const char* e = std::getenv("SE3ICP_L12_EXTRA")) l12_extra_ = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = std::getenv("SE3ICP_NN_TRACE")) nn_trace_ = std::atoi(e) != 0;
     if (const char* e = std::getenv("SE3ICP_LRF_EXACT")) lrf_exact_only_ = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SE3ICP_NN_EVENTS")) nn_events_ = std::atoi(e) != 0;
     return 0;
 }
 
@@ -656,7 +657,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         const bool detail = profile_ || nn_trace_;
         // (timed steps: the SE(3) NN bracket only when that grid is queued, plus the
         // iteration's end marker; profiled steps: every stage)
-        const bool t_se3 = detail || do_se3;
+        const bool t_se3 = detail || (do_se3 && nn_events_);
         if (detail) HIPCHK(hipEventRecord(ev[0], s));
         launch_nn_prep(v, s);
         if (t_se3) HIPCHK(hipEventRecord(ev[1], s));
@@ -673,7 +674,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(ev[6], s));
         loop_detail_[it % kLoopRing] = detail;
-        loop_flags_[it % kLoopRing] = (do_se3 ? 1 : 0) | (do_r3 ? 2 : 0);
+        loop_flags_[it % kLoopRing] = (do_se3 ? 1 : 0) | (do_r3 ? 2 : 0) | (t_se3 ? 4 : 0);
         return 0;
     };
     // wait for iteration `it`, add its kernel times; returns the pairs of iteration it+1
@@ -683,7 +684,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         float ms[6] = {};
         if (loop_detail_[it % kLoopRing]) {
             for (int k = 0; k < 6; ++k) HIPCHK(hipEventElapsedTime(&ms[k], ev[k], ev[k + 1]));
-        } else if (loop_flags_[it % kLoopRing] & 1) {
+        } else if (loop_flags_[it % kLoopRing] & 4) {
             HIPCHK(hipEventElapsedTime(&ms[1], ev[1], ev[2]));
         }
         ktimes_.nn_prep_ms += ms[0];

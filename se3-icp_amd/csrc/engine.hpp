@@ -107,6 +107,9 @@ class Engine {
     bool have12_ = false, knn_list_ = false;
     bool nn_trace_ = false;              // SE3ICP_NN_TRACE=1: per-iteration NN work on stderr
     bool lrf_exact_only_ = false;        // SE3ICP_LRF_EXACT=1: the one-query-per-wavefront k_lrf for every point
+    // SE3ICP_NN_EVENTS=0: no HIP events around the SE(3) NN grids outside profiled batches
+    // (each marker leaves the GPU idle ~5 us; time_se3_correspondence_search_ms is then 0)
+    bool nn_events_ = true;
     int lrf_split_ = 0;                  // SE3ICP_LRF_SPLIT: % of k_lrf8 waves whose hand-overs run beside the rest (0: after all; A/B 80 / 88 / 93: k_lrf +3-5 %)
     se3icp_trace* trace_ = nullptr;      // armed per-iteration record of one pair (se3icp_set_trace)
     int record_trace(se3icp_trace* tr, int it, int& phase_of_it, hipStream_t s);
