@@ -77,6 +77,27 @@ hipError_t spin_wait(hipEvent_t e) {
     }
 }
 
+// Wait until k_reduce_final has written every pair's next phase into the coherent host
+// slot (cleared to -1 before the iteration was queued): the loop needs no per-iteration
+// end event, whose marker leaves the GPU idle ~5 us.  A stream that completed (or failed)
+// with a slot still unwritten is reported instead of waited on.
+hipError_t spin_phases(const volatile int32_t* slot, int n, hipStream_t s) {
+    for (unsigned spins = 0;; ++spins) {
+        int left = 0;
+        for (int p = 0; p < n; ++p) left += slot[p] < 0;
+        if (left == 0) return hipSuccess;
+        if ((spins & 1023u) == 1023u) {
+            const hipError_t r = hipStreamQuery(s);
+            if (r == hipSuccess) {
+                left = 0;
+                for (int p = 0; p < n; ++p) left += slot[p] < 0;
+                return left == 0 ? hipSuccess : hipErrorUnknown;
+            }
+            if (r != hipErrorNotReady) return r;
+        }
+    }
+}
+
 constexpr int kStatSlots = 64;  // work counters: [64][kStatCols] u64 (spread against atomic contention)
 
 }  // namespace
@@ -648,6 +669,9 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     int trace_phase = tr ? h_pairs_[tr->pair].phase : 0;  // phase of the iteration being recorded
     auto enqueue = [&](int it) -> int {
         hipEvent_t* ev = &loop_ev_[(it % kLoopRing) * kLoopEv];
+        // the ring slot k_reduce_final of this iteration fills (its last reader, iteration
+        // it - kLoopRing, is finished): unwritten until then (spin_phases)
+        for (int p = 0; p < npairs; ++p) h_phase_[(size_t)(it % kLoopRing) * npairs + p] = -1;
         // SE(3) phase: iterations 1..max_num_se3_iterations at most (ISR.cpp:718-723, 1118)
         const bool do_se3 =
             n_se3 > 0 && (prm.max_num_se3_iterations < 1 || it <= prm.max_num_se3_iterations);
@@ -672,7 +696,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         launch_reduce(v, (const int32_t*)d_wb_.p, (const int32_t*)d_wn_.p, (PairState*)d_state_.p, (double*)d_hist_.p,
                       d_phase_ + (size_t)(it % kLoopRing) * npairs, s);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipEventRecord(ev[6], s));
+        if (detail) HIPCHK(hipEventRecord(ev[6], s));
         loop_detail_[it % kLoopRing] = detail;
         loop_flags_[it % kLoopRing] = (do_se3 ? 1 : 0) | (do_r3 ? 2 : 0) | (t_se3 ? 4 : 0);
         return 0;
@@ -680,7 +704,8 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     // wait for iteration `it`, add its kernel times; returns the pairs of iteration it+1
     auto finish = [&](int it) -> int {
         hipEvent_t* ev = &loop_ev_[(it % kLoopRing) * kLoopEv];
-        HIPCHK(spin_wait(ev[6]));
+        if (loop_detail_[it % kLoopRing]) HIPCHK(spin_wait(ev[6]));
+        else HIPCHK(spin_phases(h_phase_ + (size_t)(it % kLoopRing) * npairs, npairs, s));
         float ms[6] = {};
         if (loop_detail_[it % kLoopRing]) {
             for (int k = 0; k < 6; ++k) HIPCHK(hipEventElapsedTime(&ms[k], ev[k], ev[k + 1]));
