@@ -435,6 +435,34 @@ def test_batch_independence_16_vs_two_8(se3icp_mod):
         assert (f.num_iterations, f.num_pure_se3_iterations) == (h.num_iterations, h.num_pure_se3_iterations)
 
 
+def test_device_batch_runner_equals_register_batch(se3icp_mod):
+    """The benchmark's timed call (clouds resident in HBM, prebuilt arguments, results read
+    after the calls) returns bitwise the poses of the host-buffer batch entry, every call."""
+    torch = pytest.importorskip("torch")
+    from se3icp import datasets
+    pairs, _ = datasets.kitti_like_pairs(4, seed=4)
+    p = se3icp_mod.kitti_params()
+    host = se3icp_mod.register_batch(pairs, "se3_gicp", p)
+    src = np.ascontiguousarray(np.concatenate([a for a, _ in pairs]))
+    tgt = np.ascontiguousarray(np.concatenate([b for _, b in pairs]))
+    so = np.concatenate([[0], np.cumsum([a.shape[0] for a, _ in pairs])])
+    to = np.concatenate([[0], np.cumsum([b.shape[0] for _, b in pairs])])
+    d_src = torch.from_numpy(src).to("cuda:0")
+    d_tgt = torch.from_numpy(tgt).to("cuda:0")
+    torch.cuda.synchronize()
+    r = se3icp_mod.DeviceBatchRunner(d_src.data_ptr(), so, d_tgt.data_ptr(), to, "se3_gicp", p, device=0, slots=2)
+    r.run(0)
+    r.run(1)
+    for slot in (0, 1):
+        res = r.results(slot)
+        assert len(res) == len(host)
+        for i, (a, b) in enumerate(zip(res, host)):
+            assert np.array_equal(a.T, b.T), (slot, i, a.T - b.T)
+            assert (a.num_iterations, a.num_pure_se3_iterations) == (b.num_iterations, b.num_pure_se3_iterations)
+        kt = r.kernel_times(slot)
+        assert kt["lrf_queries"] > 0 and kt["nn_se3_launches"] > 0
+
+
 def _lrf_cloud(kind):
     from se3icp import datasets
     if kind == "kitti":
