@@ -614,11 +614,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
         return reinterpret_cast<double*>(&s_list[w][j][kParkAt]);
     };
     __shared__ int s_leaf[kW][kLeaves];
-#if SE3ICP_LRF8_F32SCAN
-    __shared__ __attribute__((aligned(16))) double s_q[kW][3 * kQ / 2];  // the queries' f32 coordinates x[8] y[8] z[8]
-#else
     __shared__ double s_q[kW][kQ][4];  // the queries' f64 coordinates (read back per leaf: no registers held)
-#endif
     // (wid through readfirstlane: the wave's LDS bases become scalar, not per-lane registers)
     const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = lane >> 3, l = lane & 7;  // query of the lane's group, lane within the group
@@ -676,7 +672,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
     // would turn the register arrays into scratch memory)
     unsigned nbv = 0u;
     int mvv = 0;  // (SE3ICP_LRF8_MERGE) sorted prefix of the group's list
-    double* qv = reinterpret_cast<double*>(&s_q[wid]);
+    double* qv = &s_q[wid][0][0];
     float fqlo[3] = {0.f, 0.f, 0.f}, fqhi[3] = {0.f, 0.f, 0.f};
     int nlist = 0;
     const int n = cl.n;
