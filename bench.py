@@ -130,9 +130,6 @@ def main():
                     help="collective backend for N > 1 (gloo: ranks may share one GPU, as in the tests)")
     ap.add_argument("--dump-poses", default="", help="rank 0 writes the gathered per-pair poses (.npy)")
     args = ap.parse_args()
-    # timing instrumentation only: no HIP event markers around the SE(3) NN grids in the timed
-    # steps (each leaves the GPU idle ~5 us); the stage times come from one profiled step
-    os.environ.setdefault("SE3ICP_NN_EVENTS", "0")
     W = WORKLOADS[args.workload]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -149,6 +146,10 @@ def main():
     ndev = max(1, torch.cuda.device_count())
     devi = local % ndev
     torch.cuda.set_device(devi)
+    # timing instrumentation only: no HIP event markers around the SE(3) NN grids in the timed
+    # steps (each leaves the GPU idle ~5 us); the stage times come from one profiled step
+    from se3icp import registration
+    registration.set_nn_events(False, devi)
     dev = torch.device("cuda", devi)
     dist = None
     xdev = dev
@@ -220,21 +221,18 @@ def main():
     step()
     kt_detail = se3icp.last_kernel_times(devi)
     se3icp.set_profiling(False, devi)
-    # (the timed steps carry no SE(3) NN events either, SE3ICP_NN_EVENTS=0: the NN stage
+    # (the timed steps carry no SE(3) NN events either, set_nn_events(False): the NN stage
     # times, the secondary roofline's included, come from this profiled step)
-    nn_keys = ["nn_prep_ms", "nn_r3_ms", "recheck_ms", "trim_ms", "reduce_ms"]
-    if os.environ.get("SE3ICP_NN_EVENTS", "1") == "0":
-        nn_keys.append("nn_se3_ms")
-    for k in nn_keys:
+    for k in ["nn_prep_ms", "nn_r3_ms", "recheck_ms", "trim_ms", "reduce_ms", "nn_se3_ms"]:
         ktot[k] = kt_detail[k] * args.steps
 
     # ---- cross-rank: max time, summed work, RCCL gather of the per-pair results
-    elapsed, loop_s, iters_all, poses_all = sharding.exchange_results(
-        dist, xdev, elapsed, loop_ms / 1000.0, iters, np.stack([r.T for r in last]))
+    elapsed, loop_s, iters_all, gathered = sharding.exchange_results(
+        dist, xdev, elapsed, loop_ms / 1000.0, iters, sharding.pair_records(last))
 
     if rank == 0:
         if args.dump_poses:
-            np.save(args.dump_poses, poses_all)
+            np.save(args.dump_poses, gathered.T)
         total_pairs = world * P * args.steps
         value = iters_all / elapsed
         ms_per_step = 1000.0 * elapsed / args.steps

@@ -30,21 +30,21 @@
 extern "C" {
 #endif
 
-#define SE3ICP_ABI_VERSION 2
+#define SE3ICP_ABI_VERSION 3
 
 typedef enum se3icp_status {
     SE3ICP_OK = 0,
     SE3ICP_ERR_INVALID_ARG = -1,
     SE3ICP_ERR_INVALID_METHOD = -2,   /* name not in the reference's whitelist */
     SE3ICP_ERR_EMPTY_CLOUD = -3,
-    SE3ICP_ERR_K_TOO_LARGE = -4,      /* number_of_nn_for_LRF above SE3ICP_MAX_KNN */
+    SE3ICP_ERR_K_TOO_LARGE = -4,      /* unused since ABI 3: number_of_nn_for_LRF is unbounded, as
+                                         the reference's (ISR.hpp:80, ISR.cpp:253); k beyond what
+                                         HBM holds fails with SE3ICP_ERR_OUT_OF_MEMORY */
     SE3ICP_ERR_NO_DEVICE = -5,        /* no HIP device / kernels not loadable: never a CPU fallback */
     SE3ICP_ERR_HIP = -6,              /* HIP runtime error */
     SE3ICP_ERR_NONFINITE = -7,        /* NaN/Inf in the resulting pose */
     SE3ICP_ERR_OUT_OF_MEMORY = -8
 } se3icp_status;
-
-#define SE3ICP_MAX_KNN 128
 
 /* Registration methods.  Names match examples/run_registration_method.cpp:19-24
  * ("pt2pt","pt2pl","gicp","se3_pt2pt","se3_pt2pl","se3_gicp") plus the two run
@@ -91,7 +91,12 @@ typedef struct se3icp_result {
     double time_se3_correspondence_search_ms; /* time_se3_correspondence_search_ */
     double time_before_pure_icp_ms;   /* time_before_pure_icp_: the whole run_se3_icp_with_cf
                                          (ISR.cpp:754, 957-958), GPU timeline; 0 for the other
-                                         methods (the reference never sets it there) */
+                                         methods (the reference never sets it there).
+                                         The times above are BATCH-WIDE: a batch of n_pairs > 1
+                                         registers its pairs in lockstep, and every pair gets
+                                         the batch's setup / loop / NN / total time, not a
+                                         per-pair share (the reference times one registration;
+                                         a batched caller divides by the batch size for a mean). */
 } se3icp_result;
 
 /* ------------------------------------------------------------- misc */
@@ -174,8 +179,9 @@ int se3icp_nn(int device, const double* query, int64_t nq, const double* data, i
  * [n_cases*16] row-major.  src_out / tgt_out: [n_cases*k*3] AoS, device pointers when
  * outputs_on_device (ready for se3icp_register_batch_device with offsets c*k), host
  * pointers otherwise.  Returns k (>= 0) or a negative se3icp_status.  Counter-based
- * random streams (Philox4x32-10 keyed by `seed`): same distributions as the
- * reference's mt19937 draws, not the same samples. */
+ * random streams (Philox4x32-10 keyed by `seed`, no host draws: any batch size in one pass):
+ * same distributions as the reference's mt19937 draws, not the same samples (for those:
+ * se3icp_synthetic_reference_device below). */
 int64_t se3icp_synthetic_pairs(int device, const double* base, int64_t n, int32_t n_cases, const double* T,
                                double ratio, double noise_var, uint64_t seed, double* src_out, double* tgt_out,
                                int outputs_on_device);
@@ -195,6 +201,16 @@ int64_t se3icp_synthetic_pairs(int device, const double* base, int64_t n, int32_
 int64_t se3icp_synthetic_reference(const double* cloud, int64_t n, int32_t n_cases, double ratio, double noise_var,
                                    double t_range, double r_range, int32_t flags, double* src_out, double* tgt_out,
                                    double* T_out);
+/* The same problems, number for number, written by the GPU for a whole batch: the host
+ * draws the reference's streams (as se3icp_synthetic_reference) and the device gathers,
+ * transforms (Transform's arithmetic, no FMA) and adds the noise, so src_out / tgt_out equal
+ * se3icp_synthetic_reference's bit for bit.  src_out / tgt_out: device pointers when
+ * outputs_on_device (ready for se3icp_register_batch_device with offsets c*k), host
+ * pointers otherwise; T_out: host [n_cases * 16] (may be NULL).  Returns k or a negative
+ * se3icp_status. */
+int64_t se3icp_synthetic_reference_device(int device, const double* cloud, int64_t n, int32_t n_cases, double ratio,
+                                          double noise_var, double t_range, double r_range, int32_t flags,
+                                          double* src_out, double* tgt_out, double* T_out, int outputs_on_device);
 /* PointCloud::RandomDownSample(ratio) right after utility::random::Seed(seed) (Open3D 0.19):
  * the kept points in file order into out [k * 3] (may be NULL); returns k. */
 int64_t se3icp_random_downsample(const double* xyz, int64_t n, double ratio, uint32_t seed, double* out);
@@ -242,11 +258,18 @@ typedef struct se3icp_trace {
 } se3icp_trace;
 int se3icp_set_trace(int device, se3icp_trace* trace);
 
-/* Diagnostic: 1 = compute the setup's kNN / TOLDI / normals with the exact one-query-per-
- * wavefront kernel for every point, 0 = the default (eight queries per wavefront, exact
- * kernel only for the queries it hands over).  Both give bitwise-identical results; the
- * tests check that.  Also settable with SE3ICP_LRF_EXACT=1. */
+/* Diagnostic: which kernels compute the setup's kNN / TOLDI / normals on `device`:
+ *   0 = the default: eight queries per wavefront (k_lrf8), the exact one-query-per-wavefront
+ *       kernel for the queries it hands over, the global-buffer kernel for k > 128;
+ *   1 = the exact one-query-per-wavefront kernel for every point (k <= 128);
+ *   2 = the global-buffer kernel (any k) for every point.
+ * All give bitwise-identical results; the tests check that. */
 int se3icp_set_lrf_exact(int device, int exact_only);
+
+/* Diagnostic: HIP events around the SE(3) NN grids of timed (non-profiled) batches, on by
+ * default; they fill time_se3_correspondence_search_ms.  Each marker leaves the GPU idle a
+ * few microseconds, so bench.py turns them off for its timed steps (the field is then 0). */
+int se3icp_set_nn_events(int device, int on);
 
 #ifdef __cplusplus
 }

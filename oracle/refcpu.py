@@ -108,10 +108,13 @@ def default_params(**overrides) -> Params:
     return p
 
 
-def cli_params() -> Params:
+def cli_params(**overrides) -> Params:
     """Overrides of examples/run_registration_method.cpp:38-42."""
-    return default_params(estimated_overlap=1.0, max_num_se3_iterations=10, mse=1e-5,
-                          mse_switch_error=5e-5, number_of_nn_for_LRF=90)
+    p = default_params(estimated_overlap=1.0, max_num_se3_iterations=10, mse=1e-5,
+                       mse_switch_error=5e-5, number_of_nn_for_LRF=90)
+    for k, v in overrides.items():
+        setattr(p, k, v)
+    return p
 
 
 def set_num_threads(n: int) -> None:

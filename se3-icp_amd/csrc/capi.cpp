@@ -60,7 +60,7 @@ const char* se3icp_status_string(int status) {
         case SE3ICP_ERR_INVALID_ARG: return "invalid argument";
         case SE3ICP_ERR_INVALID_METHOD: return "invalid method name";
         case SE3ICP_ERR_EMPTY_CLOUD: return "empty point cloud";
-        case SE3ICP_ERR_K_TOO_LARGE: return "number_of_nn_for_LRF exceeds SE3ICP_MAX_KNN";
+        case SE3ICP_ERR_K_TOO_LARGE: return "number_of_nn_for_LRF too large (unused since ABI 3: any k is taken)";
         case SE3ICP_ERR_NO_DEVICE: return "no usable HIP device (the engine has no CPU fallback)";
         case SE3ICP_ERR_HIP: return "HIP runtime error";
         case SE3ICP_ERR_NONFINITE: return "non-finite pose";
@@ -291,7 +291,16 @@ int se3icp_set_lrf_exact(int device, int exact_only) {
     Engine* e = usable_engine(device);
     if (!e) return SE3ICP_ERR_NO_DEVICE;
     std::lock_guard<std::mutex> lk(e->mutex());
-    e->set_lrf_exact(exact_only != 0);
+    if (exact_only < 0 || exact_only > 2) return SE3ICP_ERR_INVALID_ARG;
+    e->set_lrf_exact(exact_only);
+    return 0;
+}
+
+int se3icp_set_nn_events(int device, int on) {
+    Engine* e = usable_engine(device);
+    if (!e) return SE3ICP_ERR_NO_DEVICE;
+    std::lock_guard<std::mutex> lk(e->mutex());
+    e->set_nn_events(on != 0);
     return 0;
 }
 

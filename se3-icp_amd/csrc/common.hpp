@@ -17,7 +17,7 @@
 
 namespace se3icp {
 
-constexpr int kMaxKnn = 128;      // SE3ICP_MAX_KNN
+constexpr int kSmallK = 128;      // neighbourhoods the LDS kNN kernels hold; larger ones: k_knn_big.hip
 constexpr int kBlock = 256;       // threads per block of the streaming/sweep kernels
 constexpr int kRedVals = 28;      // 21 JTJ upper + 6 JTr + 1 mse-sum (pt2pt reuses the slots)
 constexpr int kStatCols = 12;     // columns of the device work-counter table (View::stats); 8..11: SE3ICP_PROF section cycles

@@ -113,14 +113,9 @@ int Engine::init() {
     if (hipGetDeviceCount(&n) != hipSuccess || dev_ < 0 || dev_ >= n) return SE3ICP_ERR_NO_DEVICE;
     HIPCHK(hipSetDevice(dev_));
     HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    HIPCHK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
-    if (const char* e = std::getenv("SE3ICP_LRF_SPLIT")) lrf_split_ = std::max(0, std::min(99, std::atoi(e)));
     for (auto& e : ev_) HIPCHK(hipEventCreate(&e));
     for (auto& e : loop_ev_) HIPCHK(hipEventCreate(&e));
-    if (const char* e = std::getenv("SE3ICP_L12_EXTRA")) l12_extra_ = std::max(0, std::min(2, std::atoi(e)));
     if (const char* e = std::getenv("SE3ICP_NN_TRACE")) nn_trace_ = std::atoi(e) != 0;
-    if (const char* e = std::getenv("SE3ICP_LRF_EXACT")) lrf_exact_only_ = std::atoi(e) != 0;
-    if (const char* e = std::getenv("SE3ICP_NN_EVENTS")) nn_events_ = std::atoi(e) != 0;
     return 0;
 }
 
@@ -133,7 +128,7 @@ Engine::~Engine() {
                      &d_red_out_, &d_work_, &d_wb_, &d_wn_, &d_chunks_, &d_partial_, &d_centers_,
                      &d_rechecked_, &d_keys0_, &d_vals1_, &d_sort_tmp_, &d_stats_,
                      &d_qlist_, &d_qcount_, &d_chunk_cost_, &d_chunk_order_, &d_hist_, &d_cert_, &d_sqlist_, &d_state_, &d_trim_cand_, &d_trim_ctr_, &d_scales_, &d_trim_hist_,
-                     &d_lrf_fb_, &d_lrf_fbn_,
+                     &d_lrf_fb_, &d_lrf_fbn_, &d_big_d_, &d_big_i_,
                      &t3_.perm, &t3_.pos, &t3_.vec, &t3_.blo, &t3_.bhi, &t3_.lo, &t3_.hi,
                      &t12_.perm, &t12_.pos, &t12_.vec, &t12_.blo, &t12_.bhi, &t12_.lo, &t12_.hi};
     for (DevBuf* b : all)
@@ -151,7 +146,6 @@ Engine::~Engine() {
         if (e) (void)hipEventDestroy(e);
     if (h_state_) (void)hipHostFree(h_state_);
     if (h_phase_) (void)hipHostFree(h_phase_);
-    if (side_) (void)hipStreamDestroy(side_);
     if (stream_) (void)hipStreamDestroy(stream_);
 }
 
@@ -257,7 +251,7 @@ View Engine::view() const {
 // ----------------------------------------------------------------------------- kd-trees
 int Engine::build_tree(int D, const float* vec, hipStream_t s, const double* vec64) {
     TreeBufs& tb = (D == 12) ? t12_ : t3_;
-    tb.L = tree_L_ + (D == 12 ? l12_extra_ : 0);
+    tb.L = tree_L_;
     const int nnodes = 2 << tb.L;
     const size_t nb = (size_t)nclouds_ * nnodes * D;
     if (!ensure<uint32_t>(tb.blo, nb) || !ensure<uint32_t>(tb.bhi, nb) || !ensure<float>(tb.lo, nb) ||
@@ -393,11 +387,36 @@ int Engine::setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool nor
     if (any_knn) {
         HIPCHK(hipMemsetAsync(d_stats_.p, 0, sizeof(unsigned long long) * kStatCols * kStatSlots, s));
         HIPCHK(hipEventRecord(ev_[6], s));
-        if (knn_list_ || lrf_exact_only_) {
+        // neighbourhoods over kSmallK (Kw = min(k, n)) go to k_knn_big, the rest to the LDS
+        // kernels; the global-buffer kernel's candidate buffers are sized to the largest
+        int kw_big = 0, n_big = 0;
+        for (int c = 0; c < nclouds_; ++c) {
+            const int kw = std::min<int>(h_setup_[c].k_knn, h_clouds_[c].n);
+            if (kw > kSmallK || lrf_exact_only_ == 2) {
+                kw_big = std::max(kw_big, kw);
+                n_big += h_clouds_[c].n;
+            }
+        }
+        int big_cap = 0, big_blocks = 0;
+        if (n_big > 0) {
+            big_cap = knn_big_cap(kw_big);
+            big_blocks = knn_big_blocks(big_cap, n_big);
+            if (!ensure<double>(d_big_d_, (size_t)big_blocks * big_cap) || !ensure<int32_t>(d_big_i_, (size_t)big_blocks * big_cap))
+                return SE3ICP_ERR_OUT_OF_MEMORY;
+        }
+        auto big = [&](const int32_t* qlist, const int32_t* qcount, int k_min) {
+            if (n_big > 0)
+                launch_knn_big(v, knn_list_ ? 1 : 0, k_min, qlist, qcount, big_blocks, (double*)d_big_d_.p,
+                               (int32_t*)d_big_i_.p, big_cap, s);
+        };
+        if (lrf_exact_only_ == 2) {
+            big(nullptr, nullptr, 0);  // (diagnostic: every query through the global-buffer kernel)
+        } else if (knn_list_ || lrf_exact_only_ == 1) {
             launch_lrf(v, knn_list_ ? 1 : 0, s);  // the sorted lists (se3icp_knn_self) need the exact kernel
+            big(nullptr, nullptr, kSmallK);
         } else {
-            // eight queries per wavefront; the few it cannot resolve from f32 keys go to
-            // the exact one-query-per-wavefront kernel
+            // eight queries per wavefront; the few it cannot resolve from f32 keys (and every
+            // query of a cloud whose k it cannot hold) go to the exact kernels
             // waves aligned to each cloud's first point (results independent of the batch)
             std::vector<int32_t> wb(nclouds_ + 1, 0);
             for (int c = 0; c < nclouds_; ++c) wb[c + 1] = wb[c] + (h_clouds_[c].n + 7) / 8;
@@ -409,24 +428,9 @@ int Engine::setup_clouds(std::vector<CloudReq>& clouds, bool on_device, bool nor
             int32_t* fbn = (int32_t*)d_lrf_fbn_.p;
             HIPCHK(hipMemsetAsync(fbn, 0, 2 * sizeof(int32_t), s));
             HIPCHK(hipMemcpyAsync(d_wb, wb.data(), sizeof(int32_t) * (nclouds_ + 1), hipMemcpyHostToDevice, s));
-            // The exact pass is latency-bound (a few thousand queries, one wave each) and
-            // k_lrf8 issue-bound: the first lrf_split_ % of the waves' hand-overs are
-            // resolved on the side stream while k_lrf8 runs the rest; the last part's
-            // hand-overs (one query per wave) close the setup's kNN on the main stream.
-            const int nwa = lrf_split_ > 0 ? (int)((long long)nw * lrf_split_ / 100) : nw;
-            launch_lrf8(v, d_wb, 0, nwa, fb, fbn, s);
-            if (nwa < nw && nwa > 0) {
-                HIPCHK(hipEventRecord(ev_[8], s));
-                HIPCHK(hipStreamWaitEvent(side_, ev_[8], 0));
-                launch_lrf_list(v, fb, fbn, side_);
-                HIPCHK(hipEventRecord(ev_[9], side_));
-                launch_lrf8(v, d_wb, nwa, nw, fb + (size_t)8 * nwa, fbn + 1, s);
-                launch_lrf_list(v, fb + (size_t)8 * nwa, fbn + 1, s, 1);
-                HIPCHK(hipStreamWaitEvent(s, ev_[9], 0));
-            } else {
-                launch_lrf8(v, d_wb, nwa, nw, fb, fbn, s);
-                launch_lrf_list(v, fb, fbn, s);
-            }
+            launch_lrf8(v, d_wb, 0, nw, fb, fbn, s);
+            launch_lrf_list(v, fb, fbn, s);
+            big(fb, fbn, kSmallK);
         }
         HIPCHK(hipEventRecord(ev_[7], s));
         HIPCHK(hipGetLastError());
@@ -524,7 +528,6 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     if (mi.est == EST_PT2PL) k_nrm_t = 30;                    // target_.EstimateNormals() default KNN(30)
     if (mi.est == EST_GICP) { k_nrm_s = 20; k_nrm_t = 20; }   // InitializePointCloudForGeneralizedICP KNN(20)
     const int kmax = std::max({k_lrf, k_nrm_s, k_nrm_t, 1});
-    if (kmax > kMaxKnn) return SE3ICP_ERR_K_TOO_LARGE;
     HIPCHK(hipSetDevice(dev_));
     hipStream_t s = user_stream ? user_stream : stream_;
     ktimes_ = KernelTimes{};
@@ -890,7 +893,6 @@ int Engine::knn_self(const double* xyz, int64_t n, int k, int32_t* idx) {
     if (!ok_) return SE3ICP_ERR_NO_DEVICE;
     if (!xyz || !idx || n <= 0) return n <= 0 ? SE3ICP_ERR_EMPTY_CLOUD : SE3ICP_ERR_INVALID_ARG;
     if (k <= 0) return SE3ICP_ERR_INVALID_ARG;
-    if (k > kMaxKnn) return SE3ICP_ERR_K_TOO_LARGE;
     HIPCHK(hipSetDevice(dev_));
     npairs_ = 0;
     int rc = alloc_points(n, k, true);
@@ -912,7 +914,6 @@ int Engine::toldi_frames(const double* xyz, int64_t n, int k, double* frames) {
     if (!ok_) return SE3ICP_ERR_NO_DEVICE;
     if (!xyz || !frames || n <= 0) return n <= 0 ? SE3ICP_ERR_EMPTY_CLOUD : SE3ICP_ERR_INVALID_ARG;
     if (k <= 0) return SE3ICP_ERR_INVALID_ARG;
-    if (k > kMaxKnn) return SE3ICP_ERR_K_TOO_LARGE;
     HIPCHK(hipSetDevice(dev_));
     npairs_ = 0;
     int rc = alloc_points(n, k);
@@ -947,7 +948,6 @@ int Engine::estimate_normals(const double* xyz, int64_t n, int k, double* normal
     if (!ok_) return SE3ICP_ERR_NO_DEVICE;
     if (!xyz || !normals || n <= 0) return n <= 0 ? SE3ICP_ERR_EMPTY_CLOUD : SE3ICP_ERR_INVALID_ARG;
     if (k <= 0) return SE3ICP_ERR_INVALID_ARG;
-    if (k > kMaxKnn) return SE3ICP_ERR_K_TOO_LARGE;
     HIPCHK(hipSetDevice(dev_));
     npairs_ = 0;
     int rc = alloc_points(n, k);

@@ -51,7 +51,8 @@ class Engine {
     std::mutex& mutex() { return mu_; }
     void set_profiling(bool on) { profile_ = on; }
     void set_trace(se3icp_trace* t) { trace_ = t; }
-    void set_lrf_exact(bool on) { lrf_exact_only_ = on; }
+    void set_lrf_exact(int mode) { lrf_exact_only_ = mode; }
+    void set_nn_events(bool on) { nn_events_ = on; }
     const KernelTimes& kernel_times() const { return ktimes_; }
 
     int register_batch(int npairs, const double* const* src, const int64_t* ns, const double* const* tgt,
@@ -96,7 +97,6 @@ class Engine {
     bool profile_ = false;
     std::mutex mu_;
     hipStream_t stream_ = nullptr;
-    hipStream_t side_ = nullptr;  // the exact hand-over pass of the setup, beside k_lrf8
     KernelTimes ktimes_;
 
     // geometry of the current batch
@@ -106,15 +106,15 @@ class Engine {
     int chunk_level_ = 0, nchunks_ = 0;  // loop NN work chunks (View::chunk_level)
     bool have12_ = false, knn_list_ = false;
     bool nn_trace_ = false;              // SE3ICP_NN_TRACE=1: per-iteration NN work on stderr
-    bool lrf_exact_only_ = false;        // SE3ICP_LRF_EXACT=1: the one-query-per-wavefront k_lrf for every point
-    // SE3ICP_NN_EVENTS=0: no HIP events around the SE(3) NN grids outside profiled batches
-    // (each marker leaves the GPU idle ~5 us; time_se3_correspondence_search_ms is then 0)
+    // se3icp_set_lrf_exact: 0 k_lrf8 + hand-overs (default), 1 the exact one-query-per-wavefront
+    // k_lrf for every point, 2 the global-buffer k_knn_big for every point (all bitwise equal)
+    int lrf_exact_only_ = 0;
+    // se3icp_set_nn_events(0): no HIP events around the SE(3) NN grids outside profiled
+    // batches (each marker leaves the GPU idle ~5 us; time_se3_correspondence_search_ms is then 0)
     bool nn_events_ = true;
-    int lrf_split_ = 0;                  // SE3ICP_LRF_SPLIT: % of k_lrf8 waves whose hand-overs run beside the rest (0: after all; A/B 80 / 88 / 93: k_lrf +3-5 %)
     se3icp_trace* trace_ = nullptr;      // armed per-iteration record of one pair (se3icp_set_trace)
     int record_trace(se3icp_trace* tr, int it, int& phase_of_it, hipStream_t s);
     double trace_prev_[kStatCols] = {};
-    int l12_extra_ = 0;  // extra levels of the 12-D trees (0: leaves of <= 64 targets, measured fastest with compacted sweeps)
     std::vector<CloudDev> h_clouds_;
     std::vector<CloudSetup> h_setup_;
     std::vector<BlockWork> h_work_;
@@ -128,7 +128,8 @@ class Engine {
         d_trim_key_, d_red_partial_, d_red_out_, d_work_, d_wb_, d_wn_, d_chunks_, d_partial_, d_centers_,
         d_rechecked_, d_keys0_, d_vals1_, d_sort_tmp_, d_stats_, d_qlist_, d_qcount_, d_chunk_cost_, d_chunk_order_, d_hist_, d_cert_,
         d_sqlist_, d_state_, d_trim_cand_, d_trim_ctr_, d_scales_, d_trim_hist_,
-        d_lrf_fb_, d_lrf_fbn_;  // k_lrf8 -> exact k_lrf hand-over list and its count
+        d_lrf_fb_, d_lrf_fbn_,  // k_lrf8 -> exact k_lrf hand-over list and its count
+        d_big_d_, d_big_i_;     // k_knn_big candidate buffers (neighbourhoods over kSmallK)
     TreeBufs t3_, t12_;
     // pinned host mirrors
     PairDev* h_pairs_ = nullptr;

@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <algorithm>
 #include <random>
 #include <vector>
 
@@ -24,6 +25,54 @@
 #include "se3icp.h"
 
 using namespace se3icp::refrand;
+
+namespace se3icp {
+namespace refrand {
+
+ReferenceDraws draw_reference(int64_t n, int32_t n_cases, double ratio, double t_range, double r_range,
+                              bool args_left_to_right, bool want_noise) {
+    ReferenceDraws D;
+    std::mt19937 o3d_engine(1);                      // open3d::utility::random::Seed(1)
+    const std::vector<int64_t> src_idx = random_downsample(n, ratio, o3d_engine);
+    const int64_t k = (int64_t)src_idx.size();
+    D.k = k;
+    D.src_idx.assign(src_idx.begin(), src_idx.end());
+    D.tgt_idx.resize((size_t)n_cases * k);
+    D.T.resize((size_t)n_cases * 16);
+    if (want_noise) D.z.resize((size_t)n_cases * 6 * k);
+    std::mt19937 gen(1);                             // B_SYN:103
+    std::uniform_real_distribution<double> dist_T(-t_range, t_range), dist_R(-r_range, r_range);
+    std::mt19937 noise_gen{1};                       // B_SYN:34-35 (static)
+    std::normal_distribution<> noise_dist;
+    for (int32_t c = 0; c < n_cases; ++c) {
+        double t[3];
+        for (double& v : t) v = dist_T(gen);
+        double roll, pitch, yaw;
+        if (args_left_to_right) {
+            roll = dist_R(gen); pitch = dist_R(gen); yaw = dist_R(gen);
+        } else {
+            yaw = dist_R(gen); pitch = dist_R(gen); roll = dist_R(gen);
+        }
+        double R[9];
+        double* T = D.T.data() + 16 * (size_t)c;
+        rot_3d(roll, pitch, yaw, R);
+        for (int r = 0; r < 3; ++r) {
+            for (int cc = 0; cc < 3; ++cc) T[4 * r + cc] = R[3 * r + cc];
+            T[4 * r + 3] = t[r];
+        }
+        T[12] = T[13] = T[14] = 0.0;
+        T[15] = 1.0;
+        const std::vector<int64_t> tgt_idx = random_downsample(n, ratio, o3d_engine);  // B_SYN:147-148
+        std::copy(tgt_idx.begin(), tgt_idx.end(), D.tgt_idx.begin() + (size_t)c * k);
+        // B_SYN:154-155: the source copy's noise first, then the target's
+        if (want_noise)
+            for (int64_t i = 0; i < 6 * k; ++i) D.z[(size_t)c * 6 * k + i] = noise_dist(noise_gen);
+    }
+    return D;
+}
+
+}  // namespace refrand
+}  // namespace se3icp
 
 extern "C" {
 
@@ -41,52 +90,26 @@ int64_t se3icp_synthetic_reference(const double* cloud, int64_t n, int32_t n_cas
                                    double* T_out) {
     if (!cloud || n <= 0 || n_cases < 0 || !(ratio >= 0.0 && ratio <= 1.0) || !(noise_var >= 0.0))
         return SE3ICP_ERR_INVALID_ARG;
-    std::mt19937 o3d_engine(1);                      // open3d::utility::random::Seed(1)
-    const std::vector<int64_t> src_idx = random_downsample(n, ratio, o3d_engine);
-    const int64_t k = (int64_t)src_idx.size();
-    std::mt19937 gen(1);                             // B_SYN:103
-    std::uniform_real_distribution<double> dist_T(-t_range, t_range), dist_R(-r_range, r_range);
-    std::mt19937 noise_gen{1};                       // B_SYN:34-35 (static)
-    std::normal_distribution<> noise_dist;
+    const ReferenceDraws D = draw_reference(n, n_cases, ratio, t_range, r_range, (flags & SE3ICP_GEN_ARGS_LTR) != 0,
+                                            src_out || tgt_out);
+    const int64_t k = D.k;
     const double sd = std::sqrt(noise_var);
-    auto add_noise = [&](double* p, int64_t m) {
-        for (int64_t i = 0; i < m; ++i) {
-            const double z0 = noise_dist(noise_gen), z1 = noise_dist(noise_gen), z2 = noise_dist(noise_gen);
-            p[3 * i] += sd * z0;
-            p[3 * i + 1] += sd * z1;
-            p[3 * i + 2] += sd * z2;
-        }
-    };
-    std::vector<double> moved((size_t)n * 3);
     for (int32_t c = 0; c < n_cases; ++c) {
-        double t[3];
-        for (double& v : t) v = dist_T(gen);
-        double roll, pitch, yaw;
-        if (flags & SE3ICP_GEN_ARGS_LTR) {
-            roll = dist_R(gen); pitch = dist_R(gen); yaw = dist_R(gen);
-        } else {
-            yaw = dist_R(gen); pitch = dist_R(gen); roll = dist_R(gen);
+        const double* T = D.T.data() + 16 * (size_t)c;
+        if (T_out) std::memcpy(T_out + 16 * (size_t)c, T, 16 * sizeof(double));
+        const double* zs = D.z.data() + (size_t)c * 6 * k;
+        const double* zt = zs + 3 * k;
+        for (int64_t i = 0; i < k && src_out; ++i) {  // add_noise_to_point_cloud: p += sd * z
+            double* o = src_out + ((size_t)c * k + i) * 3;
+            const double* p = cloud + 3 * (size_t)D.src_idx[(size_t)i];
+            for (int a = 0; a < 3; ++a) o[a] = p[a] + sd * zs[3 * i + a];
         }
-        double R[9], T[16];
-        rot_3d(roll, pitch, yaw, R);
-        for (int r = 0; r < 3; ++r) {
-            for (int cc = 0; cc < 3; ++cc) T[4 * r + cc] = R[3 * r + cc];
-            T[4 * r + 3] = t[r];
+        for (int64_t i = 0; i < k && tgt_out; ++i) {  // Transform(T) of the full cloud, then the subset
+            double* o = tgt_out + ((size_t)c * k + i) * 3;
+            double q[3];
+            transform_point(T, cloud + 3 * (size_t)D.tgt_idx[(size_t)c * k + i], q);
+            for (int a = 0; a < 3; ++a) o[a] = q[a] + sd * zt[3 * i + a];
         }
-        T[12] = T[13] = T[14] = 0.0;
-        T[15] = 1.0;
-        if (T_out) std::memcpy(T_out + 16 * (size_t)c, T, sizeof(T));
-        for (int64_t i = 0; i < n; ++i) transform_point(T, cloud + 3 * i, moved.data() + 3 * i);
-        const std::vector<int64_t> tgt_idx = random_downsample(n, ratio, o3d_engine);
-        double* so = src_out ? src_out + (size_t)c * k * 3 : nullptr;
-        double* to = tgt_out ? tgt_out + (size_t)c * k * 3 : nullptr;
-        std::vector<double> tmp_s, tmp_t;
-        if (!so) { tmp_s.resize((size_t)k * 3); so = tmp_s.data(); }
-        if (!to) { tmp_t.resize((size_t)k * 3); to = tmp_t.data(); }
-        for (int64_t i = 0; i < k; ++i) std::memcpy(so + 3 * i, cloud + 3 * src_idx[(size_t)i], 3 * sizeof(double));
-        for (int64_t i = 0; i < k; ++i) std::memcpy(to + 3 * i, moved.data() + 3 * tgt_idx[(size_t)i], 3 * sizeof(double));
-        add_noise(so, k);  // B_SYN:154-155: source copy first, then the target
-        add_noise(to, k);
     }
     return k;
 }

@@ -15,12 +15,21 @@
 // or shared state).  The noise is Box-Muller on Philox4x32-10 counters (seed, case,
 // side, point).  Counter-based streams replace the reference's mt19937 so that a GPU batch
 // of any size is made in one pass: the protocol and its distributions are the same, the
-// individual samples are not (tests/test_generators.py; the exact samples are
-// se3icp_synthetic_reference, tests/test_reference_streams.py).
+// individual samples are not (tests/test_generators.py).
+//
+// se3icp_synthetic_reference_device is the reference-exact batch: the host draws the
+// driver's own streams (refrand.hpp draw_reference: Open3D's shuffle, mt19937 T, the
+// static normal_distribution noise) and k_apply_reference gathers, transforms and adds the
+// noise with se3icp_synthetic_reference's arithmetic (Transform without FMA, p + sd * z), so
+// the device clouds equal the host's bit for bit (tests/test_generators.py).
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
 
+#include <cmath>
+#include <cstring>
+
+#include "refrand.hpp"
 #include "se3icp.h"
 
 namespace se3icp {
@@ -112,6 +121,37 @@ __global__ __launch_bounds__(256) void k_synthetic(const double* __restrict__ ba
     out[2] = p[2] + sd * r1 * cos(a1);
 }
 
+// one thread per output point: out = (T_c * cloud[idx] for a target) + sd * z, no FMA
+// (refrand.hpp transform_point; add_noise_to_point_cloud, B_SYN:13-56)
+__global__ __launch_bounds__(256) void k_apply_reference(const double* __restrict__ cloud,
+                                                         const int32_t* __restrict__ src_idx,
+                                                         const int32_t* __restrict__ tgt_idx,
+                                                         const double* __restrict__ T, const double* __restrict__ z,
+                                                         int64_t k, int n_cases, double sd, double* __restrict__ src,
+                                                         double* __restrict__ tgt) {
+#pragma clang fp contract(off)
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t per_side = (int64_t)n_cases * k;
+    if (t >= 2 * per_side) return;
+    const int side = (int)(t / per_side);
+    const int64_t r = t - side * per_side;
+    const int64_t c = r / k, i = r - c * k;
+    const double* zz = z + ((size_t)c * 6 * k + (size_t)side * 3 * k + 3 * (size_t)i);
+    double p[3];
+    if (side == 0) {
+        const double* a = cloud + 3 * (size_t)src_idx[i];
+        p[0] = a[0]; p[1] = a[1]; p[2] = a[2];
+    } else {
+        const double* a = cloud + 3 * (size_t)tgt_idx[r];
+        const double* M = T + 16 * (size_t)c;
+#pragma unroll
+        for (int e = 0; e < 3; ++e) p[e] = ((M[4 * e] * a[0] + M[4 * e + 1] * a[1]) + M[4 * e + 2] * a[2]) + M[4 * e + 3] * 1.0;
+    }
+    double* out = (side == 0 ? src : tgt) + 3 * (size_t)r;
+#pragma unroll
+    for (int e = 0; e < 3; ++e) out[e] = p[e] + sd * zz[e];
+}
+
 struct DevMem {
     void* p = nullptr;
     ~DevMem() {
@@ -160,6 +200,58 @@ extern "C" int64_t se3icp_synthetic_pairs(int device, const double* base, int64_
     hipLaunchKernelGGL(k_synthetic, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, 0, (const double*)d_base.p,
                        (uint32_t)n, (uint32_t)k, (int)n_cases, (const double*)d_T.p, sqrt(noise_var), h,
                        (uint32_t)seed, (uint32_t)(seed >> 32), so, to);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) return SE3ICP_ERR_HIP;
+    if (!outputs_on_device) {
+        if (hipMemcpy(src_out, so, out_bytes, hipMemcpyDeviceToHost) != hipSuccess ||
+            hipMemcpy(tgt_out, to, out_bytes, hipMemcpyDeviceToHost) != hipSuccess)
+            return SE3ICP_ERR_HIP;
+    }
+    return k;
+}
+
+extern "C" int64_t se3icp_synthetic_reference_device(int device, const double* cloud, int64_t n, int32_t n_cases,
+                                                     double ratio, double noise_var, double t_range, double r_range,
+                                                     int32_t flags, double* src_out, double* tgt_out, double* T_out,
+                                                     int outputs_on_device) {
+    using namespace se3icp;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return SE3ICP_ERR_NO_DEVICE;
+    if (!cloud || !src_out || !tgt_out || n_cases <= 0 || !(ratio >= 0.0 && ratio <= 1.0) || !(noise_var >= 0.0))
+        return SE3ICP_ERR_INVALID_ARG;
+    if (n <= 0) return SE3ICP_ERR_EMPTY_CLOUD;
+    if (n >= (int64_t)1 << 30) return SE3ICP_ERR_INVALID_ARG;
+    const refrand::ReferenceDraws D =
+        refrand::draw_reference(n, n_cases, ratio, t_range, r_range, (flags & SE3ICP_GEN_ARGS_LTR) != 0, true);
+    const int64_t k = D.k;
+    if (T_out) std::memcpy(T_out, D.T.data(), sizeof(double) * 16 * (size_t)n_cases);
+    if (k <= 0) return 0;
+    if (hipSetDevice(device) != hipSuccess) return SE3ICP_ERR_HIP;
+    const size_t out_bytes = sizeof(double) * 3 * (size_t)n_cases * (size_t)k;
+    DevMem d_cloud, d_si, d_ti, d_T, d_z, d_src, d_tgt;
+    if (hipMalloc(&d_cloud.p, sizeof(double) * 3 * (size_t)n) != hipSuccess ||
+        hipMalloc(&d_si.p, sizeof(int32_t) * D.src_idx.size()) != hipSuccess ||
+        hipMalloc(&d_ti.p, sizeof(int32_t) * D.tgt_idx.size()) != hipSuccess ||
+        hipMalloc(&d_T.p, sizeof(double) * D.T.size()) != hipSuccess ||
+        hipMalloc(&d_z.p, sizeof(double) * D.z.size()) != hipSuccess)
+        return SE3ICP_ERR_OUT_OF_MEMORY;
+    double* so = src_out;
+    double* to = tgt_out;
+    if (!outputs_on_device) {
+        if (hipMalloc(&d_src.p, out_bytes) != hipSuccess || hipMalloc(&d_tgt.p, out_bytes) != hipSuccess)
+            return SE3ICP_ERR_OUT_OF_MEMORY;
+        so = (double*)d_src.p;
+        to = (double*)d_tgt.p;
+    }
+    if (hipMemcpy(d_cloud.p, cloud, sizeof(double) * 3 * (size_t)n, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_si.p, D.src_idx.data(), sizeof(int32_t) * D.src_idx.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_ti.p, D.tgt_idx.data(), sizeof(int32_t) * D.tgt_idx.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_T.p, D.T.data(), sizeof(double) * D.T.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_z.p, D.z.data(), sizeof(double) * D.z.size(), hipMemcpyHostToDevice) != hipSuccess)
+        return SE3ICP_ERR_HIP;
+    const int64_t total = 2 * (int64_t)n_cases * k;
+    hipLaunchKernelGGL(k_apply_reference, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, 0,
+                       (const double*)d_cloud.p, (const int32_t*)d_si.p, (const int32_t*)d_ti.p, (const double*)d_T.p,
+                       (const double*)d_z.p, k, (int)n_cases, std::sqrt(noise_var), so, to);
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) return SE3ICP_ERR_HIP;
     if (!outputs_on_device) {
         if (hipMemcpy(src_out, so, out_bytes, hipMemcpyDeviceToHost) != hipSuccess ||

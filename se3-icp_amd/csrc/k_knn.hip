@@ -209,7 +209,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
     const double* TZ = T.tvec64 + 2 * (size_t)v.ld;
     const int first_leaf = (1 << T.L) - 1;
     double* park = &s_park[wid][0][0];
-    int* s_nbw = s_dyn + (size_t)wid * kQ * v.kmax;
+    const int ks = min(v.kmax, kSmallK);  // list stride: k_knn_big.hip takes Kw > kSmallK
+    int* s_nbw = s_dyn + (size_t)wid * kQ * ks;
     if (lane < kQ) park[lane * PK_N + PK_FLAGS] = 0.0;
     // previous query of the wave (same cloud): its k-th distance bounds the next one's
     int prev_c = -1, prev_K = 0;
@@ -239,6 +240,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
         const float* box_lo = tlo + (size_t)c * T.nnodes * 3;
         const float* box_hi = thi + (size_t)c * T.nnodes * 3;
         const int Kw = min(K, n);
+        if (Kw > kSmallK) continue;  // (k_knn_big.hip)
         const int own = first_leaf + tree_node_of(w - cl.off, n, T.L);
         ++n_queries;
         PROF_NOW(t_q0);
@@ -456,9 +458,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
         // global memory inside this loop, which lets the compiler keep the per-cloud
         // records and node boxes on the scalar path
         {
-            int* nbl = (s_nbw + j * v.kmax);
-            const int nstore = write_knn ? K : nTop;
-            for (int r = lane; r < nstore; r += 64) nbl[r] = r < nTop ? bi[r] : -1;
+            int* nbl = (s_nbw + j * ks);
+            for (int r = lane; r < nTop; r += 64) nbl[r] = bi[r];
         }
         if (lane == 0) {
             double* pj = park + j * PK_N;
@@ -501,7 +502,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
             const double* Z = TZ;
             const double qx = TX[w], qy = TY[w], qz = TZ[w];
             const int nTop = (int)pj[PK_NTOP];
-            const int* nbl = s_nbw + qj * v.kmax;
+            const int* nbl = s_nbw + qj * ks;
             if (flags & 1) {
                 const int kk = min(setup[c].k_lrf, nTop);
                 const int rz = kk / 3;
@@ -565,12 +566,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
         for (int j = 0; j < kQ; ++j) {
             const double* pj = park + j * PK_N;
             if (!((int)pj[PK_FLAGS] & 4)) continue;
-            const int K = (int)pj[PK_K];
+            const int K = (int)pj[PK_K], nTop = (int)pj[PK_NTOP];
             int* out = v.knn + (size_t)(int)pj[PK_GP] * v.kmax;
-            for (int r = lane; r < K; r += 64) {
-                const int sl = s_nbw[j * v.kmax + r];
-                out[r] = sl >= 0 ? T.perm[sl] : -1;
-            }
+            for (int r = lane; r < K; r += 64) out[r] = r < nTop ? T.perm[s_nbw[j * ks + r]] : -1;
         }
     }
     __syncthreads();
@@ -650,7 +648,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
             const double qx = TX[w], qy = TY[w], qz = TZ[w];
             const double R = pj[PK_R];
             const int kk = (int)pj[PK_KK];
-            const int* nbl = s_nbw + qj * v.kmax;
+            const int* nbl = s_nbw + qj * ks;
             for (int r = 1 + qs; r < kk; r += 8) {
                 const int q = nbl[r];
                 const double vx = X[q] - qx, vy = Y[q] - qy, vz = Z[q] - qz;
@@ -716,7 +714,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
 
 void launch_lrf(const View& v, int write_knn, hipStream_t s) {
     const int nw = (v.npts + kQ - 1) / kQ;
-    const size_t lds = sizeof(int) * (size_t)kWaves * kQ * v.kmax;
+    const size_t lds = sizeof(int) * (size_t)kWaves * kQ * std::min(v.kmax, kSmallK);
     hipLaunchKernelGGL(k_lrf, dim3((nw + kWaves - 1) / kWaves), dim3(64 * kWaves), lds, s, v, write_knn, v.cloud_of,
                        v.setup, v.clouds, v.t3.lo, v.t3.hi, nullptr, nullptr, kQ);
 }
@@ -728,7 +726,7 @@ void launch_lrf(const View& v, int write_knn, hipStream_t s) {
 #define SE3ICP_LRF_LIST_BLOCKS 1024
 #endif
 void launch_lrf_list(const View& v, const int32_t* qlist, const int32_t* qcount, hipStream_t s, int qpw) {
-    const size_t lds = sizeof(int) * (size_t)kWaves * kQ * v.kmax;
+    const size_t lds = sizeof(int) * (size_t)kWaves * kQ * std::min(v.kmax, kSmallK);
     const int nblk = std::max(1, std::min(SE3ICP_LRF_LIST_BLOCKS, (v.npts + kWaves * kQ - 1) / (kWaves * kQ)));
     hipLaunchKernelGGL(k_lrf, dim3(nblk), dim3(64 * kWaves), lds, s, v, 0, v.cloud_of, v.setup, v.clouds, v.t3.lo,
                        v.t3.hi, qlist, qcount, qpw > 0 ? std::min(qpw, kQ) : SE3ICP_LRF_LIST_QPW);

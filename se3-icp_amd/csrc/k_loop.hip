@@ -625,8 +625,11 @@ __global__ __launch_bounds__(256) void k_reduce(View v) {
 // switch / convergence: pairmath.hpp) and opens iteration it+1 (PairDev, pose history
 // row), so the next iteration's kernels are already queued behind this one.
 // next_phase[p] receives pair p's phase in iteration it+1 (PHASE_IDLE once finished); it
-// lives in coherent host memory, so the host reads it once the kernel has completed,
-// without a copy.
+// lives in coherent host memory, and the host polls it (engine.cpp spin_phases) and goes on
+// as soon as every pair's slot is written -- possibly before this kernel has completed.
+// So the slot is the only value the host may read without ordering: any host read of
+// other device state after finish() must stay stream-ordered (an async copy on the stream,
+// then a sync), as the engine's result copies are.
 __global__ __launch_bounds__(256) void k_reduce_final(View v, const int32_t* pair_wb, const int32_t* pair_wn,
                                                       PairState* state, double* hist, int32_t* next_phase) {
     const int p = blockIdx.x;

@@ -10,7 +10,7 @@
 // Pinned by the reference's own fixture: created_example_reg_problem/source.ply is the
 // RandomDownSample(0.02) of stanford_bunny.ply x 50 under Seed(1), and target.ply its
 // Transform by rot_3d(pi/9, pi/8, -pi/7), t = (1, 2, 3) -- both reproduced exactly
-// (tests/test_generators.py).
+// (tests/test_reference_streams.py).
 #pragma once
 #include <algorithm>
 #include <cmath>
@@ -64,6 +64,21 @@ inline std::vector<int64_t> random_downsample(int64_t n, double ratio, std::mt19
         if (mask[(size_t)i]) out.push_back(i);
     return out;
 }
+
+// Every random draw of examples/benchmark_synthetic.cpp:91-160 for n_cases cases, in the
+// driver's order of use (gen_ref.cpp): the shared source subset, per case T and the target
+// subset, and the N(0, 1) noise words (source copy then target, case after case).  Applied
+// by se3icp_synthetic_reference on the host and by k_gen.hip k_apply_reference on the GPU
+// with the same arithmetic (no FMA), so both give the same bits.
+struct ReferenceDraws {
+    int64_t k = 0;                  // (int)(ratio * n) points per cloud
+    std::vector<int32_t> src_idx;   // [k] kept indices of the shared source subset, ascending
+    std::vector<int32_t> tgt_idx;   // [n_cases * k] per case, ascending
+    std::vector<double> T;          // [n_cases * 16] row-major
+    std::vector<double> z;          // [n_cases * 2 * k * 3]: case c: source (k x 3) then target (k x 3)
+};
+ReferenceDraws draw_reference(int64_t n, int32_t n_cases, double ratio, double t_range, double r_range,
+                              bool args_left_to_right, bool want_noise);
 
 }  // namespace refrand
 }  // namespace se3icp

@@ -126,6 +126,13 @@ void launch_lrf_list(const View& v, const int32_t* qlist, const int32_t* qcount,
 // caller) for launch_lrf_list
 void launch_lrf8(const View& v, const int32_t* wave_base, int w_lo, int w_hi, int32_t* fb_list, int32_t* fb_count,
                  hipStream_t s);
+// neighbourhoods over kSmallK (k_knn_big.hip): one wavefront per query with a global-memory
+// candidate buffer of `cap` entries per block; queries with Kw = min(k, n) <= k_min are
+// skipped (the LDS kernels'); qlist = nullptr: every point
+int knn_big_cap(int kw_max);
+int knn_big_blocks(int cap, int nq);
+void launch_knn_big(const View& v, int write_knn, int k_min, const int32_t* qlist, const int32_t* qcount, int nblocks,
+                    double* scratch_d, int32_t* scratch_i, int cap, hipStream_t s);
 
 // ---- k_loop.hip
 // exact 1-NN of every active pair's source points: k_nn_prep settles the queries whose

@@ -3,7 +3,7 @@
 Drop-in for kenahm/se3-icp's ``IterativeSE3Registration`` (see registration.py);
 the registration itself runs in hand-written HIP kernels for gfx950 (csrc/).
 """
-from ._lib import (MAX_KNN, METHODS, Params, Result, Se3IcpError, default_params, device_count, load,  # noqa: F401
+from ._lib import (METHODS, Params, Result, Se3IcpError, default_params, device_count, load,  # noqa: F401
                    method_id, status_string)
 from .io import read_ply_xyz, write_ply_xyz  # noqa: F401
 from .registration import (DeviceBatchRunner, IterativeSE3Registration, PairResult, cli_params,  # noqa: F401
@@ -14,5 +14,5 @@ from .registration import (DeviceBatchRunner, IterativeSE3Registration, PairResu
 __all__ = [
     "IterativeSE3Registration", "register_batch", "register_batch_device", "DeviceBatchRunner", "register_batch_traced", "toldi_frames", "knn_self",
     "estimate_normals", "nearest_neighbors", "default_params", "cli_params", "kitti_params", "lounge_params",
-    "read_ply_xyz", "write_ply_xyz", "METHODS", "MAX_KNN", "Se3IcpError",
+    "read_ply_xyz", "write_ply_xyz", "METHODS", "Se3IcpError",
 ]

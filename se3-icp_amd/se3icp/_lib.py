@@ -21,7 +21,6 @@ ERR_NO_DEVICE = -5
 ERR_HIP = -6
 ERR_NONFINITE = -7
 ERR_OUT_OF_MEMORY = -8
-MAX_KNN = 128
 
 METHODS = ["pt2pt", "pt2pl", "gicp", "se3_pt2pt", "se3_pt2pl", "se3_gicp", "se3_gicp_with_cf",
            "se3_pure_pt2pt", "se3_pure_pt2pl", "se3_pure_gicp"]
@@ -35,8 +34,10 @@ EXPORTED_SYMBOLS = [
     "se3icp_get_result",
     "se3icp_register_batch", "se3icp_register_batch_device", "se3icp_register",
     "se3icp_toldi_frames", "se3icp_knn_self", "se3icp_estimate_normals", "se3icp_nn",
-    "se3icp_synthetic_pairs", "se3icp_synthetic_reference", "se3icp_random_downsample",
+    "se3icp_synthetic_pairs", "se3icp_synthetic_reference", "se3icp_synthetic_reference_device",
+    "se3icp_random_downsample",
     "se3icp_set_profiling", "se3icp_last_kernel_times", "se3icp_set_trace", "se3icp_set_lrf_exact",
+    "se3icp_set_nn_events",
     # include/se3icp_cc.h: metrics and pose files of the benchmark drivers (host only)
     "se3icp_cc_rot_3d", "se3icp_cc_angular_error_so3", "se3icp_cc_angular_error_so3_alt",
     "se3icp_cc_error_filterreg", "se3icp_cc_rot2euler", "se3icp_cc_avg_eul_error",
@@ -147,12 +148,16 @@ def load():
     L.se3icp_synthetic_reference.restype = C.c_int64
     L.se3icp_synthetic_reference.argtypes = [dp, C.c_int64, C.c_int32, C.c_double, C.c_double, C.c_double, C.c_double,
                                              C.c_int32, dp, dp, dp]
+    L.se3icp_synthetic_reference_device.restype = C.c_int64
+    L.se3icp_synthetic_reference_device.argtypes = [C.c_int, dp, C.c_int64, C.c_int32, C.c_double, C.c_double,
+                                                    C.c_double, C.c_double, C.c_int32, vp, vp, dp, C.c_int]
     L.se3icp_random_downsample.restype = C.c_int64
     L.se3icp_random_downsample.argtypes = [dp, C.c_int64, C.c_double, C.c_uint32, dp]
     L.se3icp_set_profiling.argtypes = [C.c_int, C.c_int]
     L.se3icp_last_kernel_times.argtypes = [C.c_int, dp]
     L.se3icp_set_trace.argtypes = [C.c_int, C.POINTER(Trace)]
     L.se3icp_set_lrf_exact.argtypes = [C.c_int, C.c_int]
+    L.se3icp_set_nn_events.argtypes = [C.c_int, C.c_int]
     _lib = L
     return L
 

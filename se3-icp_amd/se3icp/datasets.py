@@ -327,3 +327,35 @@ def synthetic_reference(cloud: np.ndarray, n_cases: int, ratio: float = 0.02, no
     _lib.check(int(min(r, 0)), "synthetic_reference")
     assert r == k
     return src, tgt, T
+
+
+def synthetic_reference_gpu(cloud: np.ndarray, n_cases: int, ratio: float = 0.02, noise_var: float = 0.005,
+                            t_range: float = 10.0, r_range: float = np.pi / 2, args_left_to_right: bool = False,
+                            device: int = 0, out=None):
+    """The reference's problems of synthetic_reference(), written by the GPU
+    (se3icp_synthetic_reference_device: the host draws the driver's streams, k_gen.hip
+    applies them with the same arithmetic), equal to synthetic_reference() bit for bit.
+    out=None: returns (src [C, k, 3], tgt [C, k, 3], T [C, 4, 4]) on the host;
+    out=(src_ptr, tgt_ptr): device buffers of [C * k, 3], returns (k, T)."""
+    import ctypes as C
+    from . import _lib
+    a = np.ascontiguousarray(cloud, dtype=np.float64)
+    k = int(ratio * a.shape[0])
+    T = np.zeros((n_cases, 4, 4))
+    dp = C.POINTER(C.c_double)
+    L = _lib.load()
+    flags = 1 if args_left_to_right else 0
+    if out is not None:
+        r = L.se3icp_synthetic_reference_device(device, a.ctypes.data_as(dp), a.shape[0], n_cases, ratio, noise_var,
+                                                t_range, r_range, flags, C.c_void_p(out[0]), C.c_void_p(out[1]),
+                                                T.ctypes.data_as(dp), 1)
+        _lib.check(int(min(r, 0)), "synthetic_reference_device")
+        return int(r), T
+    src = np.zeros((n_cases, k, 3))
+    tgt = np.zeros((n_cases, k, 3))
+    r = L.se3icp_synthetic_reference_device(device, a.ctypes.data_as(dp), a.shape[0], n_cases, ratio, noise_var,
+                                            t_range, r_range, flags, src.ctypes.data_as(C.c_void_p),
+                                            tgt.ctypes.data_as(C.c_void_p), T.ctypes.data_as(dp), 0)
+    _lib.check(int(min(r, 0)), "synthetic_reference_device")
+    assert r == k
+    return src, tgt, T

@@ -342,9 +342,17 @@ def nearest_neighbors(query, data, device: int = 0):
     return idx, d2, int(nr.value)
 
 
-def set_lrf_exact(on: bool, device: int = 0) -> None:
-    """Diagnostic: the exact one-query-per-wavefront kNN/TOLDI kernel for every point."""
-    _lib.check(_lib.load().se3icp_set_lrf_exact(device, 1 if on else 0))
+def set_lrf_exact(mode, device: int = 0) -> None:
+    """Diagnostic: which kernels compute the setup's kNN / TOLDI / normals.  0 / False: the
+    default (k_lrf8 + hand-overs); 1 / True: the exact one-query-per-wavefront kernel for every
+    point; 2: the global-buffer kernel (any k) for every point.  All bitwise equal."""
+    _lib.check(_lib.load().se3icp_set_lrf_exact(device, int(mode)))
+
+
+def set_nn_events(on: bool, device: int = 0) -> None:
+    """HIP events around the SE(3) NN grids of timed batches (default on; they fill
+    time_se3_correspondence_search_ms, and each leaves the GPU idle a few microseconds)."""
+    _lib.check(_lib.load().se3icp_set_nn_events(device, 1 if on else 0))
 
 
 def set_profiling(on: bool, device: int = 0) -> None:

@@ -5,13 +5,43 @@ drivers make one IterativeSE3Registration per pair, examples/benchmark_kitti.cpp
 so a batch of B pairs is split into contiguous blocks of B/G pairs per GPU and each rank
 registers its block with no data-path collective.  The only exchange is at the end: the
 max of the ranks' wall times (the job's time), the sum of their iteration counts and an
-all-gather of the per-pair poses (RCCL over xGMI on the GPU box; gloo in the CPU tests).
-The gathered poses are bitwise those of a single-rank run over the same pairs: no
-arithmetic crosses ranks.
+all-gather of every pair's result record — the pose, num_iterations_,
+num_pure_se3_iterations_ and the status, what the reference's drivers report per pair
+(examples/benchmark_kitti.cpp:163-197) — over RCCL/xGMI on the GPU box (gloo in the CPU
+tests).  The gathered records are bitwise those of a single-rank run over the same pairs:
+no arithmetic crosses ranks.
 """
 from __future__ import annotations
 
+from typing import NamedTuple
+
 import numpy as np
+
+REC = 19  # one pair's record: T (16, row-major), num_iterations, num_pure_se3_iterations, status
+
+
+class PairRecords(NamedTuple):
+    """The per-pair results of a whole (sharded) batch, in rank order."""
+    T: np.ndarray                        # [n, 4, 4]
+    num_iterations: np.ndarray           # [n] int
+    num_pure_se3_iterations: np.ndarray  # [n] int (-1 for run_icp)
+    status: np.ndarray                   # [n] int (se3icp_status)
+
+
+def pair_records(results) -> np.ndarray:
+    """[n, REC] float64 rows of se3icp results (objects with T, num_iterations,
+    num_pure_se3_iterations, status); the integers are exact in float64."""
+    rows = np.zeros((len(results), REC))
+    for i, r in enumerate(results):
+        rows[i, :16] = np.asarray(r.T, dtype=np.float64).reshape(16)
+        rows[i, 16:] = (r.num_iterations, r.num_pure_se3_iterations, r.status)
+    return rows
+
+
+def unpack_records(rows: np.ndarray) -> PairRecords:
+    rows = np.asarray(rows, dtype=np.float64).reshape(-1, REC)
+    i = rows[:, 16:].astype(np.int64)
+    return PairRecords(rows[:, :16].reshape(-1, 4, 4).copy(), i[:, 0], i[:, 1], i[:, 2])
 
 
 def shard(n_pairs_total: int, world: int, rank: int) -> tuple[int, int]:
@@ -25,34 +55,35 @@ def shard(n_pairs_total: int, world: int, rank: int) -> tuple[int, int]:
     return first, count
 
 
-def exchange_results(dist, device, elapsed_s: float, loop_s: float, iterations: int, poses: np.ndarray):
+def exchange_results(dist, device, elapsed_s: float, loop_s: float, iterations: int, records: np.ndarray):
     """Cross-rank reduction of one timed region.
 
-    Returns (elapsed_max, loop_max, iterations_sum, poses_all) where poses_all stacks every
-    rank's [n, 4, 4] poses in rank order.  `dist` is torch.distributed (or None for one
-    rank); `device` the tensor device of the backend (cuda for nccl/RCCL, cpu for gloo).
-    Ranks may hold different numbers of pairs (shard() of a batch that does not divide
-    evenly): the pair counts are gathered first and every rank's poses are padded to the
-    largest count for the fixed-size all-gather, then cut back.
+    records: the rank's [n, REC] pair_records().  Returns (elapsed_max, loop_max,
+    iterations_sum, PairRecords of every rank's pairs in rank order).  `dist` is
+    torch.distributed (or None for one rank); `device` the tensor device of the backend
+    (cuda for nccl/RCCL, cpu for gloo).  Ranks may hold different numbers of pairs (shard()
+    of a batch that does not divide evenly): the pair counts are gathered first and every
+    rank's records are padded to the largest count for the fixed-size all-gather, then cut
+    back.
     """
     import torch
 
-    poses = np.ascontiguousarray(poses, dtype=np.float64).reshape(-1, 4, 4)
+    records = np.ascontiguousarray(records, dtype=np.float64).reshape(-1, REC)
     if dist is None:
-        return float(elapsed_s), float(loop_s), int(iterations), poses
+        return float(elapsed_s), float(loop_s), int(iterations), unpack_records(records)
     t_max = torch.tensor([float(elapsed_s), float(loop_s)], dtype=torch.float64, device=device)
     dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
     tot = torch.tensor([float(iterations)], dtype=torch.float64, device=device)
     dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     world = dist.get_world_size()
-    cnt = torch.tensor([poses.shape[0]], dtype=torch.int64, device=device)
+    cnt = torch.tensor([records.shape[0]], dtype=torch.int64, device=device)
     counts = [torch.empty_like(cnt) for _ in range(world)]
     dist.all_gather(counts, cnt)
     counts = [int(c.item()) for c in counts]
-    pad = np.zeros((max(counts), 4, 4))
-    pad[:poses.shape[0]] = poses
+    pad = np.zeros((max(counts), REC))
+    pad[:records.shape[0]] = records
     mine = torch.from_numpy(pad).to(device)
     gathered = [torch.empty_like(mine) for _ in range(world)]
     dist.all_gather(gathered, mine)
-    allp = np.concatenate([g.cpu().numpy()[:c] for g, c in zip(gathered, counts)])
-    return float(t_max[0]), float(t_max[1]), int(round(float(tot[0]))), allp
+    allr = np.concatenate([g.cpu().numpy()[:c] for g, c in zip(gathered, counts)])
+    return float(t_max[0]), float(t_max[1]), int(round(float(tot[0]))), unpack_records(allr)

@@ -48,6 +48,16 @@ def _rank_poses(rank, n):
     return np.stack([np.eye(4) * (1 + rank) + k for k in range(n)])
 
 
+class _Res:  # a se3icp result's per-pair fields
+    def __init__(self, T, it, pure, status):
+        self.T, self.num_iterations, self.num_pure_se3_iterations, self.status = T, it, pure, status
+
+
+def _rank_results(rank, n):
+    return [_Res(T, 10 * rank + k + 1, 3 * rank + k, -7 if (rank, k) == (1, 1) else 0)
+            for k, T in enumerate(_rank_poses(rank, n))]
+
+
 def _rank_main(rank, world, port, out_dir, total=None):
     import torch
     import torch.distributed as dist
@@ -55,12 +65,19 @@ def _rank_main(rank, world, port, out_dir, total=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     n = 3 if total is None else sharding.shard(total, world, rank)[1]
-    poses = _rank_poses(rank, n)
     res = sharding.exchange_results(dist, torch.device("cpu"), elapsed_s=1.0 + rank, loop_s=0.5 * (rank + 1),
-                                    iterations=10 * (rank + 1), poses=poses)
+                                    iterations=10 * (rank + 1), records=sharding.pair_records(_rank_results(rank, n)))
     dist.barrier()
     dist.destroy_process_group()
-    np.savez(os.path.join(out_dir, f"r{rank}.npz"), elapsed=res[0], loop=res[1], iters=res[2], poses=res[3])
+    g = res[3]
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), elapsed=res[0], loop=res[1], iters=res[2], poses=g.T,
+             num_iterations=g.num_iterations, pure=g.num_pure_se3_iterations, status=g.status)
+
+
+def _expected_records(world, counts):
+    rs = [r for rank in range(world) for r in _rank_results(rank, counts[rank])]
+    return (np.stack([r.T for r in rs]), np.array([r.num_iterations for r in rs]),
+            np.array([r.num_pure_se3_iterations for r in rs]), np.array([r.status for r in rs]))
 
 
 def test_exchange_results_gloo_world2(tmp_path):
@@ -69,20 +86,25 @@ def test_exchange_results_gloo_world2(tmp_path):
     world = 2
     mp.start_processes(_rank_main, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
-    expect = np.concatenate([np.stack([np.eye(4) * (1 + r) + k for k in range(3)]) for r in range(world)])
+    T, it, pure, st = _expected_records(world, [3, 3])
     for r in range(world):
         d = np.load(tmp_path / f"r{r}.npz")
         assert float(d["elapsed"]) == 2.0      # max over ranks
         assert float(d["loop"]) == 1.0
         assert int(d["iters"]) == 30           # sum over ranks
-        np.testing.assert_array_equal(d["poses"], expect)   # rank-ordered gather, bitwise
+        np.testing.assert_array_equal(d["poses"], T)   # rank-ordered gather, bitwise
+        np.testing.assert_array_equal(d["num_iterations"], it)
+        np.testing.assert_array_equal(d["pure"], pure)
+        np.testing.assert_array_equal(d["status"], st)
 
 
 def test_exchange_results_single_rank_is_identity():
-    poses = np.stack([np.eye(4)] * 2)
-    e, l, it, p = sharding.exchange_results(None, None, 1.5, 0.5, 7, poses)
+    res = _rank_results(1, 2)
+    e, l, it, g = sharding.exchange_results(None, None, 1.5, 0.5, 7, sharding.pair_records(res))
     assert (e, l, it) == (1.5, 0.5, 7)
-    np.testing.assert_array_equal(p, poses)
+    np.testing.assert_array_equal(g.T, np.stack([r.T for r in res]))
+    assert list(g.num_iterations) == [11, 12] and list(g.num_pure_se3_iterations) == [3, 4]
+    assert list(g.status) == [0, -7]
 
 
 def test_exchange_results_uneven_shards_gloo_world2(tmp_path):
@@ -93,8 +115,11 @@ def test_exchange_results_uneven_shards_gloo_world2(tmp_path):
     world, total = 2, 5
     mp.start_processes(_rank_main, args=(world, _free_port(), str(tmp_path), total), nprocs=world, join=True,
                        start_method="spawn")
-    expect = np.concatenate([_rank_poses(r, sharding.shard(total, world, r)[1]) for r in range(world)])
-    assert expect.shape[0] == total
+    T, it, pure, st = _expected_records(world, [sharding.shard(total, world, r)[1] for r in range(world)])
+    assert T.shape[0] == total
     for r in range(world):
         d = np.load(tmp_path / f"r{r}.npz")
-        np.testing.assert_array_equal(d["poses"], expect)
+        np.testing.assert_array_equal(d["poses"], T)
+        np.testing.assert_array_equal(d["num_iterations"], it)
+        np.testing.assert_array_equal(d["pure"], pure)
+        np.testing.assert_array_equal(d["status"], st)

@@ -1,5 +1,10 @@
 """The synthetic benchmark generator (examples/benchmark_synthetic.cpp:91-160) on the GPU
-(k_gen.hip, se3icp_synthetic_pairs).
+(k_gen.hip): se3icp_synthetic_reference_device, the reference's own problems bit for bit,
+and se3icp_synthetic_pairs, the same protocol on counter-based streams.
+
+The reference-exact batch is checked against the host restatement
+se3icp_synthetic_reference, itself pinned by the reference's fixture and its streams
+(tests/test_reference_streams.py).
 
 The GPU generator uses counter-based Philox streams and a keyed permutation, so its
 samples differ from the reference's mt19937 / std::normal_distribution / Open3D shuffle
@@ -14,6 +19,39 @@ import pytest
 from scipy.spatial import cKDTree
 
 from se3icp import datasets
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("setup", ["moderate", "easy"])
+@pytest.mark.parametrize("ratio", [0.02, 0.2])
+def test_reference_exact_batch_on_device_equals_host(bunny_full, setup, ratio):
+    """B_SYN:91-160 for 8 cases with the driver's streams: the device clouds (gathered,
+    Transform-ed without FMA, noise added on the GPU) equal the host generator's bit for
+    bit, for the active "moderate" ranges (B_SYN:111-112) and the "easy" ones (:106-108)."""
+    tr, rr = (10.0, np.pi / 2) if setup == "moderate" else (5.0, np.pi / 4)
+    cloud = bunny_full * 50.0
+    hs, ht, hT = datasets.synthetic_reference(cloud, 8, ratio=ratio, t_range=tr, r_range=rr)
+    ds, dt, dT = datasets.synthetic_reference_gpu(cloud, 8, ratio=ratio, t_range=tr, r_range=rr)
+    assert ds.shape == hs.shape == (8, int(ratio * cloud.shape[0]), 3)
+    assert np.array_equal(dT, hT)
+    assert np.array_equal(ds.view(np.uint64), hs.view(np.uint64))
+    assert np.array_equal(dt.view(np.uint64), ht.view(np.uint64))
+
+
+@pytest.mark.gpu
+def test_reference_exact_batch_device_buffers(bunny_full):
+    """The device-resident output (ready for se3icp_register_batch_device) is the same."""
+    import torch
+    cloud = bunny_full * 50.0
+    k = int(0.02 * cloud.shape[0])
+    d_src = torch.empty((8 * k, 3), dtype=torch.float64, device="cuda")
+    d_tgt = torch.empty_like(d_src)
+    kk, T = datasets.synthetic_reference_gpu(cloud, 8, out=(d_src.data_ptr(), d_tgt.data_ptr()))
+    torch.cuda.synchronize()
+    hs, ht, hT = datasets.synthetic_reference(cloud, 8)
+    assert kk == k and np.array_equal(T, hT)
+    assert np.array_equal(d_src.cpu().numpy().reshape(8, k, 3), hs)
+    assert np.array_equal(d_tgt.cpu().numpy().reshape(8, k, 3), ht)
 
 
 def test_synthetic_cases_ranges_and_determinism():

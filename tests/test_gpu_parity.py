@@ -531,3 +531,29 @@ def test_degenerate_clouds_knn_and_frames(se3icp_mod, refcpu, kind):
         registration.set_lrf_exact(False)
     assert np.array_equal(fast_f.view(np.uint64), ex_f.view(np.uint64))
     assert np.array_equal(fast_n.view(np.uint64), ex_n.view(np.uint64))
+
+
+def test_lrf_fast_path_equals_exact_kernel_in_a_batch(se3icp_mod):
+    """In a multi-cloud batch k_lrf8's waves are aligned per cloud (the wave -> position
+    table) and each cloud's last, partial, wave is handed over whole to the exact kernel.
+    A batch of pairs whose cloud sizes are not multiples of 8 registers to bitwise the same
+    poses and iteration counts with the fast path as with the exact kernel for every point."""
+    from se3icp import datasets, registration
+    pairs, _ = datasets.kitti_like_pairs(3, seed=4, n_az=300)
+    rng = np.random.default_rng(5)
+    cut = []
+    for s, t in pairs:  # sizes = 1..7 (mod 8)
+        ns = len(s) - (len(s) % 8) - int(rng.integers(1, 8))
+        nt = len(t) - (len(t) % 8) - int(rng.integers(1, 8))
+        cut.append((s[:ns], t[:nt]))
+    assert all(len(s) % 8 and len(t) % 8 for s, t in cut)
+    p = se3icp_mod.kitti_params()
+    fast = se3icp_mod.register_batch(cut, "se3_gicp", p)
+    registration.set_lrf_exact(1)
+    try:
+        exact = se3icp_mod.register_batch(cut, "se3_gicp", p)
+    finally:
+        registration.set_lrf_exact(0)
+    for i, (a, b) in enumerate(zip(fast, exact)):
+        assert np.array_equal(a.T, b.T), (i, a.T - b.T)
+        assert (a.num_iterations, a.num_pure_se3_iterations) == (b.num_iterations, b.num_pure_se3_iterations)
