@@ -129,8 +129,8 @@ Engine::~Engine() {
                      &d_rechecked_, &d_keys0_, &d_vals1_, &d_sort_tmp_, &d_stats_,
                      &d_qlist_, &d_qcount_, &d_chunk_cost_, &d_chunk_order_, &d_hist_, &d_cert_, &d_sqlist_, &d_state_, &d_trim_cand_, &d_trim_ctr_, &d_scales_, &d_trim_hist_,
                      &d_lrf_fb_, &d_lrf_fbn_, &d_big_d_, &d_big_i_,
-                     &t3_.perm, &t3_.pos, &t3_.vec, &t3_.blo, &t3_.bhi, &t3_.lo, &t3_.hi,
-                     &t12_.perm, &t12_.pos, &t12_.vec, &t12_.blo, &t12_.bhi, &t12_.lo, &t12_.hi};
+                     &t3_.perm, &t3_.pos, &t3_.vec, &t3_.vec64, &t3_.vec64a, &t3_.blo, &t3_.bhi, &t3_.lo, &t3_.hi,
+                     &t12_.perm, &t12_.pos, &t12_.vec, &t12_.vec64, &t12_.blo, &t12_.bhi, &t12_.lo, &t12_.hi};
     for (DevBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     if (h_pairs_) (void)hipHostFree(h_pairs_);
@@ -230,6 +230,7 @@ View Engine::view() const {
         r.pos = (const int32_t*)t.pos.p;
         r.tvec = (const float*)t.vec.p;
         r.tvec64 = (const double*)t.vec64.p;
+        r.tpt64 = (const double4*)t.vec64a.p;
         r.lo = (const float*)t.lo.p;
         r.hi = (const float*)t.hi.p;
         return r;
@@ -255,7 +256,8 @@ int Engine::build_tree(int D, const float* vec, hipStream_t s, const double* vec
     const int nnodes = 2 << tb.L;
     const size_t nb = (size_t)nclouds_ * nnodes * D;
     if (!ensure<uint32_t>(tb.blo, nb) || !ensure<uint32_t>(tb.bhi, nb) || !ensure<float>(tb.lo, nb) ||
-        !ensure<float>(tb.hi, nb) || (vec64 && !ensure<double>(tb.vec64, (size_t)D * ld_)))
+        !ensure<float>(tb.hi, nb) || (vec64 && !ensure<double>(tb.vec64, (size_t)D * ld_)) ||
+        (vec64 && D == 3 && !ensure<double4>(tb.vec64a, (size_t)ld_)))
         return SE3ICP_ERR_OUT_OF_MEMORY;
     std::vector<int32_t> host_n(nclouds_);
     int max_n = 0;
@@ -278,6 +280,7 @@ int Engine::build_tree(int D, const float* vec, hipStream_t s, const double* vec
     t.tvec = (float*)tb.vec.p;
     t.vec64 = vec64;
     t.tvec64 = vec64 ? (double*)tb.vec64.p : nullptr;
+    t.tpt64 = (vec64 && D == 3) ? (double4*)tb.vec64a.p : nullptr;
     t.vec64_sources_only = D == 12;  // the loop reads f64 12-D vectors of source clouds (even ids) only
     t.blo = (uint32_t*)tb.blo.p;
     t.bhi = (uint32_t*)tb.bhi.p;

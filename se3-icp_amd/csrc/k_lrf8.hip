@@ -43,34 +43,15 @@ namespace {
 
 using namespace knn;
 
-#ifndef SE3ICP_LRF8_KW
-#define SE3ICP_LRF8_KW 4
-#endif
-constexpr int kW = SE3ICP_LRF8_KW;  // waves per block
-constexpr int kQ = 8;          // queries per wave (eight lanes each in the group phases)
-#ifndef SE3ICP_LRF8_CAP
-#define SE3ICP_LRF8_CAP 192
-#endif
-constexpr int kCap = SE3ICP_LRF8_CAP;  // candidates buffered per query (u32: cut key | candidate id), <= 256
-#ifndef SE3ICP_LRF8_SELECT
-#define SE3ICP_LRF8_SELECT 0  // bound of a tightening: 0 sorts; 1 (lists over 128) / 2 (always) a counting select (A/B: +11 % / +10 % k_lrf8)
-#endif
-#ifndef SE3ICP_LRF8_MERGE
-#define SE3ICP_LRF8_MERGE 1  // tightenings keep the list sorted: sort only the tail appended since, merge (0: sort the whole list each time)
-#endif
-#ifndef SE3ICP_LRF8_FINAL32
-#define SE3ICP_LRF8_FINAL32 1  // final rank order: u32 entry sort + odd-even fix-up of the full keys (0: a 64-bit network)
-#endif
-#ifndef SE3ICP_LRF8_F32SCAN
-#define SE3ICP_LRF8_F32SCAN 1  // leaf scans on the f32 coordinates (packed, two queries per instruction), bounds widened by the f32 error; 0: f64 distances
-#endif
-#ifndef SE3ICP_LRF8_LEAF_BITS
-#define SE3ICP_LRF8_LEAF_BITS 6
-#endif
-constexpr int kLeaves = 1 << SE3ICP_LRF8_LEAF_BITS;  // leaves one wave may scan: candidate id = (list index << 6) | lane
-constexpr unsigned kIdBits = (1u << (SE3ICP_LRF8_LEAF_BITS + 6)) - 1u;  // low bits of a list entry: the candidate id
-constexpr unsigned kAll = 0xfffffffeu;   // bound of the accept-all phase (> every finite key)
-constexpr unsigned kPad = 0xffffffffu;   // sort padding (> every bound)
+constexpr int kW = 4;     // waves per block
+constexpr int kQ = 8;     // queries per wave (eight lanes each in the group phases)
+constexpr int kCap = 192; // candidates buffered per query (u32: cut key | candidate id)
+constexpr int kLeaves = 64;              // leaves one wave may scan: candidate id = (list index << 6) | lane
+constexpr unsigned kIdBits = 0xfffu;     // low bits of a list entry: the candidate id
+// bound of the accept-all phase: every finite key (a lane past the leaf's end carries an
+// infinite distance, so its entry is above every bound)
+constexpr unsigned kAll = 0x7f7fffffu;
+constexpr unsigned kPad = 0xffffffffu;   // sort padding (> every entry)
 
 // park slots per query (doubles)
 enum Park8 {
@@ -79,7 +60,6 @@ enum Park8 {
     P8_W = 30,                // the query's tree slot
     P8_N = 31
 };
-constexpr int kSums8 = 21;
 constexpr int kParkAt = 128;  // list entry where the park starts (8-byte aligned)
 static_assert(kCap >= kParkAt + 2 * P8_N, "the park overlays the list tail");
 
@@ -161,34 +141,6 @@ __device__ __forceinline__ void sort8(unsigned (&k)[PER], int l) {
     net8<PER, 8 * PER>(k, l);
 }
 
-// key of rank r (group-uniform, 0 <= r) of a sorted group; kPad beyond the network
-template <int PER>
-__device__ __forceinline__ unsigned rank_key(const unsigned (&k)[PER], int l, int r) {
-    r = __builtin_amdgcn_readfirstlane(r);  // wave-uniform: one indexed register move (v_movrels)
-    if (r >= 8 * PER) return kPad;
-    unsigned x = k[r % PER];
-    x = (l == r / PER) ? x : 0u;
-    x |= gx(x, 1);
-    x |= gx(x, 2);
-    x |= gx(x, 4);
-    return x;
-}
-
-// Bound tightening of the group's query (eight lanes per query, all groups at once):
-// sort its list entries, bound = the Kw-th smallest cut key with every id bit set, keep the
-// entries at or below it in place (entries of equal cut key stay together: never fewer
-// than Kw).  Returns (bound, kept) for the group.
-template <int PER>
-__device__ __forceinline__ unsigned list_kth(const unsigned* list, int nbg, int l, int r) {
-    unsigned k[PER];
-#pragma unroll
-    for (int s = 0; s < PER; ++s) {
-        const int e = l * PER + s;
-        k[s] = e < nbg ? list[e] : kPad;
-    }
-    sort8<PER>(k, l);
-    return rank_key(k, l, r);
-}
 // sort the run list[0 .. len) (len <= 8 * PER) in place
 template <int PER = 16>
 __device__ __forceinline__ void sort_run(unsigned* list, int len, int l) {
@@ -215,15 +167,11 @@ __device__ __forceinline__ float f32_err3(float d, float S) {
 }
 // the list bound from the Kw-th smallest entry t (f32 keys): every point whose exact
 // distance is within the Kw-th smallest exact distance has an f32 key <= the value of t
-// plus two errors (SE3ICP_LRF8_F32SCAN; identity for f64 keys, whose order is exact)
+// plus two errors
 __device__ __forceinline__ unsigned widen_bound(unsigned t, float S) {
-#if SE3ICP_LRF8_F32SCAN
-    if (t >= 0x7f800000u) return t;
+    if (t >= 0x7f800000u) return kAll;
     const float b = __uint_as_float(t);
-    return (__float_as_uint(fmaf(2.02f, f32_err3(b, S), b)) + 2u) | kIdBits;
-#else
-    return t;
-#endif
+    return min((__float_as_uint(fmaf(2.02f, f32_err3(b, S), b)) + 2u) | kIdBits, kAll);
 }
 // number of entries <= t in the sorted run A[0 .. n)
 __device__ __forceinline__ int upper_count(const unsigned* A, int n, unsigned t) {
@@ -245,85 +193,6 @@ __device__ __forceinline__ unsigned kth_of_two(const unsigned* A, int na, const 
     const int j = r + 1 - lo;
     return max(lo > 0 ? A[lo - 1] : 0u, j > 0 ? B[j - 1] : 0u);
 }
-// The want-th smallest cut key (20-bit value, entries' top bits) of the group's list
-// without a sort: each lane counts its entries at or below a trial value, the group adds
-// the counts; the trial values interpolate between the bracket's counts, with a bisection
-// step whenever an interpolation did not halve the bracket.  Exact: returns the smallest
-// value v with count(<= v) >= want.
-__device__ __forceinline__ unsigned select_kth(const unsigned* list, int nbg, int l, int want) {
-    constexpr int PER = kCap / 8;
-    unsigned k[PER];
-    unsigned kmax = 0u, kmin = 0xfffffu;
-#pragma unroll
-    for (int s = 0; s < PER; ++s) {
-        const int e = l + 8 * s;
-        const bool v = e < nbg;
-        k[s] = v ? (list[e] >> 12) : 0xfffffu;
-        kmax = v ? max(kmax, k[s]) : kmax;
-        kmin = min(kmin, k[s]);
-    }
-    kmax = max(kmax, gx(kmax, 1)); kmax = max(kmax, gx(kmax, 2)); kmax = max(kmax, gx(kmax, 4));
-    kmin = min(kmin, gx(kmin, 1)); kmin = min(kmin, gx(kmin, 2)); kmin = min(kmin, gx(kmin, 4));
-    // count(<= lo) < want <= count(<= hi)
-    int lo = (int)kmin - 1, hi = (int)kmax, clo = 0, chi = nbg;
-    bool bis = false;
-    for (;;) {
-        const bool open = hi - lo > 1;
-        if (__ballot(open) == 0ull) break;
-        int mid;
-        if (bis) {
-            mid = (lo + hi) >> 1;
-        } else {
-            const float f = (float)(want - clo) * __builtin_amdgcn_rcpf((float)max(chi - clo, 1));
-            mid = lo + (int)((float)(hi - lo) * f);
-            mid = min(max(mid, lo + 1), hi - 1);
-        }
-        unsigned c = 0u;
-#pragma unroll
-        for (int s = 0; s < PER; ++s) c += (k[s] <= (unsigned)mid) ? 1u : 0u;
-        c += gx(c, 1);
-        c += gx(c, 2);
-        c += gx(c, 4);
-        if (open) {
-            const int width = hi - lo;
-            if ((int)c >= want) { hi = mid; chi = (int)c; }
-            else { lo = mid; clo = (int)c; }
-            bis = !bis && 2 * (hi - lo) > width;
-        }
-    }
-    return (unsigned)hi << 12;
-}
-
-__device__ __forceinline__ uint2 tighten_group(unsigned* lists, int g, int l, int nbg, int nmax, int Kw, float S) {
-    unsigned* list = lists + g * kCap;
-    unsigned tg;
-    if (SE3ICP_LRF8_SELECT >= 2 || (SE3ICP_LRF8_SELECT == 1 && nmax > 128)) {
-        tg = select_kth(list, nbg, l, Kw);
-    } else if (nmax <= 128) {
-        tg = list_kth<16>(list, nbg, l, Kw - 1);
-    } else {  // two sorted runs of <= 128 (a 256-entry network would need the kernel's registers)
-        const int na = min(nbg, 128), nb = max(nbg - 128, 0);
-        sort_run(list, na, l);
-        sort_run(list + 128, nb, l);
-        tg = kth_of_two(list, na, list + 128, nb, Kw - 1);
-    }
-    tg = widen_bound(tg | kIdBits, S);
-    // compaction in place (reads of a round precede its writes, positions only move down)
-    unsigned keep_n = 0;
-    for (int r0 = 0; r0 < nmax; r0 += 8) {
-        const int e = r0 + l;
-        const unsigned ent = e < nbg ? list[e] : kPad;
-        const bool keep = ent <= tg;
-        const unsigned long long m = __ballot(keep);
-        const unsigned gm = (unsigned)(m >> (8 * g)) & 0xffu;
-        __builtin_amdgcn_wave_barrier();
-        if (keep) list[(int)keep_n + __popc(gm & ((1u << l) - 1u))] = ent;
-        keep_n += (unsigned)__popc(gm);
-        __builtin_amdgcn_wave_barrier();
-    }
-    return make_uint2(tg, keep_n);
-}
-
 // Bound tightening over a list whose first mv entries are already sorted (the kept set of
 // the previous tightening): only the tail appended since is sorted, the Kw-th entry is
 // found by a merge-path search of the two runs, and the kept parts of both runs are merged
@@ -345,7 +214,7 @@ __device__ __forceinline__ uint3 tighten_group_sorted(unsigned* lists, int g, in
     unsigned* B = list + mv;
     if (tail_per == 8) sort_run<8>(B, nb, l);
     else if (tail_per == 16) sort_run<16>(B, nb, l);
-    const unsigned tg = nbg >= Kw ? widen_bound(kth_of_two(list, mv, B, nb, Kw - 1) | kIdBits, S) : kPad;
+    const unsigned tg = nbg >= Kw ? widen_bound(kth_of_two(list, mv, B, nb, Kw - 1) | kIdBits, S) : kAll;
     const int ka = upper_count(list, mv, tg), kb = upper_count(B, nb, tg);
     const int kept = ka + kb;
     if (__ballot(kept > 128) == 0ull) {
@@ -387,100 +256,29 @@ __device__ __forceinline__ uint3 tighten_group_sorted(unsigned* lists, int g, in
     return make_uint3(tg, keep_n, 0u);
 }
 
-// point of a list entry: the wave's leaf list holds leaf indices, the id (list index << 6 |
-// lane) picks the point
-__device__ __forceinline__ int entry_slot(unsigned ent, const int* leaves, int off, int n, int L) {
-    const unsigned id = ent & kIdBits;
-    return off + tree_first(n, L, leaves[id >> 6]) + (int)(id & 63u);
+// the f64 point of tree slot i from its (x, y, z, 0) record: one 16-B and one 8-B load of
+// one cache line (the unused fourth word is not loaded)
+struct p3 { double x, y, z; };
+__device__ __forceinline__ p3 ld3(const double4* __restrict__ P4, int i) {
+    const double2 xy = *reinterpret_cast<const double2*>(P4 + i);
+    const double z = reinterpret_cast<const double*>(P4 + i)[2];
+    return p3{xy.x, xy.y, z};
 }
 
-// 64-bit version of the group network (keys (full key << 32) | point index: the order of
-// the final lists, canonical — independent of the tree and of the batch around the cloud)
-__device__ __forceinline__ unsigned long long gx64(unsigned long long x, int m) {
-    const unsigned lo = gx((unsigned)x, m), hi = gx((unsigned)(x >> 32), m);
-    return ((unsigned long long)hi << 32) | lo;
-}
-template <int PER, int KK, int JD>
-__device__ __forceinline__ void stage8_64(unsigned long long (&k)[PER], int l) {
-    if constexpr (JD == 0) {
-        if constexpr (KK <= PER) {
-#pragma unroll
-            for (int s = 0; s < PER; ++s) {
-                const int t = s ^ (KK - 1);
-                if (s < t) {
-                    const unsigned long long a = k[s], b = k[t];
-                    const bool sw = b < a;
-                    k[s] = sw ? b : a;
-                    k[t] = sw ? a : b;
-                }
-            }
-        } else {
-            constexpr int lm = KK / PER - 1;
-            const bool lower = (l & (KK / PER / 2)) == 0;
-#pragma unroll
-            for (int s = 0; s < PER / 2; ++s) {
-                const int t = PER - 1 - s;
-                const unsigned long long a = gx64(k[t], lm), b = gx64(k[s], lm);
-                k[s] = ((a < k[s]) == lower) ? a : k[s];
-                k[t] = ((b < k[t]) == lower) ? b : k[t];
-            }
-        }
-    } else if constexpr (JD < PER) {
-#pragma unroll
-        for (int s = 0; s < PER; ++s) {
-            if ((s & JD) == 0) {
-                const int t = s | JD;
-                const unsigned long long a = k[s], b = k[t];
-                const bool sw = b < a;
-                k[s] = sw ? b : a;
-                k[t] = sw ? a : b;
-            }
-        }
-    } else {
-        constexpr int lm = JD / PER;
-        const bool lower = (l & lm) == 0;
-#pragma unroll
-        for (int s = 0; s < PER; ++s) {
-            const unsigned long long p = gx64(k[s], lm);
-            k[s] = ((p < k[s]) == lower) ? p : k[s];
-        }
-    }
-}
-template <int PER, int N, int KK = 2, int JD = 0>
-__device__ __forceinline__ void net8_64(unsigned long long (&k)[PER], int l) {
-    stage8_64<PER, KK, JD>(k, l);
-    constexpr int next_jd = JD == 0 ? KK / 4 : JD / 2;
-    if constexpr (next_jd > 0) net8_64<PER, N, KK, next_jd>(k, l);
-    else if constexpr (KK < N) net8_64<PER, N, KK * 2, 0>(k, l);
-}
-// key part of the entry of rank r (wave-uniform) of a sorted group; kPad beyond it
-__device__ __forceinline__ unsigned rank_key64(const unsigned long long (&k)[16], int l, int r) {
-    r = __builtin_amdgcn_readfirstlane(r);
-    if (r >= 128) return kPad;
-    unsigned x = (unsigned)(k[r % 16] >> 32);
-    x = (l == r / 16) ? x : 0u;
-    x |= gx(x, 1);
-    x |= gx(x, 2);
-    x |= gx(x, 4);
-    return x;
-}
-
-// The final list of the group's query (nbg <= 128 entries): full keys recomputed from the
-// points (nanoflann arithmetic), sorted with the point index as tie-break, the rank-ordered
-// tree slots written back over the list; returns false when two of the ranks the sums use
-// share an f32 key but not the f64 distance (the query then goes to the exact kernel).
-__device__ __forceinline__ bool final_group(unsigned* lists, const int* leaves, const double* __restrict__ TX,
-                                            const double* __restrict__ TY, const double* __restrict__ TZ,
-                                            const int32_t* __restrict__ perm, const int32_t* __restrict__ pos,
-                                            double qx, double qy, double qz, int off, int n, int L, int g, int l,
-                                            int nbg, int kk, int kn, bool want_t, bool want_n) {
+// The final list of the group's query (nbg <= 128 entries) in rank order.  The list
+// entries (cut key | id) sorted as u32 give the rank order up to runs whose full keys the
+// cut does not separate; the full keys ((f32 of the exact f64 distance, nanoflann's
+// arithmetic) << 32 | tree slot) of that order are put right by three odd-even
+// transposition passes and checked, and the tree slots are written back over the list in
+// rank order.  Returns false (the query goes to the exact kernel) when the order is still
+// wrong, or when two of the ranks the sums use share an f32 key and either their f64
+// distances differ or their point indices are out of order (the exact order is (f64
+// distance, point index): the reference's kNN and the exact kernel's).
+__device__ __forceinline__ bool final_group(unsigned* lists, const int* leaf_slot, const double4* __restrict__ P4,
+                                            const int32_t* __restrict__ perm, double qx, double qy, double qz, int off,
+                                            int g, int l, int nbg, int lim) {
     unsigned* list = lists + g * kCap;
     unsigned long long k[16];
-#if SE3ICP_LRF8_FINAL32
-    // The list entries (cut key | id) sorted as u32 give the rank order up to runs whose
-    // full keys the cut does not separate; the (full key << 32 | point index) keys of that
-    // order are put right by three odd-even transposition passes, and the result is
-    // checked: a list still out of order goes to the exact kernel.
     bool unsorted = false;
     {
         unsigned k32[16];
@@ -495,9 +293,11 @@ __device__ __forceinline__ bool final_group(unsigned* lists, const int* leaves, 
             const int e = l * 16 + s;
             unsigned long long x = ~0ull;
             if (e < nbg) {
-                const int slot = entry_slot(k32[s], leaves, off, n, L);
-                const unsigned key = f32_up_bits(l2_3(qx, qy, qz, TX[slot], TY[slot], TZ[slot]));
-                x = ((unsigned long long)key << 32) | (unsigned)perm[slot];
+                const unsigned id = k32[s] & kIdBits;
+                const int slot = leaf_slot[id >> 6] + (int)(id & 63u);
+                const p3 p = ld3(P4, slot);
+                const unsigned key = __float_as_uint((float)l2_3(qx, qy, qz, p.x, p.y, p.z));
+                x = ((unsigned long long)key << 32) | (unsigned)(slot - off);
             }
             k[s] = x;
         }
@@ -508,80 +308,56 @@ __device__ __forceinline__ bool final_group(unsigned* lists, const int* leaves, 
         a = lo;
         b = hi;
     };
-    auto odd_pass = [&]() __attribute__((always_inline)) {
+    const int me = (int)(threadIdx.x & 63);
+    auto next_first = [&]() __attribute__((always_inline)) {  // lane l + 1's k[0] (within the group for l < 7)
+        return ((unsigned long long)(unsigned)__shfl((int)(unsigned)(k[0] >> 32), me + 1, 64) << 32) |
+               (unsigned)__shfl((int)(unsigned)k[0], me + 1, 64);
+    };
+#pragma unroll
+    for (int s = 0; s < 16; s += 2) ce(k[s], k[s + 1]);
+    {
 #pragma unroll
         for (int s = 1; s + 1 < 16; s += 2) ce(k[s], k[s + 1]);
         // (lane l's last, lane l+1's first) within the group of eight
-        const int me = (int)(threadIdx.x & 63);
-        const unsigned long long nx = ((unsigned long long)(unsigned)__shfl((int)(unsigned)(k[0] >> 32), me + 1, 64) << 32) |
-                                      (unsigned)__shfl((int)(unsigned)k[0], me + 1, 64);
+        const unsigned long long nx = next_first();
         const unsigned long long pv = ((unsigned long long)(unsigned)__shfl((int)(unsigned)(k[15] >> 32), me - 1, 64) << 32) |
                                       (unsigned)__shfl((int)(unsigned)k[15], me - 1, 64);
         if (l < 7 && nx < k[15]) k[15] = nx;
         if (l > 0 && k[0] < pv) k[0] = pv;
-    };
+    }
 #pragma unroll
     for (int s = 0; s < 16; s += 2) ce(k[s], k[s + 1]);
-    odd_pass();
+    const unsigned long long nx = next_first();
 #pragma unroll
-    for (int s = 0; s < 16; s += 2) ce(k[s], k[s + 1]);
-    {
-        const int me = (int)(threadIdx.x & 63);
-        const unsigned long long nx = ((unsigned long long)(unsigned)__shfl((int)(unsigned)(k[0] >> 32), me + 1, 64) << 32) |
-                                      (unsigned)__shfl((int)(unsigned)k[0], me + 1, 64);
-#pragma unroll
-        for (int s = 0; s + 1 < 16; ++s) unsorted |= k[s + 1] < k[s];
-        unsorted |= (l < 7) && nx < k[15];
-    }
-#else
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-        const int e = l * 16 + s;
-        unsigned long long x = ~0ull;
-        if (e < nbg) {
-            const int slot = entry_slot(list[e], leaves, off, n, L);
-            const unsigned key = f32_up_bits(l2_3(qx, qy, qz, TX[slot], TY[slot], TZ[slot]));
-            x = ((unsigned long long)key << 32) | (unsigned)perm[slot];
-        }
-        k[s] = x;
-    }
-    net8_64<16, 128>(k, l);
-#endif
-    // Two of the first lim = min(nbg, max(kk, kn) + 1) ranks sharing an f32 key must also
-    // share the f64 distance (then both orders fall back to the index): the (key, index)
-    // order is then the exact (f64 d, index) order of the reference's kNN and of the exact
-    // kernel, whose sums this kernel reproduces bit for bit.  Otherwise the query goes to
-    // the exact kernel.
-    const int lim = min(nbg, max(kk, kn) + 1);
-    unsigned tied = 0u;  // bit s: ranks l*16+s and l*16+s+1 share an f32 key
+    for (int s = 0; s + 1 < 16; ++s) unsorted |= k[s + 1] < k[s];
+    unsorted |= (l < 7) && nx < k[15];
+    // adjacent ranks among the first lim sharing an f32 key (bit s: ranks l*16+s, +1)
+    unsigned tied = 0u;
 #pragma unroll
     for (int s = 0; s + 1 < 16; ++s) {
         const int e = l * 16 + s;
         if ((int)(e + 1 < lim) & (int)((unsigned)(k[s] >> 32) == (unsigned)(k[s + 1] >> 32))) tied |= 1u << s;
     }
     {
-        // the next lane's first key (lane l + 1 of the group)
-        const unsigned first_next = __shfl((unsigned)(k[0] >> 32), (int)(threadIdx.x & 63) + 1, 64);
         const int e = l * 16 + 15;
-        if ((int)(l < 7) & (int)(e + 1 < lim) & (int)((unsigned)(k[15] >> 32) == first_next)) tied |= 1u << 15;
+        if ((int)(l < 7) & (int)(e + 1 < lim) & (int)((unsigned)(k[15] >> 32) == (unsigned)(nx >> 32))) tied |= 1u << 15;
     }
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
         const int e = l * 16 + s;
-        if (e < nbg) list[e] = (unsigned)(off + pos[off + (int)(unsigned)k[s]]);
+        if (e < nbg) list[e] = (unsigned)off + (unsigned)k[s];
     }
     __builtin_amdgcn_wave_barrier();
-    bool bad = false;
+    bool bad = unsorted;
     while (tied) {  // rare: the tree slots of the tied ranks, now in rank order in the list
         const int e = l * 16 + __builtin_ctz(tied);
         tied &= tied - 1u;
         const int a = (int)list[e], b = (int)list[e + 1];
-        bad |= l2_3(qx, qy, qz, TX[a], TY[a], TZ[a]) != l2_3(qx, qy, qz, TX[b], TY[b], TZ[b]);
+        const p3 pa = ld3(P4, a), pb = ld3(P4, b);
+        bad |= l2_3(qx, qy, qz, pa.x, pa.y, pa.z) != l2_3(qx, qy, qz, pb.x, pb.y, pb.z);
+        bad |= perm[a] > perm[b];
     }
-#if SE3ICP_LRF8_FINAL32
-    bad |= unsorted;
-#endif
     const bool ok = !(bool)(unsigned)((__ballot(bad) >> (8 * g)) & 0xffull);
     return ok;
 }
@@ -595,34 +371,26 @@ __device__ __forceinline__ bool final_group(unsigned* lists, const int* leaves, 
 #define PROF8_ADD(acc, a, b) do {} while (0)
 #endif
 
-#ifndef SE3ICP_LRF8_EPI_WAVE
-#define SE3ICP_LRF8_EPI_WAVE 0  // eigen-solves and frames per wave (0: per block of kW waves)
-#endif
-static_assert(SE3ICP_LRF8_EPI_WAVE || (kW >= 2 && kW * kQ <= 64), "the per-block epilogue: waves 0 and 1, a lane per query");
-#ifndef SE3ICP_LRF8_WPE
-#define SE3ICP_LRF8_WPE 6  // waves per SIMD: 6 = the LDS limit (26.6 KB per block); A/B 4 -> 5 -> 6: 6.73 -> 6.45 -> 6.38 ms
-#endif
+static_assert(kW >= 2 && kW * kQ <= 64, "the per-block epilogue: waves 0 and 1, a lane per query");
 
-__global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF8_WPE))) void k_lrf8(
+// waves per SIMD: 6 = the LDS limit (26.6 KB per block); A/B 4 -> 5 -> 6: 6.73 -> 6.45 -> 6.38 ms
+__global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(6))) void k_lrf8(
     View v, const int32_t* __restrict__ cloud_of, const CloudSetup* __restrict__ setup,
     const CloudDev* __restrict__ clouds, const float* __restrict__ tlo, const float* __restrict__ thi,
-    const double* __restrict__ tx64, const int32_t* __restrict__ wave_base, int w_lo, int nwaves,
+    const double4* __restrict__ P4, const int32_t* __restrict__ wave_base, int w_lo, int nwaves,
     int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_count) {
     // (a query's park overlays the tail of its list, free once the list is final: <= 128 entries)
     __shared__ __attribute__((aligned(16))) unsigned s_list[kW][kQ][kCap];
     auto park_of = [&](int w, int j) __attribute__((always_inline)) {
         return reinterpret_cast<double*>(&s_list[w][j][kParkAt]);
     };
-    __shared__ int s_leaf[kW][kLeaves];
-    __shared__ double s_q[kW][kQ][4];  // the queries' f64 coordinates (read back per leaf: no registers held)
+    __shared__ int s_leaf[kW][kLeaves];  // first tree slot of each scanned leaf
+    __shared__ __attribute__((aligned(16))) float s_q[kW][3 * kQ];  // the queries' f32 x[8] y[8] z[8]
     // (wid through readfirstlane: the wave's LDS bases become scalar, not per-lane registers)
     const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = lane >> 3, l = lane & 7;  // query of the lane's group, lane within the group
     const int bid = xcd_block(blockIdx.x, gridDim.x);
     const TreeRef T = v.t3;
-    const double* TX = tx64;
-    const double* TY = tx64 + v.ld;
-    const double* TZ = tx64 + 2 * (size_t)v.ld;
     const int first_leaf = (1 << T.L) - 1;
     unsigned* lists = &s_list[wid][0][0];
     int* leaves = s_leaf[wid];
@@ -664,32 +432,34 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
         }
     }
     bool fb_wave = mode == 2;
-    // per-query state: bound (wave-uniform arrays) and list lengths
+    // per-query state: bound (wave-uniform arrays) and list lengths; the length of the lane's
+    // own group is picked from them only where the group phases need it (group_len)
     unsigned Tq[kQ], nbq[kQ];
 #pragma unroll
     for (int j = 0; j < kQ; ++j) { Tq[j] = kAll; nbq[j] = 0u; }
-    // the list length of the lane's own group g, kept alongside (picking nbq[g] at run time
-    // would turn the register arrays into scratch memory)
-    unsigned nbv = 0u;
-    int mvv = 0;  // (SE3ICP_LRF8_MERGE) sorted prefix of the group's list
-    double* qv = &s_q[wid][0][0];
+    auto group_len = [&]() __attribute__((always_inline)) {
+        unsigned x = nbq[0];
+#pragma unroll
+        for (int j = 1; j < kQ; ++j) x = (g == j) ? nbq[j] : x;
+        return x;
+    };
+    int mvv = 0;  // sorted prefix of the group's list
+    float* qv = s_q[wid];
     float fqlo[3] = {0.f, 0.f, 0.f}, fqhi[3] = {0.f, 0.f, 0.f};
     int nlist = 0;
     const int n = cl.n;
-    float s_norm = 0.f;  // (f32 scans) bound on |q| + |p| over the cloud, from its root box
+    float s_norm = 0.f;  // bound on |q| + |p| over the cloud, from its root box (f32 scan error)
     if (mode == 1) {
         // f32 box of the eight queries (the node boxes' frame)
         const float fx = lane < kQ ? T.tvec[w0 + lane] : 0.f;
         const float fy = lane < kQ ? T.tvec[v.ld + w0 + lane] : 0.f;
         const float fz = lane < kQ ? T.tvec[2 * (size_t)v.ld + w0 + lane] : 0.f;
-#if SE3ICP_LRF8_F32SCAN
-        {  // the queries' f32 coordinates, x[8] y[8] z[8] (over the f64 query slots)
-            float* qf = reinterpret_cast<float*>(qv);
-            if (lane < kQ) {
-                qf[lane] = fx;
-                qf[kQ + lane] = fy;
-                qf[2 * kQ + lane] = fz;
-            }
+        if (lane < kQ) {
+            qv[lane] = fx;
+            qv[kQ + lane] = fy;
+            qv[2 * kQ + lane] = fz;
+        }
+        {
             const float* rlo = tlo + (size_t)c * T.nnodes * 3;
             const float* rhi = thi + (size_t)c * T.nnodes * 3;
             float r2 = 0.f;
@@ -697,13 +467,6 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
             for (int a = 0; a < 3; ++a) r2 += fmaxf(rlo[a] * rlo[a], rhi[a] * rhi[a]);
             s_norm = 2.f * sqrtf(r2) * 1.0001f;
         }
-#else
-        if (lane < kQ) {
-            qv[4 * lane] = TX[w0 + lane];
-            qv[4 * lane + 1] = TY[w0 + lane];
-            qv[4 * lane + 2] = TZ[w0 + lane];
-        }
-#endif
         __builtin_amdgcn_wave_barrier();
         fqlo[0] = fqhi[0] = __shfl(fx, 0, 64);
         fqlo[1] = fqhi[1] = __shfl(fy, 0, 64);
@@ -725,7 +488,6 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
 #pragma unroll
         for (int j = 0; j < kQ; ++j) nmax = max(nmax, nbq[j]);
         __builtin_amdgcn_wave_barrier();
-#if SE3ICP_LRF8_MERGE
         int dmax = 0;
         bool anyz = false;
 #pragma unroll
@@ -736,45 +498,42 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
         }
         const bool presort = anyz || dmax > 128;
         const int tail_per = presort ? (nmax <= 128 ? 0 : 8) : (dmax == 0 ? 0 : dmax <= 64 ? 8 : 16);
-        const uint3 r3 = tighten_group_sorted(lists, g, l, (int)nbv, mvv, (int)nmax, Kw, presort, tail_per, s_norm);
-        const uint2 r = make_uint2(r3.x, r3.y);
+        const uint3 r3 = tighten_group_sorted(lists, g, l, (int)group_len(), mvv, (int)nmax, Kw, presort, tail_per, s_norm);
         mvv = (int)r3.z;
-#else
-        const uint2 r = tighten_group(lists, g, l, (int)nbv, (int)nmax, Kw, s_norm);
-#endif
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int j = 0; j < kQ; ++j) {
-            Tq[j] = (unsigned)__builtin_amdgcn_readlane((int)r.x, 8 * j);
-            nbq[j] = (unsigned)__builtin_amdgcn_readlane((int)r.y, 8 * j);
+            Tq[j] = (unsigned)__builtin_amdgcn_readlane((int)r3.x, 8 * j);
+            nbq[j] = (unsigned)__builtin_amdgcn_readlane((int)r3.y, 8 * j);
         }
-        nbv = r.y;
     };
 
     // ---------------------------------------------------------------- leaf scan
     // Each lane holds one point of leaf i; query j appends it when its entry (cut key |
     // id) <= Tq[j].  part: 0 the whole leaf, 1 / 2 its first / second 32 points (a leaf that
-    // does not fit a list even after a tightening is appended in two halves).
+    // does not fit a list even after a tightening is appended in two halves).  Lanes past
+    // the part carry an infinite distance: their entries exceed every bound.
     auto scan_leaf = [&](int i, int part) __attribute__((always_inline)) -> bool {
         if (nlist >= kLeaves) { fb_wave = true; PROF8_FB(0); return true; }
         const int li = nlist++;
         ++n_leaves;
-        if (lane == 0) leaves[li] = i;
         const int a = __builtin_amdgcn_readfirstlane(tree_first(n, T.L, i));
         const int b = __builtin_amdgcn_readfirstlane(tree_first(n, T.L, i + 1));
+        if (lane == 0) leaves[li] = cl.off + a;
         const bool valid = (bool)((int)(lane < b - a) & (int)(part == 0 || (part == 1) == (lane < 32)));
         const int slot = cl.off + a + (valid ? lane : 0);
         const unsigned id = (unsigned)((li << 6) | lane);
         unsigned ent[kQ];
         unsigned long long m[kQ];
         bool over = false;
-#if SE3ICP_LRF8_F32SCAN
         // the list key: the f32 squared distance of the f32 points (two queries per packed
         // instruction); the bounds carry its error (widen_bound), the final order uses exact keys
         float dq[kQ];
         {
             typedef float f2 __attribute__((ext_vector_type(2)));
-            const float px = T.tvec[slot], py = T.tvec[v.ld + slot], pz = T.tvec[2 * (size_t)v.ld + slot];
+            const float px = valid ? T.tvec[slot] : INFINITY;
+            const float py = valid ? T.tvec[v.ld + slot] : INFINITY;
+            const float pz = valid ? T.tvec[2 * (size_t)v.ld + slot] : INFINITY;
             const f2* qf2 = reinterpret_cast<const f2*>(qv);
             const f2 pxx = f2{px, px}, pyy = f2{py, py}, pzz = f2{pz, pz};
             // a - b as one v_pk_add_f32 (the compiler splits a broadcast operand into two v_sub_f32)
@@ -793,19 +552,9 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
                 dq[2 * jp + 1] = s2.y;
             }
         }
-#else
-        const double px = TX[slot], py = TY[slot], pz = TZ[slot];
-#endif
 #pragma unroll
         for (int j = 0; j < kQ; ++j) {
-#if SE3ICP_LRF8_F32SCAN
-            ent[j] = valid ? ((__float_as_uint(dq[j]) & ~kIdBits) | id) : kPad;
-#else
-            // the list key: the f32 bits of the rounded-to-nearest distance plus one ulp (>= the
-            // distance: an upper bound, all that the bounds need; the final order uses exact keys)
-            const double d = l2_3(qv[4 * j], qv[4 * j + 1], qv[4 * j + 2], px, py, pz);
-            ent[j] = valid ? (((__float_as_uint((float)d) + 1u) & ~kIdBits) | id) : kPad;
-#endif
+            ent[j] = (__float_as_uint(dq[j]) & ~kIdBits) | id;
             m[j] = __ballot(ent[j] <= Tq[j]);
             over |= nbq[j] + (unsigned)__popcll(m[j]) > (unsigned)kCap;
         }
@@ -820,9 +569,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
                 const int at = (int)nbq[j] + __builtin_amdgcn_mbcnt_hi((unsigned)(m[j] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m[j], 0u));
                 lists[j * kCap + at] = ent[j];
             }
-            const unsigned cnt = (unsigned)__popcll(m[j]);
-            nbq[j] += cnt;
-            nbv += (g == j) ? cnt : 0u;
+            nbq[j] += (unsigned)__popcll(m[j]);
         }
         __builtin_amdgcn_wave_barrier();
         return true;
@@ -964,21 +711,22 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
     PROF8_NOW(t_a1);
     PROF8_ADD(c_scan, t_a0, t_a1);
     // ---------------------------------------------------------------- final sets
-    // Each list sorted by full key (ties by point index); every set boundary must be strict
-    // (else the query goes to the exact kernel).
+    // Each list in rank order by exact key (ties by point index); every set boundary must
+    // be strict (else the query goes to the exact kernel).
     const int kl = st.k_lrf, kn_want = st.k_nrm;
     const bool want_t = kl > 0, want_n = kn_want > 0;
     bool fb_q = fb_wave;  // (group-uniform)
-    const int nbg = (int)nbv;
+    const int nbg = (int)group_len();
     const int nTop = min(Kw, nbg);
     const int kk = min(kl, nTop), kn = min(kn_want, nTop);
     const int wq = w0 + g;
     // the group's f64 query (final order, sums)
-    const double qg64x = mode == 1 ? TX[wq] : 0.0, qg64y = mode == 1 ? TY[wq] : 0.0, qg64z = mode == 1 ? TZ[wq] : 0.0;
+    p3 qg{0.0, 0.0, 0.0};
+    if (mode == 1) qg = ld3(P4, wq);
     if (mode == 1 && !fb_wave) {
         __builtin_amdgcn_wave_barrier();
-        const bool exact = final_group(lists, leaves, TX, TY, TZ, T.perm, T.pos, qg64x, qg64y, qg64z, cl.off, n, T.L,
-                                       g, l, nbg, kk, kn, want_t, want_n);
+        const bool exact = final_group(lists, leaves, P4, T.perm, qg.x, qg.y, qg.z, cl.off, g, l, nbg,
+                                       min(nbg, max(kk, kn) + 1));
         fb_q = (bool)((int)!exact | (int)(nTop < Kw));
         n_cand += (unsigned)nbg;
 #ifdef SE3ICP_PROF
@@ -994,64 +742,74 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
     const bool mine = (bool)((int)(mode == 1) & (int)!fb_q);
 
     // ---------------------------------------------------------------- per-query sums
-    // (group g, list entries l, l+8, ...; each classified by its full key; see k_knn.hip for
-    // the 21 sums and the TOLDI covariance about the quirk centroid, ISR.cpp:259-272)
+    // (group g, list entries l, l+8, ...; see k_knn.hip for the 21 sums and the TOLDI
+    // covariance about the quirk centroid, ISR.cpp:259-272).  The same loops, lane
+    // assignment and arithmetic as k_knn.hip's sums pass, over the same rank order, so the
+    // two kernels' frames agree bit for bit; the TOLDI and the normal sums are two passes
+    // (their live registers do not add up).
+    const unsigned* rl = lists + g * kCap;
+    double* pj = park_of(wid, g);
     {
-        double x[kSums8];
+        double x[12];
 #pragma unroll
-        for (int i = 0; i < kSums8; ++i) x[i] = 0.0;
+        for (int i = 0; i < 12; ++i) x[i] = 0.0;
         double Rf = 0.0;
-        #ifndef SE3ICP_LRF8_SKIP_SUMS  // (measurement build: the neighbour sums' share; wrong frames)
-        if (mine) {
-#else
-        if (false) {
-#endif
-            // the same loops, lane assignment and arithmetic as k_knn.hip's sums pass, over
-            // the same rank order: the two kernels' frames agree bit for bit
-            const double qgx = qg64x, qgy = qg64y, qgz = qg64z;
-            const unsigned* rl = lists + g * kCap;
-            if (want_t) {
-                const int rz = kk / 3;
-                const int hi = min(rz, kk - 1);
-                for (int rk = 1 + l; rk <= hi; rk += 8) {
-                    const int q = (int)rl[rk];
-                    const double vx = TX[q] - qgx, vy = TY[q] - qgy, vz = TZ[q] - qgz;
-                    if (rk < rz) { x[0] += vx; x[1] += vy; x[2] += vz; }
-                    x[3] += vx; x[4] += vy; x[5] += vz;
-                    x[6] += vx * vx; x[7] += vx * vy; x[8] += vx * vz;
-                    x[9] += vy * vy; x[10] += vy * vz; x[11] += vz * vz;
-                }
-                if (l == 0) {
-                    const int far = (int)rl[kk - 1];
-                    const double fdx = qgx - TX[far], fdy = qgy - TY[far], fdz = qgz - TZ[far];
-                    Rf = sqrt(fdx * fdx + fdy * fdy + fdz * fdz);  // ISR.cpp:256
-                }
+        if ((int)mine & (int)want_t) {
+            const int rz = kk / 3;
+            const int hi = min(rz, kk - 1);
+            for (int rk = 1 + l; rk <= hi; rk += 8) {
+                const p3 p = ld3(P4, (int)rl[rk]);
+                const double vx = p.x - qg.x, vy = p.y - qg.y, vz = p.z - qg.z;
+                if (rk < rz) { x[0] += vx; x[1] += vy; x[2] += vz; }
+                x[3] += vx; x[4] += vy; x[5] += vz;
+                x[6] += vx * vx; x[7] += vx * vy; x[8] += vx * vz;
+                x[9] += vy * vy; x[10] += vy * vz; x[11] += vz * vz;
             }
-            if (want_n) {  // EstimateNormals (ISR.cpp:643, :43): ranks 0 .. kn-1, self included
-                for (int r = l; r < kn; r += 8) {
-                    const int q = (int)rl[r];
-                    const double px = TX[q], py = TY[q], pz = TZ[q];
-                    x[12] += px; x[13] += py; x[14] += pz;
-                    x[15] += px * px; x[16] += px * py; x[17] += px * pz;
-                    x[18] += py * py; x[19] += py * pz; x[20] += pz * pz;
-                }
+            if (l == 0) {
+                const p3 f = ld3(P4, (int)rl[kk - 1]);
+                const double fdx = qg.x - f.x, fdy = qg.y - f.y, fdz = qg.z - f.z;
+                Rf = sqrt(fdx * fdx + fdy * fdy + fdz * fdz);  // ISR.cpp:256
             }
         }
 #pragma unroll
-        for (int i = 0; i < kSums8; ++i) {
+        for (int i = 0; i < 12; ++i) {
+            x[i] += gxd(x[i], 1);
+            x[i] += gxd(x[i], 2);
+            x[i] += gxd(x[i], 4);
+        }
+        __builtin_amdgcn_wave_barrier();
+        if ((int)(l == 0) & (int)mine) {
+#pragma unroll
+            for (int i = 0; i < 12; ++i) pj[P8_SUM + i] = x[i];
+            pj[P8_R] = Rf;
+        }
+    }
+    {
+        double x[9];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) x[i] = 0.0;
+        if ((int)mine & (int)want_n) {  // EstimateNormals (ISR.cpp:643, :43): ranks 0 .. kn-1, self included
+            for (int r = l; r < kn; r += 8) {
+                const p3 p = ld3(P4, (int)rl[r]);
+                const double px = p.x, py = p.y, pz = p.z;
+                x[0] += px; x[1] += py; x[2] += pz;
+                x[3] += px * px; x[4] += px * py; x[5] += px * pz;
+                x[6] += py * py; x[7] += py * pz; x[8] += pz * pz;
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
             x[i] += gxd(x[i], 1);
             x[i] += gxd(x[i], 2);
             x[i] += gxd(x[i], 4);
         }
         __builtin_amdgcn_wave_barrier();
         if (l == 0) {
-            double* pj = park_of(wid, g);
             const int flags = mine ? ((want_t ? 1 : 0) | (want_n ? 2 : 0)) : 0;
             pj[P8_FLAGS] = (double)flags;
             if (mine) {
 #pragma unroll
-                for (int i = 0; i < kSums8; ++i) pj[P8_SUM + i] = x[i];
-                pj[P8_R] = Rf;
+                for (int i = 0; i < 9; ++i) pj[P8_SUM + 12 + i] = x[i];
                 pj[P8_KK] = (double)kk;
                 pj[P8_GP] = (double)(cl.off + T.perm[wq]);
                 pj[P8_K] = (double)K;
@@ -1076,9 +834,9 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
     // its smallest eigenvector by cyclic Jacobi; normals: FastEigen3x3 of the kn-point
     // covariance (Open3D EstimateNormals, ISR.cpp:643) and the GICP covariance from it.
     auto toldi_eig = [&](double* pb) __attribute__((always_inline)) {
-        const int wb = (int)pb[P8_W];  // the query's tree slot
+        const p3 q = ld3(P4, (int)pb[P8_W]);  // the query's tree slot
         const double rz = (double)((int)pb[P8_KK] / 3);
-        const double q3[3] = {TX[wb], TY[wb], TZ[wb]};
+        const double q3[3] = {q.x, q.y, q.z};
         double cq[3], S[3];
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
@@ -1091,11 +849,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
 #pragma unroll
         for (int k = 0; k < 6; ++k)
             c6[k] = M[k] - S[ia[k]] * cq[ib[k]] - cq[ia[k]] * S[ib[k]] + rz * cq[ia[k]] * cq[ib[k]];
-#ifdef SE3ICP_LRF8_SKIP_EIG  // (measurement build: the epilogue's share of the kernel; wrong frames)
-        const d3 zn = d3{c6[0], c6[1], c6[2]};
-#else
         const d3 zn = jacobi_smallest_evec(c6[0], c6[1], c6[2], c6[3], c6[4], c6[5]);
-#endif
         pb[P8_ZN] = zn.x;
         pb[P8_ZN + 1] = zn.y;
         pb[P8_ZN + 2] = zn.z;
@@ -1116,11 +870,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
             n6[4] = cu[7] - cu[1] * cu[2];
             n6[5] = cu[8] - cu[2] * cu[2];
         }
-#ifdef SE3ICP_LRF8_SKIP_EIG
-        d3 nm = d3{n6[0], n6[1], n6[2]};
-#else
         d3 nm = fast_eigen3x3(n6[0], n6[1], n6[2], n6[3], n6[4], n6[5]);
-#endif
         if (sqrt(dot3(nm, nm)) == 0.0) nm = d3{0, 0, 1};
         const int gp = (int)pb[P8_GP];
         v.nrm64[gp] = nm.x;
@@ -1133,18 +883,6 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
             for (int r = 0; r < 6; ++r) v.cov64[(size_t)r * v.ld + gp] = cv[r];
         }
     };
-#if SE3ICP_LRF8_EPI_WAVE
-    // each wave its own eight queries (lanes 0-7 TOLDI, 8-15 normals): no block barrier,
-    // a wave that finished its traversal early retires without waiting for the others
-    __builtin_amdgcn_wave_barrier();
-    {
-        double* pb = park_of(wid, lane & 7);
-        const int b_flags = lane < 16 ? (int)pb[P8_FLAGS] : 0;
-        if ((int)(lane < 8) & (b_flags & 1)) toldi_eig(pb);
-        if ((int)(lane >= 8) & ((b_flags & 2) >> 1)) normal_eig(pb);
-    }
-    __builtin_amdgcn_wave_barrier();
-#else
     // The 3x3 problems of the block's 32 queries, one lane each: wave 0 the TOLDI ones
     // (cyclic Jacobi), wave 1 the normals at the same time.
     __syncthreads();
@@ -1155,22 +893,18 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
         if ((b_flags & 2) && wid == 1) normal_eig(pb);
     }
     __syncthreads();
-#endif
 
     // ---------------------------------------------------------------- TOLDI axes (ISR.cpp:286-306)
     {
-        double* pj = park_of(wid, g);
         const int flags = (int)pj[P8_FLAGS];
         double x6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         if (flags & 1) {
             const double nx = pj[P8_ZN], ny = pj[P8_ZN + 1], nz = pj[P8_ZN + 2];
-            const double qgx = qg64x, qgy = qg64y, qgz = qg64z;
             const double R = pj[P8_R];
             const int kkq = (int)pj[P8_KK];
-            const unsigned* rl = lists + g * kCap;
             for (int r = 1 + l; r < kkq; r += 8) {  // ranks 1 .. kk-1
-                const int slot = (int)rl[r];
-                const double vx = TX[slot] - qgx, vy = TY[slot] - qgy, vz = TZ[slot] - qgz;
+                const p3 p = ld3(P4, (int)rl[r]);
+                const double vx = p.x - qg.x, vy = p.y - qg.y, vz = p.z - qg.z;
                 x6[0] += vx; x6[1] += vy; x6[2] += vz;
                 const double an = nx * vx + ny * vy + nz * vz;
                 const double rr = R - sqrt(vx * vx + vy * vy + vz * vz);
@@ -1190,39 +924,29 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(SE3ICP_
             for (int i = 0; i < 6; ++i) pj[P8_SUM + i] = x6[i];
         }
     }
-    // the frames (ISR.cpp:298-307, 597-607)
-    auto frame_out = [&](const double* pb) __attribute__((always_inline)) {
-        const int w = (int)pb[P8_W];
-        const CloudSetup sw = setup[cloud_of[w]];
-        const double qgx = TX[w], qgy = TY[w], qgz = TZ[w];
-        d3 nrm{pb[P8_ZN], pb[P8_ZN + 1], pb[P8_ZN + 2]};
-        if (nrm.x * pb[P8_SUM] + nrm.y * pb[P8_SUM + 1] + nrm.z * pb[P8_SUM + 2] < 0.0)
-            nrm = d3{-nrm.x, -nrm.y, -nrm.z};  // ISR.cpp:298
-        const d3 zax = nrm;
-        const d3 accs{pb[P8_SUM + 3], pb[P8_SUM + 4], pb[P8_SUM + 5]};
-        d3 xax = accs - dot3(accs, zax) * zax;  // ISR.cpp:302-303 (no |x| = 0 guard, as the reference)
-        xax = (1.0 / sqrt(dot3(xax, xax))) * xax;
-        const d3 yax = cross3(zax, xax);  // ISR.cpp:306
-        const double al = sw.alpha, be = sw.beta;
-        const double f12[12] = {al * xax.x, al * xax.y, al * xax.z, al * yax.x, al * yax.y, al * yax.z,
-                                al * zax.x, al * zax.y, al * zax.z, be * qgx, be * qgy, be * qgz};
-        store_frame_rows(v.fr64, v.fr32, (int)pb[P8_GP], f12, sw.cf_target, qgx, qgy, qgz);
-    };
-#if SE3ICP_LRF8_EPI_WAVE
-    __builtin_amdgcn_wave_barrier();
-    {
-        const double* pb = park_of(wid, lane & 7);
-        const int b_flags = lane < 8 ? (int)pb[P8_FLAGS] : 0;
-        if (b_flags & 1) frame_out(pb);
-    }
-#else
-    __syncthreads();  // on wave 0 for the block's 32 queries
+    // the frames (ISR.cpp:298-307, 597-607), on wave 0 for the block's 32 queries
+    __syncthreads();
     if (wid == 0) {
         const double* pb = park_of(lane < kW * kQ ? lane / kQ : 0, lane % kQ);
         const int b_flags = lane < kW * kQ ? (int)pb[P8_FLAGS] : 0;
-        if (b_flags & 1) frame_out(pb);
+        if (b_flags & 1) {
+            const int w = (int)pb[P8_W];
+            const CloudSetup sw = setup[cloud_of[w]];
+            const p3 q = ld3(P4, w);
+            d3 nrm{pb[P8_ZN], pb[P8_ZN + 1], pb[P8_ZN + 2]};
+            if (nrm.x * pb[P8_SUM] + nrm.y * pb[P8_SUM + 1] + nrm.z * pb[P8_SUM + 2] < 0.0)
+                nrm = d3{-nrm.x, -nrm.y, -nrm.z};  // ISR.cpp:298
+            const d3 zax = nrm;
+            const d3 accs{pb[P8_SUM + 3], pb[P8_SUM + 4], pb[P8_SUM + 5]};
+            d3 xax = accs - dot3(accs, zax) * zax;  // ISR.cpp:302-303 (no |x| = 0 guard, as the reference)
+            xax = (1.0 / sqrt(dot3(xax, xax))) * xax;
+            const d3 yax = cross3(zax, xax);  // ISR.cpp:306
+            const double al = sw.alpha, be = sw.beta;
+            const double f12[12] = {al * xax.x, al * xax.y, al * xax.z, al * yax.x, al * yax.y, al * yax.z,
+                                    al * zax.x, al * zax.y, al * zax.z, be * q.x, be * q.y, be * q.z};
+            store_frame_rows(v.fr64, v.fr32, (int)pb[P8_GP], f12, sw.cf_target, q.x, q.y, q.z);
+        }
     }
-#endif
 #ifdef SE3ICP_PROF
     PROF8_NOW(t_a3);
     PROF8_ADD(c_epi, t_a2, t_a3);
@@ -1245,7 +969,7 @@ void launch_lrf8(const View& v, const int32_t* wave_base, int w_lo, int w_hi, in
     const int nb = (w_hi - w_lo + kW - 1) / kW;
     if (nb <= 0) return;
     hipLaunchKernelGGL(k_lrf8, dim3(nb), dim3(64 * kW), 0, s, v, v.cloud_of, v.setup, v.clouds, v.t3.lo, v.t3.hi,
-                       v.t3.tvec64, wave_base, w_lo, w_hi, fb_list, fb_count);
+                       v.t3.tpt64, wave_base, w_lo, w_hi, fb_list, fb_count);
 }
 
 }  // namespace se3icp

@@ -972,8 +972,11 @@ __global__ __launch_bounds__(256) void k_tree_finish(TreeView t) {
             }
         } else {
             for (int d = 0; d < t.D; ++d) t.tvec[(size_t)d * t.ld + g] = t.vec[(size_t)d * t.ld + src];
-            if (want64)
-                for (int d = 0; d < t.D; ++d) t.tvec64[(size_t)d * t.ld + g] = t.vec64[(size_t)d * t.ld + src];
+            if (want64) {
+                double x[3] = {0.0, 0.0, 0.0};
+                for (int d = 0; d < t.D; ++d) t.tvec64[(size_t)d * t.ld + g] = x[d < 3 ? d : 0] = t.vec64[(size_t)d * t.ld + src];
+                if (t.tpt64) t.tpt64[g] = make_double4(x[0], x[1], x[2], 0.0);
+            }
         }
     }
 }

@@ -29,6 +29,7 @@ struct TreeView {
     float* tvec;       // [D][ld] vectors in tree order
     const double* vec64;  // optional f64 vectors (original order, the layout of vec) ...
     double* tvec64;       // ... copied into tree order (coalesced leaf / query-chunk loads)
+    double4* tpt64;       // 3-D: the tree-ordered f64 points as (x, y, z, 0) records (one line per gather)
     int32_t vec64_sources_only;  // copy the f64 vectors of even (source) clouds only
     uint32_t* blo;     // [nclouds][nnodes][D] build scratch (orderable bits)
     uint32_t* bhi;
