@@ -46,6 +46,11 @@ using namespace knn;
 constexpr int kW = 4;     // waves per block
 constexpr int kQ = 8;     // queries per wave (eight lanes each in the group phases)
 constexpr int kCap = 192; // candidates buffered per query (u32: cut key | candidate id)
+// LDS stride of the lists: 196 entries = 49 16-B slots, odd, so that the lane-major
+// ds_read_b128 of a 128-entry run (lane l of group g: entries 16 l .. 16 l + 15) puts every
+// 16-lane bank group on 16 distinct slots of the 256-B bank row (conflict-free), and the
+// lane-major ds_read_b32 of an unaligned run is 4-way instead of 16-way
+constexpr int kStride = 196;
 constexpr int kLeaves = 64;              // leaves one wave may scan: candidate id = (list index << 6) | lane
 constexpr unsigned kIdBits = 0xfffu;     // low bits of a list entry: the candidate id
 // bound of the accept-all phase: every finite key (a lane past the leaf's end carries an
@@ -61,7 +66,7 @@ enum Park8 {
     P8_N = 31
 };
 constexpr int kParkAt = 128;  // list entry where the park starts (8-byte aligned)
-static_assert(kCap >= kParkAt + 2 * P8_N, "the park overlays the list tail");
+static_assert(kCap >= kParkAt + 2 * P8_N && kStride >= kCap, "the park overlays the list tail");
 
 // lane ^ m within a group of eight lanes (m = 1..7 as used by the networks)
 __device__ __forceinline__ unsigned gx(unsigned x, int m) {
@@ -141,7 +146,44 @@ __device__ __forceinline__ void sort8(unsigned (&k)[PER], int l) {
     net8<PER, 8 * PER>(k, l);
 }
 
-// sort the run list[0 .. len) (len <= 8 * PER) in place
+// Lane-major access of a run at a 16-B aligned list base: entry e = l * PER + s in k[s],
+// one ds_read_b128 / ds_write_b128 per four entries.  Entries past len read as kPad; a
+// store writes whole quads (a quad's entries past len land in free list space: the aligned
+// runs are the list's head, and a head that is followed by a tail is exactly 128 long).
+template <int PER>
+__device__ __forceinline__ void load_head(const unsigned* list, int len, int l, unsigned (&k)[PER]) {
+#pragma unroll
+    for (int q = 0; q < PER / 4; ++q) {
+        const int e0 = l * PER + 4 * q;
+        uint4 x = make_uint4(kPad, kPad, kPad, kPad);
+        if (e0 < len) x = *reinterpret_cast<const uint4*>(list + e0);
+        k[4 * q] = x.x;
+        k[4 * q + 1] = e0 + 1 < len ? x.y : kPad;
+        k[4 * q + 2] = e0 + 2 < len ? x.z : kPad;
+        k[4 * q + 3] = e0 + 3 < len ? x.w : kPad;
+    }
+}
+template <int PER>
+__device__ __forceinline__ void store_head(unsigned* list, int len, int l, const unsigned (&k)[PER], unsigned add = 0u) {
+#pragma unroll
+    for (int q = 0; q < PER / 4; ++q) {
+        const int e0 = l * PER + 4 * q;
+        if (e0 < len)
+            *reinterpret_cast<uint4*>(list + e0) =
+                make_uint4(k[4 * q] + add, k[4 * q + 1] + add, k[4 * q + 2] + add, k[4 * q + 3] + add);
+    }
+}
+// sort the head run list[0 .. len) (len <= 8 * PER, list 16-B aligned) in place
+template <int PER = 16>
+__device__ __forceinline__ void sort_head(unsigned* list, int len, int l) {
+    unsigned k[PER];
+    load_head<PER>(list, len, l, k);
+    sort8<PER>(k, l);
+    __builtin_amdgcn_wave_barrier();
+    store_head<PER>(list, len, l, k);
+    __builtin_amdgcn_wave_barrier();
+}
+// sort the run list[0 .. len) (len <= 8 * PER, any alignment) in place
 template <int PER = 16>
 __device__ __forceinline__ void sort_run(unsigned* list, int len, int l) {
     unsigned k[PER];
@@ -205,10 +247,10 @@ __device__ __forceinline__ unsigned kth_of_two(const unsigned* A, int na, const 
 // at the bound) are compacted unmerged (prefix 0).
 __device__ __forceinline__ uint3 tighten_group_sorted(unsigned* lists, int g, int l, int nbg, int mv, int nmax, int Kw,
                                                       bool presort, int tail_per, float S) {
-    unsigned* list = lists + g * kCap;
+    unsigned* list = lists + g * kStride;
     if (presort) {
         mv = min(nbg, 128);
-        sort_run<16>(list, mv, l);
+        sort_head<16>(list, mv, l);
     }
     const int nb = nbg - mv;
     unsigned* B = list + mv;
@@ -219,10 +261,11 @@ __device__ __forceinline__ uint3 tighten_group_sorted(unsigned* lists, int g, in
     const int kept = ka + kb;
     if (__ballot(kept > 128) == 0ull) {
         unsigned k[16];
+        load_head<16>(list, ka, l, k);
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
             const int e = l * 16 + s;
-            k[s] = e < ka ? list[e] : (e >= 128 - kb ? B[127 - e] : kPad);
+            if (e >= 128 - kb) k[s] = B[127 - e];
         }
         __builtin_amdgcn_wave_barrier();
         stage8<16, 128, 64>(k, l);
@@ -232,11 +275,7 @@ __device__ __forceinline__ uint3 tighten_group_sorted(unsigned* lists, int g, in
         stage8<16, 128, 4>(k, l);
         stage8<16, 128, 2>(k, l);
         stage8<16, 128, 1>(k, l);
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-            const int e = l * 16 + s;
-            if (e < kept) list[e] = k[s];
-        }
+        store_head<16>(list, kept, l, k);
         __builtin_amdgcn_wave_barrier();
         return make_uint3(tg, (unsigned)kept, (unsigned)kept);
     }
@@ -277,16 +316,12 @@ __device__ __forceinline__ p3 ld3(const double4* __restrict__ P4, int i) {
 __device__ __forceinline__ bool final_group(unsigned* lists, const int* leaf_slot, const double4* __restrict__ P4,
                                             const int32_t* __restrict__ perm, double qx, double qy, double qz, int off,
                                             int g, int l, int nbg, int lim) {
-    unsigned* list = lists + g * kCap;
+    unsigned* list = lists + g * kStride;
     unsigned long long k[16];
     bool unsorted = false;
     {
         unsigned k32[16];
-#pragma unroll
-        for (int s = 0; s < 16; ++s) {
-            const int e = l * 16 + s;
-            k32[s] = e < nbg ? list[e] : kPad;
-        }
+        load_head<16>(list, nbg, l, k32);
         sort8<16>(k32, l);
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
@@ -343,10 +378,11 @@ __device__ __forceinline__ bool final_group(unsigned* lists, const int* leaf_slo
         if ((int)(l < 7) & (int)(e + 1 < lim) & (int)((unsigned)(k[15] >> 32) == (unsigned)(nx >> 32))) tied |= 1u << 15;
     }
     __builtin_amdgcn_wave_barrier();
+    {
+        unsigned sl[16];
 #pragma unroll
-    for (int s = 0; s < 16; ++s) {
-        const int e = l * 16 + s;
-        if (e < nbg) list[e] = (unsigned)off + (unsigned)k[s];
+        for (int s = 0; s < 16; ++s) sl[s] = (unsigned)k[s];
+        store_head<16>(list, nbg, l, sl, (unsigned)off);
     }
     __builtin_amdgcn_wave_barrier();
     bool bad = unsorted;
@@ -380,7 +416,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(6))) vo
     const double4* __restrict__ P4, const int32_t* __restrict__ wave_base, int w_lo, int nwaves,
     int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_count) {
     // (a query's park overlays the tail of its list, free once the list is final: <= 128 entries)
-    __shared__ __attribute__((aligned(16))) unsigned s_list[kW][kQ][kCap];
+    __shared__ __attribute__((aligned(16))) unsigned s_list[kW][kQ][kStride];
     auto park_of = [&](int w, int j) __attribute__((always_inline)) {
         return reinterpret_cast<double*>(&s_list[w][j][kParkAt]);
     };
@@ -567,7 +603,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(6))) vo
         for (int j = 0; j < kQ; ++j) {
             if (ent[j] <= Tq[j]) {  // (the ballot's own compare: the exec mask, no bit test of m)
                 const int at = (int)nbq[j] + __builtin_amdgcn_mbcnt_hi((unsigned)(m[j] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m[j], 0u));
-                lists[j * kCap + at] = ent[j];
+                lists[j * kStride + at] = ent[j];
             }
             nbq[j] += (unsigned)__popcll(m[j]);
         }
@@ -747,7 +783,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(6))) vo
     // assignment and arithmetic as k_knn.hip's sums pass, over the same rank order, so the
     // two kernels' frames agree bit for bit; the TOLDI and the normal sums are two passes
     // (their live registers do not add up).
-    const unsigned* rl = lists + g * kCap;
+    const unsigned* rl = lists + g * kStride;
     double* pj = park_of(wid, g);
     {
         double x[12];
