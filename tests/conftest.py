@@ -16,6 +16,41 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device)")
 
 
+# Parity counters of the GPU tests (index near-ties, 1-ulp distances, trimmed-set swaps,
+# rechecked queries, frames outside 1e-8 ...): recorded by the tests through the
+# `parity_record` fixture and written at the end of the session to
+# gpurun_out/parity_counters.json (merged back from the GPU box; the round's copy is
+# committed under profiles/), so the record shows them without -s.
+_PARITY = {}
+
+
+@pytest.fixture(scope="session")
+def parity_record():
+    def rec(name, **counters):
+        d = _PARITY.setdefault(name, {})
+        for k, v in counters.items():
+            d[k] = v.item() if hasattr(v, "item") else v
+    return rec
+
+
+def pytest_sessionfinish(session, exitstatus):
+    if not _PARITY:
+        return
+    import json
+    out = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    path = os.path.join(out, "parity_counters.json")
+    old = {}
+    if os.path.exists(path):
+        try:
+            old = json.load(open(path))
+        except Exception:
+            old = {}
+    old.update(_PARITY)
+    with open(path, "w") as f:
+        json.dump(old, f, indent=1, sort_keys=True)
+
+
 @pytest.fixture(scope="session")
 def fixture_clouds():
     from se3icp.io import read_ply_xyz

@@ -55,8 +55,8 @@ def test_fixture_se3_icp_matches_oracle_and_ground_truth(se3icp_mod, refcpu, fix
     T = reg.current_estimated_T_
     assert np.linalg.norm(T - ref["T"]) <= 1e-5
     assert np.linalg.norm(T - fixture_T_gt) <= 1e-6
-    assert abs(reg.num_iterations_ - ref["num_iterations"]) <= 1
-    assert abs(reg.num_pure_se3_iterations_ - ref["num_pure_se3_iterations"]) <= 1
+    assert reg.num_iterations_ == ref["num_iterations"]
+    assert reg.num_pure_se3_iterations_ == ref["num_pure_se3_iterations"]
 
 
 @pytest.mark.parametrize("variant", ["pt2pt", "pt2pl", "gicp"])
@@ -67,7 +67,7 @@ def test_fixture_vanilla_icp_matches_oracle(se3icp_mod, refcpu, fixture_clouds, 
     ref = refcpu.register(src, tgt, refcpu.RUN_ICP, variant, refcpu.cli_params())
     assert np.linalg.norm(got.T - ref["T"]) <= 1e-5
     assert got.num_pure_se3_iterations == -1
-    assert abs(got.num_iterations - ref["num_iterations"]) <= 1
+    assert got.num_iterations == ref["num_iterations"]
 
 
 def test_fixture_with_cf_matches_oracle(se3icp_mod, refcpu, fixture_clouds, fixture_T_gt):
@@ -79,12 +79,13 @@ def test_fixture_with_cf_matches_oracle(se3icp_mod, refcpu, fixture_clouds, fixt
 
 
 # --------------------------------------------------------------------------- stages
-def test_knn_self_matches_oracle(se3icp_mod, refcpu, fixture_clouds):
+def test_knn_self_matches_oracle(se3icp_mod, refcpu, fixture_clouds, parity_record):
     src, _ = fixture_clouds
     k = 90
     g = se3icp_mod.knn_self(src, k)
     ri, rd = refcpu.knn_self(src, k)
     same = (g == ri)
+    parity_record("knn_self fixture k=90", queries=len(src), lists_differing_in_tie_order=int((~same.all(axis=1)).sum()))
     if not same.all():
         # allowed only where the two lists differ by exact-distance ties
         bad = np.nonzero(~same.all(axis=1))[0]
@@ -120,7 +121,7 @@ def _stage_cloud(kind, fixture_clouds):
 
 
 @pytest.mark.parametrize("kind", ["fixture", "kitti"])
-def test_toldi_frames_match_oracle(se3icp_mod, refcpu, fixture_clouds, kind):
+def test_toldi_frames_match_oracle(se3icp_mod, refcpu, fixture_clouds, kind, parity_record):
     """Frames agree to 1e-8 except where the frame is ill-conditioned, and every
     disagreement must be one: a near-degenerate smallest eigenvalue of the TOLDI
     covariance (the z axis, ISR.cpp:275-281) or a near-zero projected x axis
@@ -131,6 +132,8 @@ def test_toldi_frames_match_oracle(se3icp_mod, refcpu, fixture_clouds, kind):
     r = refcpu.toldi_frames(src, k)
     diff = np.abs(g - r).reshape(len(src), -1).max(axis=1)
     bad = np.nonzero(diff > 1e-8)[0]
+    parity_record(f"toldi frames {kind} k=90", points=len(src), frames_over_1e8=len(bad),
+                  max_diff_well_conditioned=float(np.max(diff[diff <= 1e-8], initial=0.0)))
     assert len(bad) <= 0.001 * len(src), np.sort(diff)[-10:]
     if len(bad):
         idx, _ = refcpu.knn_self(src, k)
@@ -152,7 +155,7 @@ def test_toldi_frames_match_oracle(se3icp_mod, refcpu, fixture_clouds, kind):
 
 
 @pytest.mark.parametrize("kind", ["fixture", "kitti"])
-def test_estimate_normals_match_oracle(se3icp_mod, refcpu, fixture_clouds, kind):
+def test_estimate_normals_match_oracle(se3icp_mod, refcpu, fixture_clouds, kind, parity_record):
     """Normals (sign included: FastEigen3x3 is deterministic given the covariance) agree
     to 1e-8 except at near-degenerate covariances (Open3D's cumulant covariance of the 30
     nearest points, ISR.cpp:643), and every disagreement must be one."""
@@ -162,6 +165,8 @@ def test_estimate_normals_match_oracle(se3icp_mod, refcpu, fixture_clouds, kind)
     r = refcpu.estimate_normals(src, k)
     diff = np.abs(g - r).max(axis=1)
     bad = np.nonzero(diff > 1e-8)[0]
+    parity_record(f"normals {kind} k=30", points=len(src), normals_over_1e8=len(bad),
+                  max_diff_well_conditioned=float(np.max(diff[diff <= 1e-8], initial=0.0)))
     assert len(bad) <= 0.001 * len(src)
     if len(bad):
         idx, _ = refcpu.knn_self(src, k)
@@ -218,7 +223,7 @@ def test_bunny_pair_se3_pt2pt(se3icp_mod, refcpu, bunny_unique):
     got = se3icp_mod.register_batch([(src, tgt)], "se3_pt2pt", params)[0]
     ref = refcpu.register(src, tgt, refcpu.RUN_SE3_ICP, "pt2pt", refcpu.cli_params())
     assert np.linalg.norm(got.T - ref["T"]) <= 1e-5
-    assert abs(got.num_iterations - ref["num_iterations"]) <= 1
+    assert (got.num_iterations, got.num_pure_se3_iterations) == (ref["num_iterations"], ref["num_pure_se3_iterations"])
 
 
 def test_kitti_like_batch_gicp_trimmed(se3icp_mod, refcpu):
@@ -259,9 +264,8 @@ def test_fixture_se3_pure_matches_oracle(se3icp_mod, refcpu, fixture_clouds, var
     assert reg.run_se3_pure(variant) == 0
     ref = refcpu.register(src, tgt, refcpu.RUN_SE3_PURE, variant, refcpu.cli_params())
     assert np.linalg.norm(reg.current_estimated_T_ - ref["T"]) <= 1e-5
-    assert abs(reg.num_iterations_ - ref["num_iterations"]) <= 1
-    assert reg.num_pure_se3_iterations_ == reg.num_iterations_ or \
-        abs(reg.num_pure_se3_iterations_ - ref["num_pure_se3_iterations"]) <= 1
+    assert reg.num_iterations_ == ref["num_iterations"]
+    assert reg.num_pure_se3_iterations_ == ref["num_pure_se3_iterations"]
 
 
 def test_cli_on_fixture_matches_oracle(refcpu, fixture_clouds):
@@ -286,7 +290,7 @@ def test_cli_on_fixture_matches_oracle(refcpu, fixture_clouds):
     assert np.allclose(T, ref["T"], rtol=1e-5, atol=1e-5)
 
 
-def test_kitti_full_size_pair_matches_oracle(se3icp_mod, refcpu):
+def test_kitti_full_size_pair_matches_oracle(se3icp_mod, refcpu, parity_record):
     """BASELINE.json's size (~120k points per cloud), one pair, against the oracle."""
     from se3icp import datasets
     pairs, gts = datasets.kitti_like_pairs(1, seed=4, first=5, total_pairs=8)
@@ -295,6 +299,9 @@ def test_kitti_full_size_pair_matches_oracle(se3icp_mod, refcpu):
     rp = refcpu.default_params(estimated_overlap=0.7, max_num_se3_iterations=10, mse=1e-7, mse_switch_error=5e-7,
                                number_of_nn_for_LRF=90)
     ref = refcpu.register(pairs[0][0], pairs[0][1], refcpu.RUN_SE3_ICP, "gicp", rp)
+    parity_record("C4 pair 120k se3_gicp end to end", pose_frobenius=float(np.linalg.norm(got.T - ref["T"])),
+                  iterations_gpu=got.num_iterations, iterations_ref=int(ref["num_iterations"]),
+                  rechecked_queries=got.num_rechecked)
     assert np.linalg.norm(got.T - ref["T"]) <= 1e-5
     assert got.num_iterations == ref["num_iterations"]
     assert got.num_pure_se3_iterations == ref["num_pure_se3_iterations"]
@@ -344,7 +351,7 @@ def test_batch_with_pairs_finishing_at_different_iterations(se3icp_mod, refcpu, 
     for (s, t), g in zip(pairs, got):
         ref = refcpu.register(s, t, refcpu.RUN_SE3_ICP, "pt2pl", refcpu.cli_params())
         assert np.linalg.norm(g.T - ref["T"]) <= 1e-5
-        assert abs(g.num_iterations - ref["num_iterations"]) <= 1
+        assert (g.num_iterations, g.num_pure_se3_iterations) == (ref["num_iterations"], ref["num_pure_se3_iterations"])
         its.append(g.num_iterations)
     assert len(set(its)) > 1, its  # the batch really had pairs finishing at different iterations
 

@@ -121,18 +121,23 @@ def _run_both(se3icp_mod, refcpu, src, tgt, method, gparams, rkind, rvariant, rp
     return res[0], gtr, ref
 
 
+def _record(parity_record, label, tot, g, ref):
+    parity_record("trace: " + label, iterations=int(ref["num_iterations"]),
+                  pure_se3_iterations=int(ref["num_pure_se3_iterations"]), rechecked_queries=int(g.num_rechecked), **tot)
+
+
 @pytest.mark.parametrize("variant", ["pt2pt", "pt2pl", "gicp"])
-def test_fixture_correspondences_every_iteration(se3icp_mod, refcpu, fixture_clouds, variant):
+def test_fixture_correspondences_every_iteration(se3icp_mod, refcpu, fixture_clouds, variant, parity_record):
     """C1 (examples/run_registration_method.cpp:38-42): both phases, no trimming.  The
     fixture has 188 groups of duplicate points (exact f64 ties: lowest index on both sides)."""
     src, tgt = fixture_clouds
     g, gtr, ref = _run_both(se3icp_mod, refcpu, src, tgt, "se3_" + variant, se3icp_mod.cli_params(),
                             refcpu.RUN_SE3_ICP, variant, refcpu.cli_params())
     assert set(gtr["phase"].tolist()) == {1, 2}
-    compare_traces(gtr, ref, 1.0, f"C1 se3_{variant}")
+    _record(parity_record, f"C1 se3_{variant}", compare_traces(gtr, ref, 1.0, f"C1 se3_{variant}"), g, ref)
 
 
-def test_kitti_full_size_correspondences_every_iteration(se3icp_mod, refcpu):
+def test_kitti_full_size_correspondences_every_iteration(se3icp_mod, refcpu, parity_record):
     """C4 size (~120k points), se3_gicp with the KITTI driver's parameters
     (examples/benchmark_kitti.cpp:133-148): trimmed at overlap 0.7, both phases."""
     from se3icp import datasets
@@ -145,11 +150,12 @@ def test_kitti_full_size_correspondences_every_iteration(se3icp_mod, refcpu):
                             refcpu.RUN_SE3_ICP, "gicp", rp)
     assert set(gtr["phase"].tolist()) == {1, 2}
     tot = compare_traces(gtr, ref, 0.7, "C4 se3_gicp 120k")
+    _record(parity_record, "C4 se3_gicp 120k", tot, g, ref)
     # near-ties are rare: well under one query in 10^4
     assert tot["idx_diff"] <= 1e-4 * tot["queries"]
 
 
-def test_rgbd_cf_correspondences_every_iteration(se3icp_mod, refcpu):
+def test_rgbd_cf_correspondences_every_iteration(se3icp_mod, refcpu, parity_record):
     """run_se3_icp_with_cf (ISR.cpp:742-959) on a C5-style RGB-D pair (trimmed at 0.75,
     confidence-weighted GICP, translation rows from the points)."""
     from se3icp import datasets
@@ -159,7 +165,7 @@ def test_rgbd_cf_correspondences_every_iteration(se3icp_mod, refcpu):
                                number_of_nn_for_LRF=90)
     g, gtr, ref = _run_both(se3icp_mod, refcpu, src, tgt, "se3_gicp_with_cf", se3icp_mod.lounge_params(),
                             refcpu.RUN_SE3_ICP_CF, "gicp", rp)
-    compare_traces(gtr, ref, 0.75, "cf RGB-D")
+    _record(parity_record, "cf RGB-D", compare_traces(gtr, ref, 0.75, "cf RGB-D"), g, ref)
 
 
 def test_trace_is_one_shot_and_optional(se3icp_mod, fixture_clouds):
@@ -197,7 +203,7 @@ def _near_tie_queries(data, rng, n_q):
 
 
 @pytest.mark.parametrize("dim", [12, 3])
-def test_adversarial_near_ties_at_120k(se3icp_mod, refcpu, dim):
+def test_adversarial_near_ties_at_120k(se3icp_mod, refcpu, dim, parity_record):
     """>= 100k queries, each within a few ulps (or more) of equidistant between its two
     nearest targets: the f32 sweep cannot order most of them, so the certificate
     (loopdev.hpp f32_err) must send them to the f64 recheck, whose answer must be the
@@ -216,6 +222,8 @@ def test_adversarial_near_ties_at_120k(se3icp_mod, refcpu, dim):
     ri, rd2 = refcpu.nn(q, data)
     mism = np.nonzero(gi != ri)[0]
     print(f"[near-tie] dim {dim}: {n} queries, {nrech} rechecked in f64, {mism.size} index differences")
+    parity_record(f"adversarial near-ties {dim}-D", queries=n, rechecked_f64=int(nrech), index_differences=int(mism.size),
+                  d2_bit_differences=int((gd2 != rd2).sum()))
     assert mism.size == 0, (mism[:8], gi[mism[:8]], ri[mism[:8]])
     assert np.array_equal(gd2, rd2)
     assert nrech >= n // 10  # most ulp-level ties cannot be certified in f32
