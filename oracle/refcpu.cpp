@@ -891,6 +891,9 @@ struct Registration {
     int num_iterations_ = 0, num_pure_se3_iterations_ = -1;
     double scaling_factor = 1.0;
     double t_setup = 0, t_loop = 0, t_nn = 0;
+    // phase breakdown: TOLDI frames (kNN + LRF, ISR.cpp:590-591), normals /
+    // GICP covariances (:642-648), trimming (:669-671), estimator + pose / cloud updates (:689-716)
+    double t_toldi = 0, t_normals = 0, t_trim = 0, t_solve = 0;
     refcpu_trace* trace = nullptr;
 
     void record(int it, const Mat4& Ti, double mse, int nkept, const std::vector<Corr>& raw) {
@@ -1002,8 +1005,10 @@ struct Registration {
         scale(source_moving_, scaling_factor);
         scale(target_, scaling_factor);
         KDTree ts(source_.raw(), (int)source_.points.size(), 3), tt(target_.raw(), (int)target_.points.size(), 3);
+        const double tl = now_ms();
         toldi_all(source_, ts, prm.number_of_nn_for_LRF, source_se3_cloud_);
         toldi_all(target_, tt, prm.number_of_nn_for_LRF, target_se3_cloud_);
+        t_toldi = now_ms() - tl;
         for (auto* cl : {&source_se3_cloud_, &target_se3_cloud_})
             for (auto& M : *cl) {
                 for (int i = 0; i < 3; i++)
@@ -1042,12 +1047,14 @@ struct Registration {
         double mse_prev = 1e7, mse_cur = 1e7, mse_rel = 1e7, change = 1e7;
         num_iterations_ = 0;
         num_pure_se3_iterations_ = 0;
+        const double tnr = now_ms();
         if (cf || variant == REFCPU_GICP) {
             init_gicp(source_moving_, 1e-3);
             init_gicp(target_, 1e-3);
         } else if (variant == REFCPU_PT2PL) {
             estimate_normals(target_, 30);
         }
+        t_normals = now_ms() - tnr;
         t_setup = now_ms() - t0;
         double t1 = now_ms();
         bool sw = false;
@@ -1062,7 +1069,10 @@ struct Registration {
                 nn_xyz(tree_xyz, raw);
             }
             t_nn += now_ms() - tn;
+            const double tt0 = now_ms();
             std::vector<Corr> kept = trim(raw, prm.estimated_overlap);
+            const double tt1 = now_ms();
+            t_trim += tt1 - tt0;
             mse_prev = mse_cur;
             mse_cur = cf ? mse_euclid(kept) : mse_of(kept);
             mse_rel = std::fabs(mse_cur - mse_prev);
@@ -1081,6 +1091,7 @@ struct Registration {
             const int ns = (int)source_se3_cloud_.size();
 #pragma omp parallel for schedule(static)
             for (int k = 0; k < ns; k++) source_se3_cloud_[k] = mul(Ti, source_se3_cloud_[k]);
+            t_solve += now_ms() - tt1;
             record(num_iterations_ - 1, Ti, mse_cur, (int)kept.size(), raw);
             if (pure) {
                 if (num_iterations_ == prm.max_num_se3_iterations || mse_rel < scaling_factor * prm.mse) break;
@@ -1109,8 +1120,10 @@ struct Registration {
         KDTree tree_xyz(target_.raw(), (int)target_.points.size(), 3);
         T = Mat4::I();
         double mse_prev = 1e7, mse_cur = 1e7, mse_rel = 1e7;
+        const double tnr = now_ms();
         if (variant == REFCPU_PT2PL) estimate_normals(target_, 30);
         if (variant == REFCPU_GICP) { init_gicp(source_moving_, 1e-3); init_gicp(target_, 1e-3); }
+        t_normals = now_ms() - tnr;
         num_iterations_ = 0;
         t_setup = now_ms() - t0;
         double t1 = now_ms();
@@ -1119,13 +1132,17 @@ struct Registration {
             double tn = now_ms();
             nn_xyz(tree_xyz, raw);
             t_nn += now_ms() - tn;
+            const double tt0 = now_ms();
             std::vector<Corr> kept = trim(raw, prm.estimated_overlap);
+            const double tt1 = now_ms();
+            t_trim += tt1 - tt0;
             mse_prev = mse_cur;
             mse_cur = mse_of(kept);
             mse_rel = std::fabs(mse_cur - mse_prev);
             Mat4 Ti = estimate(variant, kept);
             transform(source_moving_, Ti);
             T = mul(Ti, T);
+            t_solve += now_ms() - tt1;
             record(num_iterations_, Ti, mse_cur, (int)kept.size(), raw);
             num_iterations_++;
             if (num_iterations_ == prm.max_num_iterations || mse_rel < prm.mse) break;
@@ -1201,6 +1218,10 @@ int refcpu_register(const double* src, int64_t n_src, const double* tgt, int64_t
     out->time_setup_ms = R.t_setup;
     out->time_loop_ms = R.t_loop;
     out->time_nn_ms = R.t_nn;
+    out->time_toldi_ms = R.t_toldi;
+    out->time_normals_ms = R.t_normals;
+    out->time_trim_ms = R.t_trim;
+    out->time_solve_ms = R.t_solve;
     return 0;
 }
 

@@ -57,6 +57,10 @@ typedef struct refcpu_result {
     double time_setup_ms;           /* normalization + LRF + normals/covariances */
     double time_loop_ms;            /* the while(true) loop */
     double time_nn_ms;              /* correspondence search inside the loop */
+    double time_toldi_ms;           /* setup: kNN + TOLDI frames of both clouds (ISR.cpp:590-591) */
+    double time_normals_ms;         /* setup: normals / GICP covariances (ISR.cpp:642-648) */
+    double time_trim_ms;            /* loop: trimmed rejector (ISR.cpp:669-671) */
+    double time_solve_ms;           /* loop: MSE, estimator, Transform, SE(3) update (ISR.cpp:684-716) */
 } refcpu_result;
 
 /* Optional per-iteration trace.  Any pointer may be NULL.

@@ -43,6 +43,10 @@ class Result(C.Structure):
         ("time_setup_ms", C.c_double),
         ("time_loop_ms", C.c_double),
         ("time_nn_ms", C.c_double),
+        ("time_toldi_ms", C.c_double),
+        ("time_normals_ms", C.c_double),
+        ("time_trim_ms", C.c_double),
+        ("time_solve_ms", C.c_double),
     ]
 
 
@@ -157,7 +161,9 @@ def register(src, tgt, run_kind=RUN_SE3_ICP, variant="pt2pl", params: Params | N
         raise RuntimeError(f"refcpu_register failed: {rc}")
     out.update(T=np.array(res.T).reshape(4, 4), num_iterations=res.num_iterations,
                num_pure_se3_iterations=res.num_pure_se3_iterations, scaling_factor=res.scaling_factor,
-               time_setup_ms=res.time_setup_ms, time_loop_ms=res.time_loop_ms, time_nn_ms=res.time_nn_ms)
+               time_setup_ms=res.time_setup_ms, time_loop_ms=res.time_loop_ms, time_nn_ms=res.time_nn_ms,
+               time_toldi_ms=res.time_toldi_ms, time_normals_ms=res.time_normals_ms, time_trim_ms=res.time_trim_ms,
+               time_solve_ms=res.time_solve_ms)
     return out
 
 

@@ -474,10 +474,12 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(6))) vo
 #pragma unroll
     for (int j = 0; j < kQ; ++j) { Tq[j] = kAll; nbq[j] = 0u; }
     auto group_len = [&]() __attribute__((always_inline)) {
-        unsigned x = nbq[0];
+        // lane 8 j gets nbq[j] (v_writelane), every lane reads its group's first lane (a
+        // select chain over the scalars is turned into a scratch array indexed by g)
+        int x = 0;
 #pragma unroll
-        for (int j = 1; j < kQ; ++j) x = (g == j) ? nbq[j] : x;
-        return x;
+        for (int j = 0; j < kQ; ++j) asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(x) : "s"(nbq[j]), "n"(8 * j));
+        return (unsigned)__shfl(x, lane & ~7, 64);
     };
     int mvv = 0;  // sorted prefix of the group's list
     float* qv = s_q[wid];
