@@ -44,12 +44,14 @@ WORKLOADS = {
                            number_of_nn_for_LRF=90),
                desc="C4: se3_gicp, KITTI driver params (overlap 0.7, mse 1e-7, switch 5e-7, max_se3 10, k=90)",
                data="synthetic (64-beam LiDAR ray-cast street scenes, seed 4; KITTI not available offline)"),
-    "C2": dict(method="se3_pt2pt", ppg=1, run="se3", variant="pt2pt",
+    "C2": dict(method="se3_pt2pt", ppg=8, run="se3", variant="pt2pt",
                params=dict(estimated_overlap=1.0, max_num_se3_iterations=10, mse=1e-5, mse_switch_error=5e-5,
                            number_of_nn_for_LRF=90),
-               desc="C2: se3_pt2pt on the unique Stanford bunny (34,834 pts x50, noise var 0.005), "
-                    "benchmark_synthetic.cpp:356-363 params",
-               data="stanford_bunny.ply unique vertices (tests/golden), random rigid T + noise per pair (seed 1+i)"),
+               desc="C2: se3_pt2pt on the reference's synthetic bunny problems (benchmark_synthetic.cpp:91-160 with "
+                    "its own mt19937 / normal_distribution / RandomDownSample streams, noise var 0.005) at "
+                    "RandomDownSample(0.2) of stanford_bunny.ply x50 = 41,670 pts per cloud (BASELINE '~40k'; the "
+                    "driver itself uses 0.02), B_SYN:356-363 params, 8 cases per GPU",
+               data="stanford_bunny.ply (tests/golden) -> se3icp_synthetic_reference_device, generated on the GPU"),
     "C3": dict(method="se3_pt2pl", ppg=32, run="se3", variant="pt2pl",
                params=dict(estimated_overlap=0.75, max_num_se3_iterations=10, mse_switch_error=5e-5,
                            number_of_nn_for_LRF=90),
@@ -103,15 +105,24 @@ def pmc_counter(kernel_substr: str, counter: str):
     return None
 
 
-def make_pairs(wl: str, total: int, first: int, count: int, n_az: int):
+C2_SETUPS = {"easy": (5.0, np.pi / 4), "moderate": (10.0, np.pi / 2)}  # B_SYN:106-108, :111-112
+
+
+def make_pairs(wl: str, total: int, first: int, count: int, n_az: int, c2_setup: str = "easy", device: int = 0):
     """The rank's pairs [first, first + count) of a `total`-pair sequence, with ground truths."""
     from se3icp import datasets
     if wl == "C4":
         return datasets.kitti_like_pairs(count, seed=4, first=first, total_pairs=total, n_az=n_az)
     if wl == "C2":
-        base = np.load(os.path.join(ROOT, "tests", "golden", "bunny_unique_f32.npy")).astype(np.float64)
-        out = [datasets.bunny_pair(base, seed=1 + i) for i in range(first, first + count)]
-        return [(s, t) for s, t, _ in out], [T for _, _, T in out]
+        # the reference's own problems, case after case (its streams are sequential: every
+        # rank draws the whole sequence and keeps its block), written by the GPU
+        u = np.load(os.path.join(ROOT, "tests", "golden", "bunny_unique_f32.npy"))
+        ids = np.load(os.path.join(ROOT, "tests", "golden", "bunny_vertex_ids.npy"))
+        cloud = u[ids].astype(np.float64) * 50.0
+        tr, rr = C2_SETUPS[c2_setup]
+        src, tgt, T = datasets.synthetic_reference_gpu(cloud, total, ratio=0.2, noise_var=0.005, t_range=tr,
+                                                       r_range=rr, device=device)
+        return ([(src[i], tgt[i]) for i in range(first, first + count)], [T[i] for i in range(first, first + count)])
     seed = 3 if wl == "C3" else 5
     pairs, gts = datasets.rgbd_pairs(total, seed=seed, stride=4)
     return pairs[first:first + count], gts[first:first + count]
@@ -129,6 +140,10 @@ def main():
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="collective backend for N > 1 (gloo: ranks may share one GPU, as in the tests)")
     ap.add_argument("--dump-poses", default="", help="rank 0 writes the gathered per-pair poses (.npy)")
+    ap.add_argument("--c2-setup", choices=sorted(C2_SETUPS), default="easy",
+                    help="C2 transform ranges: BASELINE's easy_data (B_SYN:106-108) or the driver's active moderate ones")
+    ap.add_argument("--secondary", choices=["auto", "off"], default="auto",
+                    help="C4 at N=1: also time the whole 64-pair batch on this GPU (strong-scaling anchor)")
     args = ap.parse_args()
     W = WORKLOADS[args.workload]
 
@@ -164,7 +179,7 @@ def main():
     P = args.pairs_per_gpu or W["ppg"]
     t0 = time.time()
     first, count = sharding.shard(world * P, world, rank)  # weak scaling: P pairs per rank
-    pairs, gts = make_pairs(args.workload, world * P, first, count, args.n_az)
+    pairs, gts = make_pairs(args.workload, world * P, first, count, args.n_az, args.c2_setup, devi)
     npts = [p[0].shape[0] for p in pairs] + [p[1].shape[0] for p in pairs]
     log(f"rank {rank}: {args.workload} generated {count} pairs in {time.time() - t0:.1f}s, points/cloud "
         f"min {min(npts)} mean {np.mean(npts):.0f} max {max(npts)}")
@@ -249,6 +264,7 @@ def main():
                     "exact_kernel_queries_per_step": ktot.get("lrf_fallback", 0.0) / args.steps}
         roof_nn = nn_roofline(ktot, kms)
         roof_lrf = lrf_roofline(ktot, kms, args.steps, W["params"]["number_of_nn_for_LRF"])
+        roof_red = reduce_roofline(last, pairs, W, kms["reduce_ms"] / args.steps)
         # the bench line's roofline is the step's dominant kernel by GPU time; the other
         # named kernel is reported beside it
         nn_step = roof_nn["avg_launch_ms"] * roof_nn["launches"] / args.steps
@@ -289,10 +305,13 @@ def main():
             "phase_ms_per_step": {"setup": round(setup_ms / args.steps, 3), "loop": round(loop_ms / args.steps, 3)},
             "roofline": dominant,
             "roofline_other": other,
+            "roofline_reduce": roof_red,
             "cpu_baseline": None,
         }
+        if args.workload == "C4" and world == 1 and args.secondary == "auto":
+            out["secondary_64_pairs_one_gpu"] = bench_batch64(args, W, params, dev, devi)
         if world == 1 and args.cpu_baseline == "auto":
-            out["cpu_baseline"], out["parity_vs_cpu"] = cpu_baseline(pairs, last, W, value)
+            out["cpu_baseline"], out["parity_vs_cpu"] = cpu_baseline(pairs, last, W, value, params, devi)
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
@@ -372,6 +391,70 @@ def lrf_roofline(ktot, kms, steps, k):
     }
 
 
+# HBM bytes k_reduce reads per source point of an active pair in one iteration: every point
+# its correspondence's float distance (the trim key, 4 B); a kept one also its target index
+# (4), both f64 points (2 x 24), and per estimator the target normal (pt2pl, 24), both GICP
+# covariances (2 x 48), the two cf confidences (2 x 8)
+REDUCE_BYTES_KEPT = {"pt2pt": 56, "pt2pl": 80, "gicp": 152, "gicp_cf": 168}
+
+
+def reduce_roofline(res, pairs, W, red_ms):
+    """k_reduce + k_reduce_final (the per-iteration estimator sums, ISR.cpp:689-703 / 57-110,
+    and the device-side solve) against HBM: algorithmic bytes of every iteration of every
+    pair (REDUCE_BYTES_KEPT per kept correspondence, 4 B per trimmed one) over their time."""
+    key = "gicp_cf" if W["run"] == "cf" else W["variant"]
+    ratio = np.float32(W["params"].get("estimated_overlap", 1.0))
+    tot, corr, launches = 0.0, 0.0, 0
+    for r, (s, _) in zip(res, pairs):
+        ns = s.shape[0]
+        k = int(np.floor(ratio * np.float32(ns)))
+        k = ns if k >= ns else k
+        tot += r.num_iterations * (k * REDUCE_BYTES_KEPT[key] + (ns - k) * 4)
+        corr += r.num_iterations * k
+        launches = max(launches, r.num_iterations)
+    achieved = tot / (red_ms / 1000.0) / 1e9 if red_ms > 0 else 0.0
+    traffic, src = pmc_traffic("k_reduce(")
+    return {"kernel": "k_reduce + k_reduce_final", "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "avg_launch_ms": round(red_ms / max(1, launches), 4),
+            "launches": launches, "bytes_per_unit": {"kept_correspondence": REDUCE_BYTES_KEPT[key], "trimmed": 4},
+            "units_per_launch": {"kept_correspondences": round(corr / max(1, launches))},
+            "traffic": traffic, "traffic_source": src,
+            "note": "one launch pair per loop iteration for every active pair of the batch; the 28 sums per pair are "
+                    "then solved on the device (k_reduce_final)"}
+
+
+def bench_batch64(args, W, params, dev, devi, steps=3):
+    """The whole 64-pair KITTI batch of BASELINE configs[3] on this one GPU (the batch the
+    8-GPU job shards), timed like the main steps: a strong-scaling anchor beside the weak-
+    scaling value."""
+    import torch
+    import se3icp
+    from se3icp import datasets
+    t0 = time.time()
+    pairs, _ = datasets.kitti_like_pairs(64, seed=4, first=0, total_pairs=64, n_az=args.n_az)
+    log(f"secondary: 64 pairs generated in {time.time() - t0:.1f}s")
+    src = np.concatenate([p[0] for p in pairs])
+    tgt = np.concatenate([p[1] for p in pairs])
+    so = np.concatenate([[0], np.cumsum([p[0].shape[0] for p in pairs])])
+    to = np.concatenate([[0], np.cumsum([p[1].shape[0] for p in pairs])])
+    d_src = torch.from_numpy(src).to(dev)
+    d_tgt = torch.from_numpy(tgt).to(dev)
+    torch.cuda.synchronize()
+    runner = se3icp.DeviceBatchRunner(d_src.data_ptr(), so, d_tgt.data_ptr(), to, W["method"], params, device=devi,
+                                      slots=steps)
+    runner.run(0)  # warm-up
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for k in range(steps):
+        runner.run(k)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t
+    its = sum(sum(r.num_iterations for r in runner.results(k)) for k in range(steps))
+    return {"pairs": 64, "steps": steps, "ms_per_step": round(1000.0 * el / steps, 3), "value": round(its / el, 3),
+            "unit": "ICP iterations/s", "pairs_per_sec": round(64 * steps / el, 4),
+            "note": "examples/benchmark_kitti.cpp:120-197 as one batch on one GPU (synthetic scans, seed 4)"}
+
+
 def host_info():
     """nproc, CPU model, sockets and physical cores of the host, and the cgroup CPU quota."""
     info = {"nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0))}
@@ -400,7 +483,7 @@ def host_info():
     return info
 
 
-def cpu_baseline(pairs, gpu_res, W, gpu_value, budget_s=25.0):
+def cpu_baseline(pairs, gpu_res, W, gpu_value, gpu_params=None, devi=0, budget_s=25.0):
     """BASELINE.md §2 protocol: the oracle (C++/OpenMP restatement of the reference, kd-tree
     NN) on the host cores — all physical cores, the cgroup's CPU share when it is smaller,
     and 1 thread; 1 warm-up pair, then the median of 3 repeats of a sample of the rank's
@@ -430,11 +513,14 @@ def cpu_baseline(pairs, gpu_res, W, gpu_value, budget_s=25.0):
     # sample: enough pairs that one multi-thread repeat takes >= ~2 s
     n_sample = int(min(len(pairs), max(1, np.ceil(2.0 / max(t_warm, 1e-3)))))
     runs = []
-    parity_its = []
+    cpu_res = {}  # pair -> the oracle's result (first repeat at the first thread count)
+    phases = ["time_toldi_ms", "time_normals_ms", "time_nn_ms", "time_trim_ms", "time_solve_ms", "time_setup_ms",
+              "time_loop_ms"]
     for nt in counts:
         refcpu.set_num_threads(nt)
         ns = n_sample if nt > 1 else 1
         reps, used = [], 0.0
+        ph = {k: 0.0 for k in phases}
         for _ in range(3):
             it_sum, t_sum, loop_ms = 0, 0.0, 0.0
             for i in range(ns):
@@ -442,8 +528,10 @@ def cpu_baseline(pairs, gpu_res, W, gpu_value, budget_s=25.0):
                 it_sum += r["num_iterations"]
                 t_sum += dt
                 loop_ms += r["time_loop_ms"]
+                for k in phases:
+                    ph[k] += r[k]
                 if nt == counts[0]:
-                    parity_its.append((i, r["num_iterations"]))
+                    cpu_res.setdefault(i, r)
             reps.append((t_sum, it_sum, loop_ms))
             used += t_sum
             if used > budget_s:
@@ -451,10 +539,14 @@ def cpu_baseline(pairs, gpu_res, W, gpu_value, budget_s=25.0):
         t_med = statistics.median([x[0] for x in reps])
         its = reps[0][1]
         lm = statistics.median([x[2] for x in reps])
+        npr = ns * len(reps)
         runs.append({"threads": nt, "pairs": ns, "repeats": len(reps), "iterations": its,
                      "median_s": round(t_med, 4), "iter_per_s": round(its / t_med, 4),
                      "loop_iter_per_s": round(its / (lm / 1000.0), 4) if lm > 0 else None,
-                     "pairs_per_s": round(ns / t_med, 4)})
+                     "pairs_per_s": round(ns / t_med, 4),
+                     # where the reference's time goes, per pair: TOLDI (ISR.cpp:590-591), normals /
+                     # covariances (:642-648), NN (:661/665), trim (:669-671), solve + updates (:684-716)
+                     "phase_ms_per_pair": {k[5:-3]: round(ph[k] / npr, 3) for k in phases}})
         log(f"cpu baseline: {nt} threads: {ns} pairs x {len(reps)} repeats, median {t_med:.2f}s, "
             f"{its / t_med:.2f} iter/s")
     best = max(runs, key=lambda r: r["iter_per_s"])
@@ -468,9 +560,30 @@ def cpu_baseline(pairs, gpu_res, W, gpu_value, budget_s=25.0):
             "speedup_gpu_vs_cpu": round(gpu_value / best["iter_per_s"], 2),
             # the ideal-scaling ceiling of the host: 1-thread rate x every physical core
             "speedup_vs_1thread_x_physical_cores": round(gpu_value / (one["iter_per_s"] * phys), 2)}
-    parity = {"pose_frobenius_pair0": float(np.linalg.norm(gpu_res[0].T - first["T"])),
-              "iterations_gpu": [gpu_res[i].num_iterations for i, _ in parity_its[:n_sample]],
-              "iterations_cpu": [n for _, n in parity_its[:n_sample]]}
+    # per sampled pair: pose and iteration counts; for the first pair also the correspondence
+    # set of every iteration (traced on both sides): the share of equal target indices
+    per_pair = []
+    for i in sorted(cpu_res):
+        r = cpu_res[i]
+        per_pair.append({"pair": i, "pose_frobenius": float(np.linalg.norm(gpu_res[i].T - r["T"])),
+                         "iterations_gpu": gpu_res[i].num_iterations, "iterations_cpu": r["num_iterations"],
+                         "se3_iterations_gpu": gpu_res[i].num_pure_se3_iterations,
+                         "se3_iterations_cpu": r["num_pure_se3_iterations"]})
+    parity = {"pairs": per_pair, "max_pose_frobenius": max(p["pose_frobenius"] for p in per_pair),
+              "iterations_equal": all(p["iterations_gpu"] == p["iterations_cpu"] for p in per_pair)}
+    try:
+        import se3icp
+        s, t = pairs[0]
+        _, gtr = se3icp.register_batch_traced([(s, t)], W["method"], gpu_params, pair=0, max_iters=160, device=devi)
+        refcpu.set_num_threads(counts[0])
+        ref = refcpu.register(s, t, run, W["variant"], p, trace_iters=160)
+        n_it = min(len(gtr["phase"]), int(ref["num_iterations"]))
+        eq = sum(int((gtr["corr_idx"][k] == ref["corr_idx"][k]).sum()) for k in range(n_it))
+        tot = n_it * s.shape[0]
+        parity["correspondences_pair0"] = {"iterations": n_it, "queries": tot, "equal": eq,
+                                           "equal_pct": round(100.0 * eq / max(1, tot), 5)}
+    except Exception as e:  # noqa: BLE001 (the parity record is a diagnostic)
+        parity["correspondences_pair0"] = {"error": str(e)}
     return base, parity
 
 
