@@ -742,6 +742,18 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
                          sum[2] - trace_prev_[2], sum[3] - trace_prev_[3], ms[0], ms[1], ms[2], ms[3]);
             for (int k = 0; k < kStatCols; ++k) trace_prev_[k] = sum[k];
 #ifdef SE3ICP_PROF
+            {
+                // waves and summed wave time of this iteration's SE(3) group waves (column 11:
+                // (1 << 44) + dt per wave, integer sums over the slots)
+                static unsigned long long prev11 = 0;
+                unsigned long long s11 = 0;
+                for (int i = 0; i < kStatSlots; ++i) s11 += stats[kStatCols * i + 11];
+                const unsigned long long d = s11 - prev11;
+                prev11 = s11;
+                const unsigned long long nw = d >> 44, dt = d & ((1ull << 44) - 1);
+                std::fprintf(stderr, "[nn] iter %d: %llu SE(3) group waves, mean %.1f us, summed %.1f ms (100 MHz clock)\n",
+                             it, nw, nw ? (double)dt / nw / 100.0 : 0.0, (double)dt / 1e5);
+            }
             std::fprintf(stderr, "[nn] iter %d: longest SE(3) group wave %.1f us (%llu box-test steps, %llu leaf visits, "
                          "%llu queries)\n", it, (double)(stats[10] >> 40) / 100.0, (stats[10] >> 20) & 0xfffffull,
                          (stats[10] >> 6) & 0x3fffull, stats[10] & 63ull);
