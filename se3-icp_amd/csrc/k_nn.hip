@@ -38,6 +38,12 @@ namespace {
 using namespace loopdev;
 
 constexpr int kWaves = 4;
+#ifndef SE3ICP_NN_GWAVES
+#define SE3ICP_NN_GWAVES 1  // waves per k_nn_group block
+#endif
+// (one wave per block: a block's LDS is released when its last wave ends, so 4-wave blocks
+// whose waves end at different times strand LDS -- a CU holds at most five 28.7 KB blocks)
+constexpr int kGWaves = SE3ICP_NN_GWAVES;
 // Leaves wanted by at most this many lanes take the compacted path (8 lanes per query)
 #ifndef SE3ICP_NN_TPL
 #define SE3ICP_NN_TPL 4  // targets per lane in the compacted leaf sweeps (held in registers across queries)
@@ -555,15 +561,15 @@ __device__ __forceinline__ void single_one(const View& v, const PairDev* P, int 
                                            unsigned* n_box);
 
 template <int D>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_WPE))) void k_nn_group(View v) {
+__global__ __launch_bounds__(64 * kGWaves) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_WPE))) void k_nn_group(View v) {
     constexpr int NV = (D + 3) / 4;
-    __shared__ float4 s_tile[kWaves][kLeafMax * NV];
+    __shared__ float4 s_tile[kGWaves][kLeafMax * NV];
     // compacted leaf sweeps (12-D): the wave's query vectors, the list of lanes that want
     // the current leaf, and the per-query top-2 of the leaf
-    __shared__ float4 s_q[kWaves][64 * NV];
-    __shared__ int s_wl[kWaves][64];
-    __shared__ float s_r1[kWaves][64], s_r2[kWaves][64];
-    __shared__ int s_rb[kWaves][64];
+    __shared__ float4 s_q[kGWaves][64 * NV];
+    __shared__ int s_wl[kGWaves][64];
+    __shared__ float s_r1[kGWaves][64], s_r2[kGWaves][64];
+    __shared__ int s_rb[kGWaves][64];
     const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // wave-uniform work item: group jg (64 listed queries) of chunk c; the pair record,
     // node boxes and leaf ranges become scalar loads
@@ -571,9 +577,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_W
     // shorter waves for a launch whose time is set by its longest waves)
     constexpr int kSplit = D == 12 ? SE3ICP_NN_SPLIT : 1;
     // (blocks of one XCD take consecutive chunks: a pair's target tree stays in that XCD's L2)
-    const int bx = SE3ICP_NN_XCD == 2 ? xcd_block_runs(blockIdx.x, gridDim.x, SE3ICP_NN_XCD_RUN)
+    const int bx = SE3ICP_NN_XCD == 2 ? xcd_block_runs(blockIdx.x, gridDim.x, SE3ICP_NN_XCD_RUN * 4 / kGWaves)
                    : SE3ICP_NN_XCD ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-    const int wi = __builtin_amdgcn_readfirstlane(bx * kWaves + wid);
+    const int wi = __builtin_amdgcn_readfirstlane(bx * kGWaves + wid);
     const int gq = wi / kSplit, q_lo = (wi % kSplit) * (64 / kSplit);
     if ((gq >> 4) >= v.nchunks) return;
     // chunk at dispatch position gq >> 4 (k_nn_order: the costliest chunks start first, so
@@ -1027,15 +1033,15 @@ void launch_nn_prep(const View& v, hipStream_t s) {
     hipLaunchKernelGGL(k_nn_prep, dim3(v.nchunks), dim3(kChunkQ), 0, s, v);
     if (SE3ICP_NN_ORDER) hipLaunchKernelGGL(k_nn_order, dim3(1), dim3(1024), 0, s, v.chunk_cost, v.chunk_order, v.nchunks);
 }
-// 16 groups of 64 per chunk, kWaves groups per block
+// 16 groups of 64 per chunk, kGWaves groups per block
 // and the single-query kernel over a fixed grid (SE3ICP_NN_SINGLE_BLOCKS x 4 waves)
 void launch_nn_se3(const View& v, hipStream_t s) {
-    hipLaunchKernelGGL(k_nn_group<12>, dim3(v.nchunks * (kChunkQ / 64) * SE3ICP_NN_SPLIT / kWaves), dim3(64 * kWaves), 0,
+    hipLaunchKernelGGL(k_nn_group<12>, dim3(v.nchunks * (kChunkQ / 64) * SE3ICP_NN_SPLIT / kGWaves), dim3(64 * kGWaves), 0,
                        s, v);
     hipLaunchKernelGGL(k_nn_single<12>, dim3(SE3ICP_NN_SINGLE_BLOCKS), dim3(256), 0, s, v);
 }
 void launch_nn_r3(const View& v, hipStream_t s) {
-    hipLaunchKernelGGL(k_nn_group<3>, dim3(v.nchunks * (kChunkQ / 64) / kWaves), dim3(64 * kWaves), 0, s, v);
+    hipLaunchKernelGGL(k_nn_group<3>, dim3(v.nchunks * (kChunkQ / 64) / kGWaves), dim3(64 * kGWaves), 0, s, v);
     hipLaunchKernelGGL(k_nn_single<3>, dim3(SE3ICP_NN_SINGLE_BLOCKS), dim3(256), 0, s, v);
 }
 
