@@ -20,7 +20,7 @@ namespace se3icp {
 constexpr int kSmallK = 128;      // neighbourhoods the LDS kNN kernels hold; larger ones: k_knn_big.hip
 constexpr int kBlock = 256;       // threads per block of the streaming/sweep kernels
 constexpr int kRedVals = 28;      // 21 JTJ upper + 6 JTr + 1 mse-sum (pt2pt reuses the slots)
-constexpr int kStatCols = 12;     // columns of the device work-counter table (View::stats); 8..11: SE3ICP_PROF section cycles
+constexpr int kStatCols = 15;     // columns of the device work-counter table (View::stats); 8..14: SE3ICP_PROF section cycles
 constexpr int kHist = 256;        // pose history ring of the loop (View::hist), iterations
 constexpr int kTrimList = 4096;   // k_trim: LDS key list / window capacity per pair
 constexpr int kTrimBlocks = 32;   // k_trim_window: blocks per pair

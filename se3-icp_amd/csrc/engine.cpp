@@ -740,20 +740,24 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
                          it, sum[5] - trace_prev_[5], sum[4] - trace_prev_[4], sum[0] - trace_prev_[0],
                          sum[1] - trace_prev_[1], sum[7] - trace_prev_[7], sum[6] - trace_prev_[6],
                          sum[2] - trace_prev_[2], sum[3] - trace_prev_[3], ms[0], ms[1], ms[2], ms[3]);
-            for (int k = 0; k < kStatCols; ++k) trace_prev_[k] = sum[k];
 #ifdef SE3ICP_PROF
             {
-                // waves and summed wave time of this iteration's SE(3) group waves (column 11:
-                // (1 << 44) + dt per wave, integer sums over the slots)
-                static unsigned long long prev11 = 0;
-                unsigned long long s11 = 0;
-                for (int i = 0; i < kStatSlots; ++i) s11 += stats[kStatCols * i + 11];
-                const unsigned long long d = s11 - prev11;
-                prev11 = s11;
-                const unsigned long long nw = d >> 44, dt = d & ((1ull << 44) - 1);
-                std::fprintf(stderr, "[nn] iter %d: %llu SE(3) group waves, mean %.1f us, summed %.1f ms (100 MHz clock)\n",
-                             it, nw, nw ? (double)dt / nw / 100.0 : 0.0, (double)dt / 1e5);
+                // this iteration's SE(3) group waves: count and summed duration (column 11:
+                // (1 << 44) + dt per wave, 100 MHz clock), shader cycles in leaf visits (12),
+                // in their target loads (14) and in the whole wave (13)
+                double d[kStatCols];
+                for (int k = 0; k < kStatCols; ++k) d[k] = sum[k] - trace_prev_[k];
+                const double nw = std::floor(d[11] / 17592186044416.0), dt = d[11] - nw * 17592186044416.0;
+                std::fprintf(stderr, "[nn] iter %d: %.0f SE(3) group waves, mean %.1f us, summed %.1f ms (100 MHz clock)\n",
+                             it, nw, nw > 0 ? dt / nw / 100.0 : 0.0, dt / 1e5);
+                std::fprintf(stderr, "[nn] iter %d: wave cycles in leaf visits %.1f %% (target loads %.1f %%), "
+                             "%.0f cycles per leaf visit, %.0f per box-test step\n", it, 100.0 * d[12] / std::max(1.0, d[13]),
+                             100.0 * d[14] / std::max(1.0, d[13]), d[12] / std::max(1.0, d[9]),
+                             (d[13] - d[12]) / std::max(1.0, d[1] / 128.0));
             }
+#endif
+            for (int k = 0; k < kStatCols; ++k) trace_prev_[k] = sum[k];
+#ifdef SE3ICP_PROF
             std::fprintf(stderr, "[nn] iter %d: longest SE(3) group wave %.1f us (%llu box-test steps, %llu leaf visits, "
                          "%llu queries)\n", it, (double)(stats[10] >> 40) / 100.0, (stats[10] >> 20) & 0xfffffull,
                          (stats[10] >> 6) & 0x3fffull, stats[10] & 63ull);

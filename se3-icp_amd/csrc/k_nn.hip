@@ -88,6 +88,36 @@ __device__ __forceinline__ float box_lb12(const float* lo, const float* hi, cons
     return s2.x + s2.y;
 }
 
+// box_lb12 for a wave-uniform box (the group walk's nodes): read through the constant
+// address space, so the two 48-byte corners come in as scalar loads -- no vector-memory
+// address processing for 64 identical addresses, and the scalar cache's latency
+typedef const __attribute__((address_space(4))) float cfloat;
+__device__ __forceinline__ float box_lb12_u(const float* lo_, const float* hi_, const f32x2* q2) {
+    cfloat* lo = (cfloat*)lo_;
+    cfloat* hi = (cfloat*)hi_;
+    f32x2 s2;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+        const f32x2 a = f32x2{lo[2 * r], lo[2 * r + 1]} - q2[r];
+        const f32x2 b = q2[r] - f32x2{hi[2 * r], hi[2 * r + 1]};
+        const f32x2 e = f32x2{fmaxf(fmaxf(a.x, b.x), 0.f), fmaxf(fmaxf(a.y, b.y), 0.f)};
+        s2 = (r == 0) ? e * e : __builtin_elementwise_fma(e, e, s2);
+    }
+    return s2.x + s2.y;
+}
+template <int D>
+__device__ __forceinline__ float box_lb_u(const float* lo_, const float* hi_, const float* q) {
+    cfloat* lo = (cfloat*)lo_;
+    cfloat* hi = (cfloat*)hi_;
+    float s = 0.f;
+#pragma unroll
+    for (int r = 0; r < D; ++r) {
+        const float e = fmaxf(fmaxf(lo[r] - q[r], q[r] - hi[r]), 0.f);
+        s = fmaf(e, e, s);
+    }
+    return s;
+}
+
 // f32 squared 12-D distance of a query (dimension pairs) to a staged target: two
 // interleaved FMA chains (even / odd dimensions) and one add, within the D-term chain
 // bound f32_err assumes
@@ -683,6 +713,8 @@ __global__ __launch_bounds__(64 * kGWaves) __attribute__((amdgpu_waves_per_eu(SE
     unsigned n_leaf = 0;             // leaves swept (the chunk cost)
 #ifdef SE3ICP_PROF
     unsigned n_want = 0, n_leafv = 0;
+    unsigned long long c_leaf = 0, c_lload = 0;  // shader-clock cycles in leaf visits / their target loads
+    const unsigned long long c_w0 = __builtin_amdgcn_s_memtime();
     const unsigned n_valid = (unsigned)__popcll(__ballot(valid));
     const unsigned long long t_w0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -729,8 +761,8 @@ __global__ __launch_bounds__(64 * kGWaves) __attribute__((amdgpu_waves_per_eu(SE
             int w = 64;
             if (D == 12 || SE3ICP_NN_COMPACT3) {
                 float lbh;
-                if constexpr (D == 12) lbh = box_lb12(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q2);
-                else lbh = box_lb<D>(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q);
+                if constexpr (D == 12) lbh = box_lb12_u(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q2);
+                else lbh = box_lb_u<D>(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q);
                 W = __ballot(lbh * (1.f - 2e-6f) < thr);
                 if (W == 0ull) continue;
                 w = __popcll(W);
@@ -739,6 +771,7 @@ __global__ __launch_bounds__(64 * kGWaves) __attribute__((amdgpu_waves_per_eu(SE
 #ifdef SE3ICP_PROF
             n_want += __popcll(W & __ballot(valid));
             ++n_leafv;
+            const unsigned long long c_l0 = __builtin_amdgcn_s_memtime();
 #endif
             __builtin_amdgcn_wave_barrier();
             if (lane < cnt) {
@@ -749,6 +782,11 @@ __global__ __launch_bounds__(64 * kGWaves) __attribute__((amdgpu_waves_per_eu(SE
                 for (int k = 0; k < NV; ++k) tile[lane * NV + k] = make_float4(e[4 * k], e[4 * k + 1], e[4 * k + 2], e[4 * k + 3]);
             }
             __builtin_amdgcn_wave_barrier();
+#ifdef SE3ICP_PROF
+            __builtin_amdgcn_s_waitcnt(0);
+            const unsigned long long c_l1 = __builtin_amdgcn_s_memtime();
+            c_lload += c_l1 - c_l0;
+#endif
             if (w > (D == 12 ? SE3ICP_NN_COMPACT : SE3ICP_NN_COMPACT3)) {
                 // every lane sweeps every target (broadcast LDS reads)
                 for (int j = 0; j < cnt; ++j) {
@@ -793,6 +831,9 @@ __global__ __launch_bounds__(64 * kGWaves) __attribute__((amdgpu_waves_per_eu(SE
                 }
             }
             if ((int)valid & (int)(d1 < INFINITY)) thr = fminf(thr, widen(d1, d2));
+#ifdef SE3ICP_PROF
+            c_leaf += __builtin_amdgcn_s_memtime() - c_l0;
+#endif
             continue;
         }
 #if SE3ICP_NN_TWOLEVEL
@@ -807,8 +848,8 @@ __global__ __launch_bounds__(64 * kGWaves) __attribute__((amdgpu_waves_per_eu(SE
             float lg[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                if constexpr (D == 12) lg[k] = box_lb12(box_lo + (size_t)(g0 + k) * D, box_hi + (size_t)(g0 + k) * D, q2);
-                else lg[k] = box_lb<D>(box_lo + (size_t)(g0 + k) * D, box_hi + (size_t)(g0 + k) * D, q);
+                if constexpr (D == 12) lg[k] = box_lb12_u(box_lo + (size_t)(g0 + k) * D, box_hi + (size_t)(g0 + k) * D, q2);
+                else lg[k] = box_lb_u<D>(box_lo + (size_t)(g0 + k) * D, box_hi + (size_t)(g0 + k) * D, q);
             }
             bool vg[4];
 #pragma unroll
@@ -834,11 +875,11 @@ __global__ __launch_bounds__(64 * kGWaves) __attribute__((amdgpu_waves_per_eu(SE
         const int hl = 2 * h + 1, hr = 2 * h + 2;
         float ll, lr;
         if constexpr (D == 12) {
-            ll = box_lb12(box_lo + (size_t)hl * D, box_hi + (size_t)hl * D, q2);
-            lr = box_lb12(box_lo + (size_t)hr * D, box_hi + (size_t)hr * D, q2);
+            ll = box_lb12_u(box_lo + (size_t)hl * D, box_hi + (size_t)hl * D, q2);
+            lr = box_lb12_u(box_lo + (size_t)hr * D, box_hi + (size_t)hr * D, q2);
         } else {
-            ll = box_lb<D>(box_lo + (size_t)hl * D, box_hi + (size_t)hl * D, q);
-            lr = box_lb<D>(box_lo + (size_t)hr * D, box_hi + (size_t)hr * D, q);
+            ll = box_lb_u<D>(box_lo + (size_t)hl * D, box_hi + (size_t)hl * D, q);
+            lr = box_lb_u<D>(box_lo + (size_t)hr * D, box_hi + (size_t)hr * D, q);
         }
         // the f32 bound is within (D+2) ulps of the exact distance to the (inflated) box
         const bool vl = __ballot(ll * (1.f - 2e-6f) < thr) != 0ull;
@@ -866,6 +907,9 @@ __global__ __launch_bounds__(64 * kGWaves) __attribute__((amdgpu_waves_per_eu(SE
                                         ((unsigned long long)min(n_leafv, 0x3fffu) << 6) | (n_valid % 64u));
             atomicAdd(v.stats + kStatCols + 10, dt * dt);                      // (spread)
             atomicAdd(v.stats + kStatCols * (gi & 63) + 11, (1ull << 44) + dt);  // waves, wave time
+            atomicAdd(v.stats + kStatCols * (gi & 63) + 12, c_leaf);   // shader cycles in leaf visits,
+            atomicAdd(v.stats + kStatCols * (gi & 63) + 14, c_lload);  // in their target loads,
+            atomicAdd(v.stats + kStatCols * (gi & 63) + 13, __builtin_amdgcn_s_memtime() - c_w0);  // in the wave
         }
 #endif
     }
@@ -933,8 +977,8 @@ __device__ __forceinline__ void single_one(const View& v, const PairDev* P, int 
     const float* box_lo = TR.lo + (size_t)P->tgt * TR.nnodes * D;
     const float* box_hi = TR.hi + (size_t)P->tgt * TR.nnodes * D;
     auto lbound = [&](int h) __attribute__((always_inline)) {
-        if constexpr (D == 12) return box_lb12(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q2);
-        else return box_lb<D>(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q);
+        if constexpr (D == 12) return box_lb12_u(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q2);
+        else return box_lb_u<D>(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q);
     };
     const int L = TR.L;
     const int sh = L > 6 ? 6 : L;
