@@ -32,17 +32,21 @@ __device__ __forceinline__ float ord_float(uint32_t u) {
     return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
 }
 
-__global__ __launch_bounds__(256) void k_tree_init(TreeView t, int32_t* perm2) {
+// identity permutations; the sampled-box scratch of the first `box_nodes` heap nodes of
+// every cloud (the levels k_tree_bbox serves) cleared
+__global__ __launch_bounds__(256) void k_tree_init(TreeView t, int32_t* perm2, int box_nodes) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g < t.npts) {
         const CloudDev cl = t.clouds[t.cloud_of[g]];
         t.perm[g] = g - cl.off;
         perm2[g] = g - cl.off;  // (both buffers hold valid point indices at all times)
     }
-    const size_t nb = (size_t)t.nclouds * t.nnodes * t.D;
+    const int per = box_nodes * t.D;
+    const size_t nb = (size_t)t.nclouds * per;
     for (size_t i = g; i < nb; i += (size_t)gridDim.x * blockDim.x) {
-        t.blo[i] = 0xffffffffu;
-        t.bhi[i] = 0u;
+        const size_t at = (i / per) * ((size_t)t.nnodes * t.D) + i % per;
+        t.blo[at] = 0xffffffffu;
+        t.bhi[at] = 0u;
     }
 }
 
@@ -160,9 +164,8 @@ __global__ __launch_bounds__(256) void k_tree_bbox(TreeView t, int level) {
 //   scatter each point's rank among its node's points of the same class -> its new position
 // Ties keep their tree order, so the build is deterministic.
 constexpr int kPartBits = 11, kPartBins = 1 << kPartBits;  // bins per pass; keys of 2 * kPartBits bits
-#ifndef SE3ICP_TREE_GSPLIT
-#define SE3ICP_TREE_GSPLIT 0  // global levels' split dimension: 0 widest sampled extent, 1 largest sample variance (A/B: SE(3) NN +9 %, setup +0.2 ms)
-#endif
+// (split dimension: the widest sampled extent; the largest sample variance, as the LDS
+// levels use, measured +9 % SE(3) NN time at the global levels)
 constexpr int kPartThreads = 256, kPartPer = 4, kPartElems = kPartThreads * kPartPer;
 constexpr int kSelThreads = 1024, kSelPer = kPartBins / kSelThreads;
 constexpr int kHistPer = 8, kHistElems = kPartThreads * kHistPer;  // tree positions per histogram block
@@ -199,117 +202,6 @@ __device__ __forceinline__ PartDim part_dim_of(const uint32_t* blo, const uint32
     return r;
 }
 
-#if SE3ICP_TREE_GSPLIT == 1
-// Split dimension of the global levels by the largest sample variance, as the LDS levels
-// (k_tree_local) choose theirs: every kSplitSample-th point's coordinates, quantised to
-// kMomBits bits over its cloud's root box, summed in 64-bit integers (order-independent
-// atomics: the tree stays deterministic).  Per node: count, then (sum, sum of squares) per
-// dimension.
-constexpr int kMomBits = 20;
-struct PartRoot {
-    float lo[12], s[12];  // q = (x - lo) * s in [0, 2^kMomBits)
-};
-__global__ __launch_bounds__(64) void k_part_root(TreeView t, PartRoot* root) {
-    const int c = blockIdx.x * 64 + threadIdx.x;
-    if (c >= t.nclouds) return;
-    const size_t base = (size_t)c * t.nnodes * t.D;  // the root's sampled box (k_tree_bbox, level 0)
-    PartRoot r;
-    for (int d = 0; d < 12; ++d) { r.lo[d] = 0.f; r.s[d] = 0.f; }
-    for (int d = 0; d < t.D; ++d) {
-        const float lo = ord_float(t.blo[base + d]), ext = ord_float(t.bhi[base + d]) - lo;
-        r.lo[d] = lo;
-        r.s[d] = (ext > 0.f && ext < INFINITY) ? (float)((1 << kMomBits) - 1) / ext : 0.f;
-    }
-    root[c] = r;
-}
-
-template <int D>
-__global__ __launch_bounds__(256) void k_part_moments(TreeView t, int level, const PartRoot* root,
-                                                      unsigned long long* mom) {
-    const int g = (blockIdx.x * blockDim.x + threadIdx.x) * kSplitSample;
-    const int lane = threadIdx.x & 63;
-    const bool valid = g < t.npts;
-    int c = -1, node = -1;
-    unsigned long long s1[D], s2[D];
-    if (valid) {
-        c = t.cloud_of[g];
-        const CloudDev cl = t.clouds[c];
-        node = tree_node_of(g - cl.off, cl.n, level);
-        const int pt = cl.off + t.perm[g];
-        const PartRoot& r = root[c];
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            float qf = (t.vec[tree_in_ix(t, d, pt)] - r.lo[d]) * r.s[d];
-            qf = fminf(fmaxf(qf, 0.f), (float)((1 << kMomBits) - 1));  // NaN -> 0
-            const unsigned long long q = (unsigned)qf;
-            s1[d] = q;
-            s2[d] = q * q;
-        }
-    } else {
-#pragma unroll
-        for (int d = 0; d < D; ++d) { s1[d] = 0ull; s2[d] = 0ull; }
-    }
-    unsigned cnt = valid ? 1u : 0u;
-    const long long key = valid ? ((long long)c << 32) | (unsigned)node : -1;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const long long ok = __shfl_down(key, o, 64);
-        const bool same = (lane + o < 64) && ok == key;
-        const unsigned oc = __shfl_down(cnt, o, 64);
-        if (same) cnt += oc;
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            const unsigned long long a = __shfl_down(s1[d], o, 64), b = __shfl_down(s2[d], o, 64);
-            if (same) { s1[d] += a; s2[d] += b; }
-        }
-    }
-    const long long prev = __shfl_up(key, 1, 64);
-    const bool head = valid && (lane == 0 || prev != key);
-    if (head) {
-        unsigned long long* m = mom + (size_t)((c << level) + node) * (1 + 2 * D);
-        atomicAdd(m, (unsigned long long)cnt);
-#pragma unroll
-        for (int d = 0; d < D; ++d) {
-            atomicAdd(m + 1 + 2 * d, s1[d]);
-            atomicAdd(m + 2 + 2 * d, s2[d]);
-        }
-    }
-}
-
-// every node's split: the dimension of largest variance; the key quantises that
-// coordinate over mean +- 8 sd (points beyond clamp to the end bins).  Clears the moments.
-__global__ __launch_bounds__(64) void k_part_dims(TreeView t, int level, const PartRoot* root, unsigned long long* mom,
-                                                  PartDim* dims) {
-    const int id = blockIdx.x * 64 + threadIdx.x;
-    if (id >= (t.nclouds << level)) return;
-    const int c = id >> level;
-    const int D = t.D;
-    unsigned long long* m = mom + (size_t)id * (1 + 2 * D);
-    const PartRoot& r = root[c];
-    const double n = (double)m[0];
-    int best = 0;
-    double bvar = -1.0, bmean = 0.0;
-    for (int d = 0; d < D; ++d) {
-        double var = 0.0, mean = 0.0;
-        if (n > 0.0 && r.s[d] > 0.f) {
-            const double mq = (double)m[1 + 2 * d] / n;
-            const double vq = fmax((double)m[2 + 2 * d] / n - mq * mq, 0.0);
-            const double inv = 1.0 / (double)r.s[d];
-            var = vq * inv * inv;
-            mean = (double)r.lo[d] + mq * inv;
-        }
-        if (var > bvar) { bvar = var; best = d; bmean = mean; }
-    }
-    for (int k = 0; k < 1 + 2 * D; ++k) m[k] = 0ull;
-    const double sd = sqrt(bvar);
-    PartDim pd;
-    pd.best = best;
-    pd.lo = (float)(bmean - 8.0 * sd);
-    pd.scale = (sd > 0.0 && sd < 1e30) ? (float)((double)kKeyMax / (16.0 * sd)) : 0.f;
-    pd.pad = 0;
-    dims[id] = pd;
-}
-#else
 // every node's split from its sampled box (k_tree_bbox); once per node, not per point
 __global__ __launch_bounds__(64) void k_part_dims(TreeView t, int level, PartDim* dims) {
     const int id = blockIdx.x * 64 + threadIdx.x;
@@ -318,7 +210,6 @@ __global__ __launch_bounds__(64) void k_part_dims(TreeView t, int level, PartDim
     const size_t base = ((size_t)c * t.nnodes + tree_heap(level, node)) * t.D;
     dims[id] = part_dim_of(t.blo + base, t.bhi + base, t.D);
 }
-#endif
 
 // node ids (cloud << level | node) grow with the tree position
 __device__ __forceinline__ int part_node_id(int c, int level, int node) { return (c << level) + node; }
@@ -328,20 +219,16 @@ __device__ __forceinline__ int part_node_id_at(const TreeView& t, int level, int
     return part_node_id(c, level, tree_node_of(g - cl.off, cl.n, level));
 }
 
-#ifndef SE3ICP_TREE_HIST_ATOMIC
-#define SE3ICP_TREE_HIST_ATOMIC 1  // block histograms added into per-node histograms (0: written whole, summed by k_part_select)
-#endif
 // Per block of kHistElems tree positions: the histograms of the (at most) two nodes the
 // block starts in, in LDS, written out whole (dense[block][2][bins]); points of further
 // nodes (small clouds) go to the per-node overflow histograms by global atomics.
 __global__ __launch_bounds__(kPartThreads) void k_part_hist(TreeView t, int level, const PartDim* dims, uint32_t* q_out,
-                                                           uint32_t* dense, int32_t* block_id0, uint32_t* overflow) {
+                                                           uint32_t* overflow) {
     __shared__ uint32_t s_h[2 * kPartBins];
     const int tid = threadIdx.x;
     for (int i = tid; i < 2 * kPartBins; i += kPartThreads) s_h[i] = 0u;
     const int g0 = blockIdx.x * kHistElems;
     const int id0 = part_node_id_at(t, level, g0);
-    if (tid == 0) block_id0[blockIdx.x] = id0;
     __syncthreads();
 #pragma unroll 4
     for (int u = 0; u < kHistPer; ++u) {
@@ -363,29 +250,23 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(TreeView t, int leve
         }
     }
     __syncthreads();
-#if SE3ICP_TREE_HIST_ATOMIC
     // the block's two node histograms added into the per-node histograms (its non-zero bins;
     // integer adds: the order does not matter), so k_part_select reads one histogram per node
     for (int i = tid; i < 2 * kPartBins; i += kPartThreads) {
         const uint32_t x = s_h[i];
         if (x) atomicAdd(&overflow[(size_t)(id0 + i / kPartBins) * kPartBins + (i & (kPartBins - 1))], x);
     }
-#else
-    uint32_t* out = dense + (size_t)blockIdx.x * 2 * kPartBins;
-    for (int i = tid; i < 2 * kPartBins; i += kPartThreads) out[i] = s_h[i];
-#endif
 }
 
-// one workgroup per node of the level: its histogram (the blocks' dense slots + overflow),
+// one workgroup per node of the level: its histogram (summed by k_part_hist's atomics),
 // the median bin; the overflow histogram is cleared for the next level
-__global__ __launch_bounds__(kSelThreads) void k_part_select(TreeView t, int level, const uint32_t* dense,
-                                                            const int32_t* block_id0, uint32_t* overflow, PartSel* sel) {
+__global__ __launch_bounds__(kSelThreads) void k_part_select(TreeView t, int level, uint32_t* overflow, PartSel* sel) {
     __shared__ uint32_t s_sum[kSelThreads];
     const int nl = 1 << level;
     const int id = blockIdx.x;
     const int c = id >> level, node = id & (nl - 1);
     const CloudDev cl = t.clouds[c];
-    const int a = tree_first(cl.n, level, node), b = tree_first(cl.n, level, node + 1);
+    const int a = tree_first(cl.n, level, node);
     const int mL = tree_first(cl.n, level + 1, 2 * node + 1) - a;
     const int tid = threadIdx.x;
     uint32_t v[kSelPer];
@@ -394,18 +275,6 @@ __global__ __launch_bounds__(kSelThreads) void k_part_select(TreeView t, int lev
     for (int k = 0; k < kSelPer; ++k) {
         v[k] = ov[tid * kSelPer + k];
         ov[tid * kSelPer + k] = 0u;
-    }
-    if ((int)!SE3ICP_TREE_HIST_ATOMIC & (int)(b > a)) {
-        const int kb0 = (cl.off + a) / kHistElems, kb1 = (cl.off + b - 1) / kHistElems;
-#pragma unroll 8
-        for (int kb = kb0; kb <= kb1; ++kb) {
-            const int slot = id - block_id0[kb];
-            if ((unsigned)slot < 2u) {
-                const uint32_t* h = dense + ((size_t)kb * 2 + slot) * kPartBins;
-#pragma unroll
-                for (int k = 0; k < kSelPer; ++k) v[k] += h[tid * kSelPer + k];
-            }
-        }
     }
     uint32_t tot = 0;
 #pragma unroll
@@ -616,6 +485,248 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(TreeView t, int l
     }
 }
 
+// ---- global levels, one launch per level: a workgroup per node of the level computes
+// the same split as the passes above (the sampled box of every kSplitSample-th global tree
+// position, the 22-bit key over its widest extent, the median by two 11-bit histograms,
+// the stable left / tie / right partition), with LDS histograms and one block scan instead
+// of device-wide passes.  A node's points are read as wave-contiguous 64-position chunks.
+#ifndef SE3ICP_TREE_WG_MIN
+#define SE3ICP_TREE_WG_MIN 64  // levels with at least this many nodes (over all clouds) use k_tree_level
+#endif
+constexpr int kLevThreads = 1024, kLevWaves = kLevThreads / 64;
+constexpr int kLevU = 16;  // loads in flight per thread in the passes over a node
+
+// block-wide exclusive scan of one u32 per thread (kLevThreads): returns the exclusive
+// prefix, *total the block's sum (two barriers)
+__device__ __forceinline__ uint32_t lev_scan(uint32_t x, uint32_t* s_w, uint32_t* total) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t inc = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) s_w[wv] = inc;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kLevWaves; ++w) {
+        const uint32_t v = s_w[w];
+        pre += w < wv ? v : 0u;
+        tot += v;
+    }
+    __syncthreads();
+    *total = tot;
+    return pre + inc - x;
+}
+
+// the bin (2 per thread) where the cumulative count reaches `want` (bin 0 when want = 0),
+// as k_part_select / k_part_select2 choose it; the thread that owns it writes
+// (bin, want - count before it, its count).  The thread's bins are cleared for the next pass.
+__device__ __forceinline__ void lev_select(uint32_t* s_h, uint32_t* s_w, int* s_sel, int want, int shift_prev) {
+    const int tid = threadIdx.x;
+    const uint32_t v0 = s_h[2 * tid], v1 = s_h[2 * tid + 1];
+    uint32_t tot;
+    const uint32_t cum = lev_scan(v0 + v1, s_w, &tot);
+    s_h[2 * tid] = 0u;
+    s_h[2 * tid + 1] = 0u;
+    const uint32_t w = (uint32_t)want;
+    const uint32_t c1 = cum + v0;
+    const int pick = ((int)(cum < w) & (int)(c1 >= w)) | ((int)(want == 0) & (int)(tid == 0)) ? 0
+                     : ((int)(c1 < w) & (int)(c1 + v1 >= w)) ? 1 : -1;
+    if (pick >= 0) {
+        const int bin = 2 * tid + pick;
+        s_sel[0] = shift_prev >= 0 ? (shift_prev << kPartBits) | bin : bin;
+        s_sel[1] = want - (int)(pick ? c1 : cum);
+        s_sel[2] = (int)(pick ? v1 : v0);
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(kLevThreads) void k_tree_level(TreeView t, int level, const int32_t* __restrict__ perm_in,
+                                                            int32_t* __restrict__ perm_out, uint32_t* __restrict__ qbuf) {
+    __shared__ uint32_t s_h[kPartBins];
+    __shared__ uint32_t s_lo[D], s_hi[D];
+    __shared__ uint32_t s_w[kLevWaves];
+    __shared__ int s_sel[3];
+    __shared__ uint32_t s_cnt[kLevWaves][2];
+    const int c = blockIdx.x >> level, node = blockIdx.x & ((1 << level) - 1);
+    const CloudDev cl = t.clouds[c];
+    const int n = cl.n;
+    const int a = tree_first(n, level, node), m = tree_first(n, level, node + 1) - a;
+    const int mL = tree_first(n, level + 1, 2 * node + 1) - a;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    if (m <= 0) return;  // (block-uniform)
+#ifdef SE3ICP_PROF
+    unsigned long long tp[6];
+    tp[0] = __builtin_amdgcn_s_memtime();
+#define LEV_T(i) tp[i] = __builtin_amdgcn_s_memtime()
+#else
+#define LEV_T(i)
+#endif
+    const int base = cl.off + a;  // global tree position of the node's first point
+    for (int i = tid; i < kPartBins; i += kLevThreads) s_h[i] = 0u;
+    if (tid < D) {
+        s_lo[tid] = 0xffffffffu;
+        s_hi[tid] = 0u;
+    }
+    // 1. the box of the samples: global tree positions that are multiples of kSplitSample
+    {
+        uint32_t lo[D], hi[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) { lo[d] = 0xffffffffu; hi[d] = 0u; }
+        const int e0 = (kSplitSample - base % kSplitSample) % kSplitSample;
+        constexpr int U1 = D == 12 ? 4 : 8;  // samples in flight per thread
+#pragma clang loop unroll(disable) vectorize(disable)
+        for (int e1 = e0 + tid * kSplitSample; e1 < m; e1 += U1 * kLevThreads * kSplitSample) {
+            int pp[U1];
+#pragma unroll
+            for (int u = 0; u < U1; ++u) {
+                const int e = e1 + u * kLevThreads * kSplitSample;
+                pp[u] = e < m ? cl.off + perm_in[base + e] : -1;
+            }
+            float x[U1][D];
+#pragma unroll
+            for (int u = 0; u < U1; ++u)
+#pragma unroll
+                for (int d = 0; d < D; ++d) x[u][d] = t.vec[tree_in_ix(t, d, pp[u] < 0 ? cl.off : pp[u])];
+#pragma unroll
+            for (int u = 0; u < U1; ++u)
+                if (pp[u] >= 0) {
+#pragma unroll
+                    for (int d = 0; d < D; ++d) {
+                        const uint32_t o = ord_bits(x[u][d]);
+                        lo[d] = min(lo[d], o);
+                        hi[d] = max(hi[d], o);
+                    }
+                }
+        }
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                lo[d] = min(lo[d], xor_lane(lo[d], o));
+                hi[d] = max(hi[d], xor_lane(hi[d], o));
+            }
+        }
+        __syncthreads();  // (s_lo / s_hi initialised)
+        if (lane == 0) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                atomicMin(&s_lo[d], lo[d]);
+                atomicMax(&s_hi[d], hi[d]);
+            }
+        }
+        __syncthreads();
+    }
+    LEV_T(1);
+    const PartDim pd = part_dim_of(s_lo, s_hi, D);
+    // 2. keys (kept in qbuf) and the coarse histogram; kLevU independent loads in flight
+    // per thread (the node is read by latency-bound chains otherwise)
+#pragma unroll 1
+    for (int e0 = tid; e0 < m; e0 += kLevU * kLevThreads) {
+        int pp[kLevU];
+        float x[kLevU];
+#pragma unroll
+        for (int u = 0; u < kLevU; ++u) {
+            const int e = e0 + u * kLevThreads;
+            pp[u] = e < m ? perm_in[base + e] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kLevU; ++u) x[u] = t.vec[tree_in_ix(t, pd.best, cl.off + pp[u])];
+#pragma unroll
+        for (int u = 0; u < kLevU; ++u) {
+            const int e = e0 + u * kLevThreads;
+            float qf = (x[u] - pd.lo) * pd.scale;
+            qf = fminf(fmaxf(qf, 0.f), kKeyMax);  // NaN -> 0
+            const uint32_t key = (uint32_t)qf;
+            if (e < m) {
+                qbuf[base + e] = key;
+                atomicAdd(&s_h[key >> kPartBits], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    LEV_T(2);
+    lev_select(s_h, s_w, s_sel, mL, -1);
+    __syncthreads();
+    // 3. the fine histogram inside the median bin (each thread re-reads its own keys)
+    const int bin = s_sel[0];
+#pragma unroll 1
+    for (int e0 = tid; e0 < m; e0 += kLevU * kLevThreads) {
+        uint32_t k[kLevU];
+#pragma unroll
+        for (int u = 0; u < kLevU; ++u) {
+            const int e = e0 + u * kLevThreads;
+            k[u] = e < m ? qbuf[base + e] : 0xffffffffu;
+        }
+#pragma unroll
+        for (int u = 0; u < kLevU; ++u)
+            if ((int)(k[u] >> kPartBits) == bin) atomicAdd(&s_h[k[u] & (kPartBins - 1)], 1u);
+    }
+    __syncthreads();
+    LEV_T(3);
+    lev_select(s_h, s_w, s_sel, s_sel[1], bin);
+    __syncthreads();
+    LEV_T(4);
+    const int T = s_sel[0], tl = s_sel[1], tn = s_sel[2];
+    // 4. stable partition: wave w owns the 64-position chunks [w S, (w + 1) S) of the node;
+    // its (left, tie) counts, their prefix over the waves, then every point's rank by ballots
+    const int S = ((m + kLevWaves * 64 - 1) / (kLevWaves * 64)) * 64;
+    const int s0 = wv * S, s1 = min(m, s0 + S);
+    uint32_t nl = 0, nt = 0;
+#pragma unroll 1
+    for (int e0 = s0; e0 < s1; e0 += kLevU * 64) {
+        int q[kLevU];
+#pragma unroll
+        for (int u = 0; u < kLevU; ++u) {
+            const int e = e0 + u * 64 + lane;
+            q[u] = e < s1 ? (int)qbuf[base + e] : 0x7fffffff;
+        }
+#pragma unroll
+        for (int u = 0; u < kLevU; ++u) {
+            nl += __popcll(__ballot(q[u] < T));
+            nt += __popcll(__ballot(q[u] == T));
+        }
+    }
+    if (lane == 0) { s_cnt[wv][0] = nl; s_cnt[wv][1] = nt; }
+    __syncthreads();
+    uint32_t r0 = 0, r1 = 0;
+#pragma unroll 1
+    for (int w = 0; w < wv; ++w) { r0 += s_cnt[w][0]; r1 += s_cnt[w][1]; }
+#pragma unroll 1
+    for (int e0 = s0; e0 < s1; e0 += kLevU * 64) {
+        int q[kLevU], pp[kLevU];
+#pragma unroll
+        for (int u = 0; u < kLevU; ++u) {
+            const int e = e0 + u * 64 + lane;
+            q[u] = e < s1 ? (int)qbuf[base + e] : 0x7fffffff;
+            pp[u] = e < s1 ? perm_in[base + e] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kLevU; ++u) {
+            const int e = e0 + u * 64 + lane;
+            const unsigned long long bl = __ballot(q[u] < T), bt = __ballot(q[u] == T);
+            const int rl = (int)r0 + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bl >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bl, 0u));
+            const int rt = (int)r1 + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bt >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bt, 0u));
+            int dst;
+            if (q[u] < T) dst = rl;
+            else if (q[u] == T) dst = rt < tl ? (mL - tl) + rt : mL + (rt - tl);
+            else dst = mL + (tn - tl) + (e - rl - rt);
+            if ((int)(e < s1) & (int)((unsigned)dst < (unsigned)m)) perm_out[base + dst] = pp[u];  // (always, by construction)
+            r0 += (uint32_t)__popcll(bl);
+            r1 += (uint32_t)__popcll(bt);
+        }
+    }
+#ifdef SE3ICP_PROF
+    LEV_T(5);
+    if ((int)(tid == 0) & (int)(blockIdx.x == 0))
+        printf("[tree] D=%d level %d m=%d: box %llu keys %llu fine %llu select %llu partition %llu cycles\n", D, level, m,
+               tp[1] - tp[0], tp[2] - tp[1], tp[3] - tp[2], tp[4] - tp[3], tp[5] - tp[4]);
+#endif
+#undef LEV_T
+}
+
 // The levels below G in one workgroup per level-G node (<= kLocalMax points): the node's
 // permutation stays in LDS and every level is a bitonic sort of (sub-node, coordinate
 // along the sub-node's widest dimension) keys -- the same median splits as the global
@@ -624,17 +735,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(TreeView t, int l
 #define SE3ICP_LOCAL_MAX 4096
 #endif
 constexpr int kLocalMax = SE3ICP_LOCAL_MAX;  // power of two
-[[maybe_unused]] constexpr int kLocalBits = __builtin_ctz(kLocalMax);  // element field of the block sort keys
 constexpr int kWaveSortPer = 8;  // sub-nodes of <= 512 points: register sort by one wave
-#ifndef SE3ICP_TREE_SPLIT
-#define SE3ICP_TREE_SPLIT 1
-#endif
-#ifndef SE3ICP_TREE_LPART
-#define SE3ICP_TREE_LPART 1  // LDS levels over 512 points: 1 median partition, 0 block bitonic sort
-#endif
-#ifndef SE3ICP_TREE_STRIDE
-#define SE3ICP_TREE_STRIDE 16
-#endif
 constexpr int kLocalThreads = 512;
 
 template <int D>
@@ -663,8 +764,7 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
                 // every 16th point: denser samples measured slower overall (strides 1, 4, 8,
                 // 16, 32, 64 tried) -- the 12-D gathers cost build time and did not buy
                 // better trees
-                const int stride = SE3ICP_TREE_STRIDE;
-#if SE3ICP_TREE_SPLIT == 1
+                constexpr int stride = 16;
                 // widest spread: the dimension of largest sample variance
                 float s1[D], s2[D];
 #pragma unroll
@@ -696,33 +796,6 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
                     const float e = b * inv - mu * mu;
                     if (e > ext) { ext = e; best = d; if (lane == 0) { s_mu[k] = mu; s_sd[k] = sqrtf(fmaxf(e, 0.f)); } }
                 }
-#else
-                float lo[D], hi[D];
-#pragma unroll
-                for (int d = 0; d < D; ++d) { lo[d] = INFINITY; hi[d] = -INFINITY; }
-                for (int e = a0 + lane * stride; e < a1; e += 64 * stride) {
-                    const int p = s_val[e];
-#pragma unroll
-                    for (int d = 0; d < D; ++d) {
-                        const float x = t.vec[tree_in_ix(t, d, cl.off + p)];
-                        lo[d] = fminf(lo[d], x);
-                        hi[d] = fmaxf(hi[d], x);
-                    }
-                }
-                int best = 0;
-                float ext = -1.f;
-#pragma unroll 1  // (a full unroll here crashes amdgcn instruction selection in ROCm 7.2)
-                for (int d = 0; d < D; ++d) {
-                    float l0 = lo[d], h0 = hi[d];
-#pragma unroll
-                    for (int o = 32; o >= 1; o >>= 1) {
-                        l0 = fminf(l0, __shfl_xor(l0, o, 64));
-                        h0 = fmaxf(h0, __shfl_xor(h0, o, 64));
-                    }
-                    const float e = h0 - l0;
-                    if (e > ext) { ext = e; best = d; }
-                }
-#endif
                 if (lane == 0) s_best[k] = best;
             }
         }
@@ -761,7 +834,6 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
             __syncthreads();
             continue;
         }
-#if SE3ICP_TREE_LPART && SE3ICP_TREE_SPLIT == 1
         // large sub-nodes (<= 4 of them): a stable median partition in LDS, as the global
         // levels do -- the split coordinate quantised to 22 bits over the sub-node's sample
         // mean +- 8 sd, the median bin by two 11-bit histogram passes, then each point's
@@ -900,45 +972,6 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
                 if ((unsigned)dst[u] < (unsigned)m) s_val[dst[u]] = val[u];
             __syncthreads();
         }
-#else
-        // large sub-nodes: block-wide bitonic sort of (sub-node, coordinate, element) keys
-        // (7 + 32 + log2(kLocalMax) bits), kLocalMax / 512 per thread in registers; only the stages with partners
-        // in another wave go through LDS
-        {
-            constexpr int PER = kLocalMax / kLocalThreads;
-            unsigned long long k[PER];
-#pragma unroll
-            for (int u = 0; u < PER; ++u) {
-                const int e = tid * PER + u;
-                k[u] = ~0ull;
-                if (e < m) {
-                    const int sub = tree_node_of(A + e, n, l) - (i << r);
-                    const uint32_t c = ord_bits(t.vec[tree_in_ix(t, s_best[sub], cl.off + s_val[e])]);
-                    k[u] = ((unsigned long long)(unsigned)sub << (32 + kLocalBits)) | ((unsigned long long)c << kLocalBits) |
-                           (unsigned)e;
-                }
-            }
-            bitonic_net<PER, kLocalMax, 64 * PER>(k, tid, s_key);
-            __syncthreads();
-#pragma unroll
-            for (int u = 0; u < PER; ++u) s_key[tid * PER + u] = k[u];
-            __syncthreads();
-            // gather the permutation through the element field
-            int nv[PER];
-#pragma unroll
-            for (int u = 0; u < PER; ++u) {
-                const int e = tid * PER + u;
-                nv[u] = e < m ? s_val[(int)(s_key[e] & (unsigned long long)(kLocalMax - 1))] : 0;
-            }
-            __syncthreads();
-#pragma unroll
-            for (int u = 0; u < PER; ++u) {
-                const int e = tid * PER + u;
-                if (e < m) s_val[e] = nv[u];
-            }
-            __syncthreads();
-        }
-#endif
     }
     for (int e = tid; e < m; e += kLocalThreads) t.perm[cl.off + A + e] = s_val[e];
 }
@@ -1042,13 +1075,9 @@ int tree_global_levels(int max_n, int L) {
 
 namespace {
 struct PartScratch {
-    uint32_t* dense;
-    int32_t* block_id0;
-    uint32_t* overflow;
+    uint32_t* overflow;  // per node of the multi-pass levels: histogram (coarse, then fine)
     PartSel* sel;
-    PartDim* dims[1];
-    void* root;               // PartRoot per cloud (variance splits)
-    unsigned long long* mom;  // per node: count, (sum, sum of squares) per dimension
+    PartDim* dims;
     SegCnt* tails;
     SegCnt* carry;
     size_t overflow_words;
@@ -1056,30 +1085,21 @@ struct PartScratch {
 size_t part_layout(int npts, int nclouds, int G, char* base, PartScratch* ps) {
     const size_t nodes = G > 0 ? (size_t)nclouds << (G - 1) : 0;
     const size_t nblk = ((size_t)npts + kPartElems - 1) / kPartElems;
-    const size_t nhist = ((size_t)npts + kHistElems - 1) / kHistElems;
     size_t off = 0;
     auto take = [&](size_t bytes) {
         const size_t at = off;
         off += (bytes + 255) & ~(size_t)255;
         return base ? base + at : nullptr;
     };
-    char* dn = take(G > 0 ? nhist * 2 * kPartBins * sizeof(uint32_t) : 0);
-    char* b0 = take(nhist * sizeof(int32_t));
     char* ov = take(nodes * kPartBins * sizeof(uint32_t));
     char* sl = take(nodes * sizeof(PartSel));
     char* d0 = take(nodes * sizeof(PartDim));
-    char* rt = take((size_t)nclouds * 96);
-    char* mm = take(nodes * 25 * sizeof(unsigned long long));
     char* tl = take(nblk * sizeof(SegCnt));
     char* cr = take(nblk * sizeof(SegCnt));
     if (ps) {
-        ps->dense = (uint32_t*)dn;
-        ps->block_id0 = (int32_t*)b0;
         ps->overflow = (uint32_t*)ov;
         ps->sel = (PartSel*)sl;
-        ps->dims[0] = (PartDim*)d0;
-        ps->root = rt;
-        ps->mom = (unsigned long long*)mm;
+        ps->dims = (PartDim*)d0;
         ps->tails = (SegCnt*)tl;
         ps->carry = (SegCnt*)cr;
         ps->overflow_words = nodes * kPartBins;
@@ -1108,35 +1128,27 @@ int build_trees(TreeView t, void* tmp, size_t tmp_bytes, uint32_t* qbuf, int32_t
     TreeView tc = t;
     tc.perm = (G % 2 == 0) ? final_perm : perm_alt;
     int32_t* other = (G % 2 == 0) ? perm_alt : final_perm;
-    hipLaunchKernelGGL(k_tree_init, dim3(gfill), dim3(256), 0, s, tc, other);
+    int H = 0;  // levels of the multi-pass path (k_tree_bbox / k_part_*)
+    while (H < G && (t.nclouds << H) < SE3ICP_TREE_WG_MIN) ++H;
+    hipLaunchKernelGGL(k_tree_init, dim3(gfill), dim3(256), 0, s, tc, other, (1 << H) - 1);
     if (ps.overflow_words) hipLaunchKernelGGL(k_clear_words, dim3(256), dim3(256), 0, s, ps.overflow, ps.overflow_words);
     const int nblk = (t.npts + kPartElems - 1) / kPartElems;
     const int nhist = (t.npts + kHistElems - 1) / kHistElems;
-#if SE3ICP_TREE_GSPLIT == 1
-    if (G > 0) {
-        hipLaunchKernelGGL(bbox, dim3(nbs), dim3(256), 0, s, tc, 0);  // the roots' boxes: the moments' scale
-        hipLaunchKernelGGL(k_part_root, dim3((t.nclouds + 63) / 64), dim3(64), 0, s, tc, (PartRoot*)ps.root);
-        hipLaunchKernelGGL(k_clear_words, dim3(64), dim3(256), 0, s, (uint32_t*)ps.mom,
-                           ((size_t)t.nclouds << (G - 1)) * 25 * 2);
-    }
-#endif
     for (int l = 0; l < G; ++l) {
-        PartDim* dims = ps.dims[0];
-#if SE3ICP_TREE_GSPLIT == 1
-        hipLaunchKernelGGL(t.D == 12 ? k_part_moments<12> : k_part_moments<3>, dim3(nbs), dim3(256), 0, s, tc, l,
-                           (const PartRoot*)ps.root, ps.mom);
-        hipLaunchKernelGGL(k_part_dims, dim3(((t.nclouds << l) + 63) / 64), dim3(64), 0, s, tc, l,
-                           (const PartRoot*)ps.root, ps.mom, dims);
-#else
+        if (l >= H) {
+            // enough nodes to fill the GPU with a workgroup each: one launch for the level
+            hipLaunchKernelGGL(t.D == 12 ? k_tree_level<12> : k_tree_level<3>, dim3(t.nclouds << l), dim3(kLevThreads), 0,
+                               s, tc, l, (const int32_t*)tc.perm, other, qbuf);
+            std::swap(tc.perm, other);
+            continue;
+        }
+        PartDim* dims = ps.dims;
         // (the split dimension from every kSplitSample-th point's box: estimating the
         // children's boxes from the parent's cut was measured to give slower searches)
         hipLaunchKernelGGL(bbox, dim3(nbs), dim3(256), 0, s, tc, l);
         hipLaunchKernelGGL(k_part_dims, dim3(((t.nclouds << l) + 63) / 64), dim3(64), 0, s, tc, l, dims);
-#endif
-        hipLaunchKernelGGL(k_part_hist, dim3(nhist), dim3(kPartThreads), 0, s, tc, l, dims, qbuf, ps.dense, ps.block_id0,
-                           ps.overflow);
-        hipLaunchKernelGGL(k_part_select, dim3(t.nclouds << l), dim3(kSelThreads), 0, s, tc, l, (const uint32_t*)ps.dense,
-                           (const int32_t*)ps.block_id0, ps.overflow, ps.sel);
+        hipLaunchKernelGGL(k_part_hist, dim3(nhist), dim3(kPartThreads), 0, s, tc, l, dims, qbuf, ps.overflow);
+        hipLaunchKernelGGL(k_part_select, dim3(t.nclouds << l), dim3(kSelThreads), 0, s, tc, l, ps.overflow, ps.sel);
         hipLaunchKernelGGL(k_part_hist2, dim3(nb), dim3(256), 0, s, tc, l, (const uint32_t*)qbuf, (const PartSel*)ps.sel,
                            ps.overflow);
         hipLaunchKernelGGL(k_part_select2, dim3(t.nclouds << l), dim3(256), 0, s, ps.overflow, ps.sel);
