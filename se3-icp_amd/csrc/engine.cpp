@@ -129,8 +129,8 @@ Engine::~Engine() {
                      &d_rechecked_, &d_keys0_, &d_vals1_, &d_sort_tmp_, &d_stats_,
                      &d_qlist_, &d_qcount_, &d_chunk_cost_, &d_chunk_order_, &d_hist_, &d_cert_, &d_sqlist_, &d_state_, &d_trim_cand_, &d_trim_ctr_, &d_scales_, &d_trim_hist_,
                      &d_lrf_fb_, &d_lrf_fbn_, &d_big_d_, &d_big_i_,
-                     &t3_.perm, &t3_.pos, &t3_.vec, &t3_.vec64, &t3_.vec64a, &t3_.blo, &t3_.bhi, &t3_.lo, &t3_.hi,
-                     &t12_.perm, &t12_.pos, &t12_.vec, &t12_.vec64, &t12_.blo, &t12_.bhi, &t12_.lo, &t12_.hi};
+                     &t3_.perm, &t3_.pos, &t3_.vec, &t3_.vec64, &t3_.vec64a, &t3_.blo, &t3_.bhi, &t3_.lo, &t3_.hi, &t3_.scr,
+                     &t12_.perm, &t12_.pos, &t12_.vec, &t12_.vec64, &t12_.blo, &t12_.bhi, &t12_.lo, &t12_.hi, &t12_.scr};
     for (DevBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     if (h_pairs_) (void)hipHostFree(h_pairs_);
@@ -256,7 +256,8 @@ int Engine::build_tree(int D, const float* vec, hipStream_t s, const double* vec
     const int nnodes = 2 << tb.L;
     const size_t nb = (size_t)nclouds_ * nnodes * D;
     if (!ensure<uint32_t>(tb.blo, nb) || !ensure<uint32_t>(tb.bhi, nb) || !ensure<float>(tb.lo, nb) ||
-        !ensure<float>(tb.hi, nb) || (vec64 && !ensure<double>(tb.vec64, (size_t)D * ld_)) ||
+        !ensure<float>(tb.hi, nb) || !ensure<float>(tb.scr, (size_t)D * ld_) ||
+        (vec64 && !ensure<double>(tb.vec64, (size_t)D * ld_)) ||
         (vec64 && D == 3 && !ensure<double4>(tb.vec64a, (size_t)ld_)))
         return SE3ICP_ERR_OUT_OF_MEMORY;
     std::vector<int32_t> host_n(nclouds_);
@@ -284,6 +285,7 @@ int Engine::build_tree(int D, const float* vec, hipStream_t s, const double* vec
     t.vec64_sources_only = D == 12;  // the loop reads f64 12-D vectors of source clouds (even ids) only
     t.blo = (uint32_t*)tb.blo.p;
     t.bhi = (uint32_t*)tb.bhi.p;
+    t.scr = (float*)tb.scr.p;
     t.lo = (float*)tb.lo.p;
     t.hi = (float*)tb.hi.p;
     if (build_trees(t, d_sort_tmp_.p, d_sort_tmp_.bytes, (uint32_t*)d_keys0_.p, (int32_t*)d_vals1_.p, s) != 0)
@@ -470,6 +472,7 @@ int Engine::read_lrf_stats() {
     ktimes_.lrf_candidates = sum[4];
     ktimes_.lrf_fallback = sum[6];
 #ifdef SE3ICP_PROF
+    tree_prof_report();
     std::fprintf(stderr, "[prof] k_lrf cycles/query: knn|scan %.0f sort|tighten %.0f sums|final+sums %.0f finish %.0f "
                  "(queries %.0f, wave cycles summed over the kernel's waves)\n",
                  sum[8] / sum[0], sum[9] / sum[0], sum[10] / sum[0], sum[11] / sum[0], sum[0]);

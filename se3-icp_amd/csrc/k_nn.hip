@@ -37,7 +37,6 @@ namespace {
 
 using namespace loopdev;
 
-constexpr int kWaves = 4;
 #ifndef SE3ICP_NN_GWAVES
 #define SE3ICP_NN_GWAVES 1  // waves per k_nn_group block
 #endif

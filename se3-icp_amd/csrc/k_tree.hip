@@ -15,6 +15,7 @@
 // inflated by a few ulps so the f32 boxes bound the f64 points they stand for.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <type_traits>
 
 #include "tree.hpp"
@@ -23,6 +24,12 @@
 namespace se3icp {
 
 namespace {
+
+#ifdef SE3ICP_PROF
+// k_tree_local phase ends over all workgroups (100 MHz clock): [D == 12][0] start (min),
+// [1..4] the latest end of load / levels / final / boxes
+__device__ unsigned long long g_tree_prof[2][5] = {{~0ull, 0, 0, 0, 0}, {~0ull, 0, 0, 0, 0}};
+#endif
 
 __device__ __forceinline__ uint32_t ord_bits(float f) {
     const uint32_t u = __float_as_uint(f);
@@ -728,20 +735,29 @@ __global__ __launch_bounds__(kLevThreads) void k_tree_level(TreeView t, int leve
 }
 
 // The levels below G in one workgroup per level-G node (<= kLocalMax points): the node's
-// permutation stays in LDS and every level is a bitonic sort of (sub-node, coordinate
-// along the sub-node's widest dimension) keys -- the same median splits as the global
-// levels, without a device-wide radix sort per level.
+// permutation stays in LDS and every level splits its sub-nodes at the median of the
+// coordinate of largest sample variance (a register sort by one wave for sub-nodes of
+// <= 512 points, a stable LDS partition above).  The node's vectors are first copied into
+// t.tvec at their level-G positions (column-major), so the levels read a few L2-resident
+// columns instead of gathering rows of the input.  The workgroup then finishes its subtree
+// in place of k_tree_finish / k_tree_leafbox / k_tree_up: the final permutation and its
+// inverse, the tree-ordered f32 (and f64) vectors, and the boxes of every leaf and inner
+// node below level G.  s_val holds level-G positions e (s_p[e]: the point); ties in the
+// wave sorts are broken by the point index, as when s_val held the points.
 #ifndef SE3ICP_LOCAL_MAX
 #define SE3ICP_LOCAL_MAX 4096
 #endif
 constexpr int kLocalMax = SE3ICP_LOCAL_MAX;  // power of two
 constexpr int kWaveSortPer = 8;  // sub-nodes of <= 512 points: register sort by one wave
 constexpr int kLocalThreads = 512;
+static_assert(kLocalMax <= 4096, "wave-sort keys carry the position in 12 bits");
 
 template <int D>
-__global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G) {
-    __shared__ unsigned long long s_key[kLocalMax];
+// (4 waves per SIMD: two workgroups per CU, <= 128 VGPRs)
+__global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4))) void k_tree_local(TreeView t, int G) {
+    __shared__ unsigned long long s_key[kLocalMax];  // (histograms, then one column of the node)
     __shared__ int32_t s_val[kLocalMax];
+    __shared__ int32_t s_p[kLocalMax];
     __shared__ int s_best[128];
     __shared__ float s_mu[128], s_sd[128];  // the split coordinate's sample mean and sd (variance splits)
     const int nG = 1 << G;
@@ -750,8 +766,34 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
     const int n = cl.n;
     const int A = tree_first(n, G, i), m = tree_first(n, G, i + 1) - A;
     const int tid = threadIdx.x;
-    if (m <= 1) return;
-    for (int e = tid; e < kLocalMax; e += kLocalThreads) s_val[e] = e < m ? t.perm[cl.off + A + e] : -1;
+    const size_t ld = t.ld;
+    float* row0 = t.scr + (size_t)(cl.off + A) * D;  // the node's vectors at the level-G positions: row0[e * D + d]
+#ifdef SE3ICP_PROF
+    unsigned long long tq[5];
+    tq[0] = __builtin_amdgcn_s_memrealtime();
+#endif
+    // the node's points and their vectors at the level-G positions
+    for (int e = tid; e < kLocalMax; e += kLocalThreads) {
+        const int p = e < m ? t.perm[cl.off + A + e] : -1;
+        s_val[e] = e;
+        s_p[e] = p;
+        if (p >= 0) {
+            if constexpr (D == 12) {
+                const float4* r = reinterpret_cast<const float4*>(t.vec + (size_t)(cl.off + p) * 12);
+                float4* w = reinterpret_cast<float4*>(row0 + (size_t)e * 12);
+#pragma unroll
+                for (int k = 0; k < 3; ++k) w[k] = r[k];
+            } else {
+#pragma unroll
+                for (int d = 0; d < D; ++d) row0[e * D + d] = t.vec[(size_t)d * ld + cl.off + p];
+            }
+        }
+    }
+    __syncthreads();  // (global writes of the workgroup, read back by other threads of it)
+    const bool pk = n <= (1 << 20);  // tie order of the wave sorts: (point, position) in 32 bits
+#ifdef SE3ICP_PROF
+    tq[1] = __builtin_amdgcn_s_memrealtime();
+#endif
     for (int l = G; l < t.L; ++l) {
         const int r = l - G;
         const int nsub = 1 << r;  // sub-nodes of this level under the WG's node (<= 128: see the host)
@@ -775,7 +817,7 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
                     ++cnt;
 #pragma unroll
                     for (int d = 0; d < D; ++d) {
-                        const float x = t.vec[tree_in_ix(t, d, cl.off + p)];
+                        const float x = row0[p * D + d];
                         s1[d] += x;
                         s2[d] = fmaf(x, x, s2[d]);
                     }
@@ -817,14 +859,15 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
                         key[u] = ~0ull;
                         if (e < a1) {
                             const int p = s_val[e];
-                            key[u] = ((unsigned long long)ord_bits(t.vec[tree_in_ix(t, bd, cl.off + p)]) << 32) | (unsigned)p;
+                            const unsigned lo = pk ? ((unsigned)s_p[p] << 12) | (unsigned)p : (unsigned)p;
+                            key[u] = ((unsigned long long)ord_bits(row0[p * D + bd]) << 32) | lo;
                         }
                     }
                     wave_sort_keys<PER>(key);
 #pragma unroll
                     for (int u = 0; u < PER; ++u) {
                         const int e = a0 + lane * PER + u;
-                        if (e < a1) s_val[e] = (int32_t)(unsigned)key[u];
+                        if (e < a1) s_val[e] = (int32_t)((unsigned)key[u] & (pk ? 0xfffu : 0xffffffffu));
                     }
                 }
             };
@@ -860,7 +903,7 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
                     const int sub = tree_node_of(A + e, n, l) - (i << r);
                     const int p = s_val[e];
                     const float sd = s_sd[sub];
-                    const float x = t.vec[tree_in_ix(t, s_best[sub], cl.off + p)];
+                    const float x = row0[p * D + s_best[sub]];
                     float qf = sd > 0.f ? (x - (s_mu[sub] - 8.f * sd)) * (4194303.f / (16.f * sd)) : 0.f;
                     qf = fminf(fmaxf(qf, 0.f), 4194303.f);  // NaN -> 0
                     q[u] = (uint32_t)qf;
@@ -973,7 +1016,98 @@ __global__ __launch_bounds__(kLocalThreads) void k_tree_local(TreeView t, int G)
             __syncthreads();
         }
     }
-    for (int e = tid; e < m; e += kLocalThreads) t.perm[cl.off + A + e] = s_val[e];
+#ifdef SE3ICP_PROF
+    tq[2] = __builtin_amdgcn_s_memrealtime();
+#endif
+    // the final order, a wave per leaf (<= 64 consecutive tree positions): permutation,
+    // inverse, f32 and f64 vectors (the layouts k_tree_finish writes) and the leaf's box
+    // (inflated as k_tree_leafbox does)
+    const bool want64 = (t.tvec64 != nullptr) & !((t.vec64_sources_only != 0) & ((c & 1) != 0));
+    const int R = t.L - G;  // levels of the subtree below its root
+    const int lane = tid & 63, wv = tid >> 6;
+    const size_t bbase = (size_t)c * t.nnodes * D;
+    for (int j = wv; j < (1 << R); j += kLocalThreads / 64) {
+        const int leaf = (i << R) + j;
+        const int a0 = tree_first(n, t.L, leaf), a1 = tree_first(n, t.L, leaf + 1);
+        const bool in = lane < a1 - a0;
+        const int x = a0 - A + (in ? lane : 0);
+        const int e = s_val[x];
+        const int p = s_p[e];
+        const int g = cl.off + A + x, src = cl.off + p;
+        float v[D];
+        if constexpr (D == 12) {
+            const float4* r = reinterpret_cast<const float4*>(row0 + (size_t)e * 12);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const float4 q = r[k];
+                v[4 * k] = q.x; v[4 * k + 1] = q.y; v[4 * k + 2] = q.z; v[4 * k + 3] = q.w;
+            }
+        } else {
+#pragma unroll
+            for (int d = 0; d < D; ++d) v[d] = row0[e * D + d];
+        }
+        if (in) {
+            t.perm[g] = p;
+            t.pos[src] = A + x;
+#pragma unroll
+            for (int d = 0; d < D; ++d) t.tvec[(size_t)d * ld + g] = v[d];
+            if (want64) {
+                if constexpr (D == 12) {
+                    const double2* r64 = reinterpret_cast<const double2*>(t.vec64 + (size_t)src * 12);
+#pragma unroll
+                    for (int k = 0; k < 6; ++k) {
+                        const double2 w = r64[k];
+                        t.tvec64[(size_t)(2 * k) * ld + g] = w.x;
+                        t.tvec64[(size_t)(2 * k + 1) * ld + g] = w.y;
+                    }
+                } else {
+                    double w[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+                    for (int d = 0; d < D; ++d) t.tvec64[(size_t)d * ld + g] = w[d] = t.vec64[(size_t)d * ld + src];
+                    if (t.tpt64) t.tpt64[g] = make_double4(w[0], w[1], w[2], 0.0);
+                }
+            }
+        }
+        const size_t hb = bbase + (size_t)tree_heap(t.L, leaf) * D;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            float lo = in ? v[d] : INFINITY, hi = in ? v[d] : -INFINITY;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) {
+                lo = fminf(lo, __shfl_xor(lo, o, 64));
+                hi = fmaxf(hi, __shfl_xor(hi, o, 64));
+            }
+            if (lo <= hi) {
+                lo = lo - (fabsf(lo) * 4.8e-7f + 1e-30f);
+                hi = hi + (fabsf(hi) * 4.8e-7f + 1e-30f);
+            }
+            if (lane == d) {  // empty leaf: [inf, -inf], a box no query reaches
+                t.lo[hb + d] = lo;
+                t.hi[hb + d] = hi;
+            }
+        }
+    }
+#ifdef SE3ICP_PROF
+    tq[3] = __builtin_amdgcn_s_memrealtime();
+#endif
+    __syncthreads();
+    for (int rr = R - 1; rr >= 0; --rr) {
+        for (int it = tid; it < (D << rr); it += kLocalThreads) {
+            const int j = it / D, d = it % D;
+            const size_t h = (size_t)tree_heap(G + rr, (i << rr) + j);
+            const size_t cl_ = bbase + (2 * h + 1) * D + d, cr_ = bbase + (2 * h + 2) * D + d;
+            t.lo[bbase + h * D + d] = fminf(t.lo[cl_], t.lo[cr_]);
+            t.hi[bbase + h * D + d] = fmaxf(t.hi[cl_], t.hi[cr_]);
+        }
+        __syncthreads();
+    }
+#ifdef SE3ICP_PROF
+    tq[4] = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) {
+        atomicMin(&g_tree_prof[D == 12][0], tq[0]);
+        for (int k = 1; k < 5; ++k) atomicMax(&g_tree_prof[D == 12][k], tq[k]);
+    }
+#endif
 }
 
 __global__ __launch_bounds__(256) void k_tree_finish(TreeView t) {
@@ -1047,10 +1181,11 @@ __global__ __launch_bounds__(256) void k_tree_leafbox(TreeView t) {
     }
 }
 
-// internal boxes = unions of the children, level by level (one block per cloud)
-__global__ __launch_bounds__(1024) void k_tree_up(TreeView t) {
+// internal boxes of the levels above `top` = unions of the children, level by level (one
+// block per cloud)
+__global__ __launch_bounds__(1024) void k_tree_up(TreeView t, int top) {
     const int c = blockIdx.x;
-    for (int l = t.L - 1; l >= 0; --l) {
+    for (int l = top - 1; l >= 0; --l) {
         const int items = (1 << l) * t.D;
         for (int it = threadIdx.x; it < items; it += blockDim.x) {
             const int i = it / t.D, d = it % t.D;
@@ -1160,14 +1295,33 @@ int build_trees(TreeView t, void* tmp, size_t tmp_bytes, uint32_t* qbuf, int32_t
         std::swap(tc.perm, other);
     }
     t.perm = final_perm;
-    if (G < t.L)
+    if (G < t.L) {
+        // the levels below G, the tree-ordered vectors and the boxes below G per level-G node
         hipLaunchKernelGGL(t.D == 12 ? k_tree_local<12> : k_tree_local<3>, dim3(t.nclouds << G), dim3(kLocalThreads), 0,
                            s, t, G);
-    hipLaunchKernelGGL(k_tree_finish, dim3(nb), dim3(256), 0, s, t);
-    const int nleaves = t.nclouds << t.L;
-    hipLaunchKernelGGL(t.D == 12 ? k_tree_leafbox<12> : k_tree_leafbox<3>, dim3((nleaves + 3) / 4), dim3(256), 0, s, t);
-    hipLaunchKernelGGL(k_tree_up, dim3(t.nclouds), dim3(1024), 0, s, t);
+        hipLaunchKernelGGL(k_tree_up, dim3(t.nclouds), dim3(1024), 0, s, t, G);
+    } else {
+        hipLaunchKernelGGL(k_tree_finish, dim3(nb), dim3(256), 0, s, t);
+        const int nleaves = t.nclouds << t.L;
+        hipLaunchKernelGGL(t.D == 12 ? k_tree_leafbox<12> : k_tree_leafbox<3>, dim3((nleaves + 3) / 4), dim3(256), 0, s, t);
+        hipLaunchKernelGGL(k_tree_up, dim3(t.nclouds), dim3(1024), 0, s, t, t.L);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+void tree_prof_report() {
+#ifdef SE3ICP_PROF
+    unsigned long long h[2][5];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_tree_prof), sizeof(h)) != hipSuccess) return;
+    for (int k = 0; k < 2; ++k)
+        if (h[k][0] && h[k][0] != ~0ull)
+            std::fprintf(stderr, "[prof] k_tree_local<%d>: latest phase ends load %.1f levels %.1f final %.1f boxes %.1f us\n",
+                         k ? 12 : 3, (h[k][1] - h[k][0]) / 100.0, (h[k][2] - h[k][0]) / 100.0, (h[k][3] - h[k][0]) / 100.0,
+                         (h[k][4] - h[k][0]) / 100.0);
+    unsigned long long z[2][5];
+    for (int k = 0; k < 2; ++k) { z[k][0] = ~0ull; for (int j = 1; j < 5; ++j) z[k][j] = 0; }
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tree_prof), z, sizeof(z));
+#endif
 }
 
 size_t tree_build_temp_bytes(int npts, int nclouds, int max_n, int L) {

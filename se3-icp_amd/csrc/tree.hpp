@@ -33,6 +33,7 @@ struct TreeView {
     int32_t vec64_sources_only;  // copy the f64 vectors of even (source) clouds only
     uint32_t* blo;     // [nclouds][nnodes][D] build scratch (orderable bits)
     uint32_t* bhi;
+    float* scr;        // [D][ld] build scratch (k_tree_local: the vectors at the level-G positions)
     float* lo;         // [nclouds][nnodes][D] node boxes
     float* hi;
     const int32_t* host_n;  // host copy of the clouds' point counts (level split of the build)
@@ -64,5 +65,6 @@ inline int tree_depth_for(int max_n) {
 int build_trees(TreeView t, void* tmp, size_t tmp_bytes, uint32_t* qbuf, int32_t* perm_alt, hipStream_t s);
 size_t tree_build_temp_bytes(int npts, int nclouds, int max_n, int L);
 int tree_global_levels(int max_n, int L);
+void tree_prof_report();  // (SE3ICP_PROF builds: k_tree_local's phase timeline, then reset)
 
 }  // namespace se3icp
