@@ -127,7 +127,7 @@ Engine::~Engine() {
                      &d_corr_idx_, &d_corr_dist_, &d_flag_list_, &d_flag_count_, &d_trim_key_, &d_red_partial_,
                      &d_red_out_, &d_work_, &d_wb_, &d_wn_, &d_chunks_, &d_partial_, &d_centers_,
                      &d_rechecked_, &d_keys0_, &d_vals1_, &d_sort_tmp_, &d_stats_,
-                     &d_qlist_, &d_qcount_, &d_chunk_cost_, &d_chunk_order_, &d_hist_, &d_cert_, &d_sqlist_, &d_state_, &d_trim_cand_, &d_trim_ctr_, &d_scales_, &d_trim_hist_,
+                     &d_qlist_, &d_qcount_, &d_hist_, &d_cert_, &d_sqlist_, &d_state_, &d_trim_cand_, &d_trim_ctr_, &d_scales_, &d_trim_hist_,
                      &d_lrf_fb_, &d_lrf_fbn_, &d_big_d_, &d_big_i_,
                      &t3_.perm, &t3_.pos, &t3_.vec, &t3_.vec64, &t3_.vec64a, &t3_.blo, &t3_.bhi, &t3_.lo, &t3_.hi, &t3_.scr,
                      &t12_.perm, &t12_.pos, &t12_.vec, &t12_.vec64, &t12_.blo, &t12_.bhi, &t12_.lo, &t12_.hi, &t12_.scr};
@@ -241,8 +241,6 @@ View Engine::view() const {
     v.nchunks = nchunks_;
     v.qlist = (int32_t*)d_qlist_.p;
     v.qcount = (int32_t*)d_qcount_.p;
-    v.chunk_cost = (uint32_t*)d_chunk_cost_.p;
-    v.chunk_order = (int32_t*)d_chunk_order_.p;
     v.sq_list = (int32_t*)d_sqlist_.p;
     v.hist = (const double*)d_hist_.p;
     v.cert = (float4*)d_cert_.p;
@@ -502,10 +500,8 @@ int Engine::setup_chunks(int npairs, hipStream_t s) {
     chunk_level_ = std::max(0, tree_L_ - 4);
     nchunks_ = npairs << chunk_level_;
     if (!ensure<int32_t>(d_qlist_, (size_t)nchunks_ * kChunkQ) || !ensure<int32_t>(d_qcount_, (size_t)nchunks_ * (kChunkQ / 64)) ||
-        !ensure<uint32_t>(d_chunk_cost_, (size_t)nchunks_) || !ensure<int32_t>(d_chunk_order_, (size_t)nchunks_) ||
         !ensure<double>(d_hist_, (size_t)kHist * npairs * 12))
         return SE3ICP_ERR_OUT_OF_MEMORY;
-    HIPCHK(hipMemsetAsync(d_chunk_cost_.p, 0, sizeof(uint32_t) * nchunks_, s));
     if (pinned(h_hist_, h_hist_cap_, (size_t)npairs * 12)) return SE3ICP_ERR_OUT_OF_MEMORY;
     HIPCHK(hipMemsetAsync(d_cert_.p, 0xff, sizeof(float4) * ld_, s));  // iteration -1: no certificate
     return 0;

@@ -167,10 +167,8 @@ __device__ __forceinline__ void wave_bitonic(double* bd, int* bi, int lane, int 
 // The per-cloud records and node boxes are also passed as restrict-qualified arguments:
 // with no possible aliasing store the compiler can serve their wave-uniform reads from
 // the scalar cache (s_load) instead of vector loads.
-#ifndef SE3ICP_LRF_WPE
-#define SE3ICP_LRF_WPE 5
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_WPE))) void k_lrf(View v, int write_knn, const int32_t* __restrict__ cloud_of,
+// (5 waves per SIMD)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k_lrf(View v, int write_knn, const int32_t* __restrict__ cloud_of,
                                              const CloudSetup* __restrict__ setup,
                                              const CloudDev* __restrict__ clouds, const float* __restrict__ tlo,
                                              const float* __restrict__ thi, const int32_t* __restrict__ qlist,
@@ -182,17 +180,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
     extern __shared__ int s_dyn[];
     __shared__ double s_park[kWaves][kQ][PK_N];
     const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#ifdef SE3ICP_LRF_LDSPAD  // occupancy experiment: unused LDS
-    __shared__ int s_pad[SE3ICP_LRF_LDSPAD / 4];
-    if (v.npts < 0) s_pad[threadIdx.x] = 0;
-#endif
     // first global slot (3-D tree order) of the wave's kQ queries; wave-uniform so that
     // the per-cloud records and the node boxes are scalar loads
-#if SE3ICP_LRF_XCD
     const int bid = xcd_block(blockIdx.x, gridDim.x);  // neighbouring blocks (tree order) share an XCD's L2
-#else
-    const int bid = blockIdx.x;
-#endif
     // queries: tree slots 0 .. npts-1, or (list mode, the queries k_lrf8 hands over) the
     // slots qlist[0 .. *qcount-1], the grid striding over them
     const int nvq = qlist ? *qcount : v.npts;
@@ -216,11 +206,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
     int prev_c = -1, prev_K = 0;
     double prev_kth = 0.0, pqx = 0.0, pqy = 0.0, pqz = 0.0;
     unsigned n_queries = 0, n_leaves = 0, n_sel = 0, n_box = 0, n_cand = 0;
-#ifdef SE3ICP_LRF_NOCOUNT  // work counters off (SGPR pressure experiment)
-#define LRF_COUNT(x) do {} while (0)
-#else
 #define LRF_COUNT(x) x
-#endif
 #ifdef SE3ICP_PROF
     unsigned long long c_knn = 0, c_sort = 0, c_sum = 0, c_fin = 0;
 #endif
@@ -356,7 +342,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
             }
             nb += __popcll(m);
             // the first bound from Kw candidates (a seeded bound is loose), then whenever the buffer fills
-            if ((!tight && nb >= Kw && (SE3ICP_LRF_TIGHT || !have_thr)) || nb > kBuf - kLeafMax) select_thr();
+            if ((!tight && nb >= Kw && !have_thr) || nb > kBuf - kLeafMax) select_thr();
         };
         auto open = [&](float lb) __attribute__((always_inline)) {  // may a box at lb hold a candidate?
             return !have_thr || lb <= thr_f;
@@ -386,37 +372,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
                 float lbA = INFINITY;
                 if (ai < nA) lbA = box_lb3(box_lo + 3 * (firstA + ai), box_hi + 3 * (firstA + ai), fx, fy, fz);
                 LRF_COUNT(++n_box);
-#if SE3ICP_LRF_ORDER == 1
-                // nearest first: the bound tightens fastest and the rest fall to it
-                for (;;) {
-                    const float m = wave_minf(lbA);
-                    const unsigned long long mm = __ballot(lbA == m);
-                    if (mm == 0ull || !open(m)) break;
-                    const int j = __builtin_ctzll(mm);
-                    if (lane == j) lbA = INFINITY;
-#else
                 OutwardBits itA(__ballot((int)(ai < nA) & (int)open(lbA)), (own_i >> sh) - c0);
                 for (int j; (j = itA.next()) >= 0;) {
                     if (!open(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbA), j)))) continue;
-#endif
                     const int l0 = (c0 + j) << sh;  // first leaf of the level-A node
                     const int li = l0 + lane;
                     float lbL = INFINITY;
                     if ((int)(lane < (1 << sh)) & ((int)(li < s_lo) | (int)(li > s_hi)))
                         lbL = box_lb3(box_lo + 3 * (first_leaf + li), box_hi + 3 * (first_leaf + li), fx, fy, fz);
                     LRF_COUNT(++n_box);
-#if SE3ICP_LRF_ORDER == 1
-                    for (;;) {
-                        const float ml = wave_minf(lbL);
-                        const unsigned long long ml_m = __ballot(lbL == ml);
-                        if (ml_m == 0ull || !open(ml)) break;
-                        const int t = __builtin_ctzll(ml_m);
-                        if (lane == t) lbL = INFINITY;
-#else
                     OutwardBits itL(__ballot(open(lbL)), own_i - l0);
                     for (int t; (t = itL.next()) >= 0;) {
                         if (!open(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbL), t)))) continue;
-#endif
                         leaf(first_leaf + l0 + t);
                     }
                 }
@@ -430,11 +397,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SE3ICP_LRF_
         __builtin_amdgcn_wave_barrier();
         {
             const int lim = min(nb, Kw + 1);  // ranks whose order matters (top-Kw and its boundary)
-            bool done = false;
-#if SE3ICP_LRF_FASTSORT
-            done = nb <= 128 ? wave_sort_u64<2>(bd, bi, lane, nb, lim) : wave_sort_u64<4>(bd, bi, lane, nb, lim);
+            const bool done = nb <= 128 ? wave_sort_u64<2>(bd, bi, lane, nb, lim) : wave_sort_u64<4>(bd, bi, lane, nb, lim);
             __builtin_amdgcn_wave_barrier();
-#endif
             if (!done) {  // exact (f64 d, point index) order; the lists keep tree slots
                 for (int e = lane; e < nb; e += 64) bi[e] = T.perm[bi[e]];
                 __builtin_amdgcn_wave_barrier();
@@ -719,17 +683,13 @@ void launch_lrf(const View& v, int write_knn, hipStream_t s) {
                        v.setup, v.clouds, v.t3.lo, v.t3.hi, nullptr, nullptr, kQ);
 }
 
-#ifndef SE3ICP_LRF_LIST_QPW
-#define SE3ICP_LRF_LIST_QPW 4  // queries per wave of the hand-over pass (measured: 1, 2, 4, 8)
-#endif
-#ifndef SE3ICP_LRF_LIST_BLOCKS
-#define SE3ICP_LRF_LIST_BLOCKS 1024
-#endif
+constexpr int kListQpw = 4;        // queries per wave of the hand-over pass (measured: 1, 2, 4, 8)
+constexpr int kListBlocks = 1024;  // its grid (strided)
 void launch_lrf_list(const View& v, const int32_t* qlist, const int32_t* qcount, hipStream_t s, int qpw) {
     const size_t lds = sizeof(int) * (size_t)kWaves * kQ * std::min(v.kmax, kSmallK);
-    const int nblk = std::max(1, std::min(SE3ICP_LRF_LIST_BLOCKS, (v.npts + kWaves * kQ - 1) / (kWaves * kQ)));
+    const int nblk = std::max(1, std::min(kListBlocks, (v.npts + kWaves * kQ - 1) / (kWaves * kQ)));
     hipLaunchKernelGGL(k_lrf, dim3(nblk), dim3(64 * kWaves), lds, s, v, 0, v.cloud_of, v.setup, v.clouds, v.t3.lo,
-                       v.t3.hi, qlist, qcount, qpw > 0 ? std::min(qpw, kQ) : SE3ICP_LRF_LIST_QPW);
+                       v.t3.hi, qlist, qcount, qpw > 0 ? std::min(qpw, kQ) : kListQpw);
 }
 
 }  // namespace se3icp

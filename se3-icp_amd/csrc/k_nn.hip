@@ -37,25 +37,14 @@ namespace {
 
 using namespace loopdev;
 
-#ifndef SE3ICP_NN_GWAVES
-#define SE3ICP_NN_GWAVES 1  // waves per k_nn_group block
-#endif
-// (one wave per block: a block's LDS is released when its last wave ends, so 4-wave blocks
-// whose waves end at different times strand LDS -- a CU holds at most five 28.7 KB blocks)
-constexpr int kGWaves = SE3ICP_NN_GWAVES;
-// Leaves wanted by at most this many lanes take the compacted path (8 lanes per query)
-#ifndef SE3ICP_NN_TPL
-#define SE3ICP_NN_TPL 4  // targets per lane in the compacted leaf sweeps (held in registers across queries)
-#endif
-#ifndef SE3ICP_NN_COMPACT3
-#define SE3ICP_NN_COMPACT3 40  // R3 phase (0: broadcast sweeps only)
-#endif
-#ifndef SE3ICP_NN_COMPACT
-#define SE3ICP_NN_COMPACT 40
-#endif
-#ifndef SE3ICP_NN_SEED
-#define SE3ICP_NN_SEED 1  // first searches seeded by a greedy tree descent (and this many leaf targets)
-#endif
+// Tuned constants (A/B on the bench's C4 batch; the rejected alternatives are listed in
+// DESIGN.md's measurement log):
+//   k_nn_group blocks are ONE wave: a block's LDS is released when its last wave ends, so
+//   4-wave blocks whose waves ended at different times stranded LDS (a CU held at most five
+//   28.7 KB blocks): SE(3) NN -9 %.
+constexpr int kTPL = 4;        // targets per lane in the compacted leaf sweeps (kept in registers across queries)
+constexpr int kCompact = 40;   // a leaf wanted by at most this many lanes takes the compacted sweep (12-D and 3-D)
+constexpr int kSeedTargets = 1;  // first searches: seeded by a greedy tree descent and this many leaf targets
 
 // packed f32 pairs: v_pk_add_f32 / v_pk_fma_f32 issue two lanes' worth of f32 math per
 // instruction (the f32 vector peak of gfx950 assumes them)
@@ -136,7 +125,7 @@ __device__ __forceinline__ float dist12(const f32x2* q2, const float4* t) {
 // sub, sub+LPQ, sub+2LPQ, sub+3LPQ per lane (LPQ * 4 >= cnt), the group's top-2 into
 // r1/r2/rb[query].  The lane's 4 targets are loop-invariant over the queries: the
 // compiler keeps them in registers (4 waves/SIMD; measured faster than re-reading at 5).
-template <int D, int LPQ, int TPL = SE3ICP_NN_TPL>
+template <int D, int LPQ, int TPL = kTPL>
 __device__ __forceinline__ void compact_sweep(const float4* tile, const float4* sq, const int* wl, float* r1, float* r2,
                                               int* rb, int w, int cnt, int ta, int lane) {
     constexpr int NV = (D + 3) / 4;
@@ -192,48 +181,17 @@ __device__ __forceinline__ void compact_sweep(const float4* tile, const float4* 
     }
 }
 
-// chunks with at least this many searched queries use k_nn_group, sparser ones k_nn_single
+// chunks with at least kDense searched queries use k_nn_group, sparser ones k_nn_single
 // (measured: a 12-D wave-per-query search costs ~5x the lanes' share of a group's, a 3-D
-// one far more, but a group's latency bounds an iteration with few groups)
-#ifndef SE3ICP_NN_WPE
-#define SE3ICP_NN_WPE 4  // waves per SIMD of k_nn_group (4: its natural 128 VGPRs)
-#endif
-#ifndef SE3ICP_NN_XCD_RUN
-#define SE3ICP_NN_XCD_RUN 64  // (SE3ICP_NN_XCD 2) group blocks per XCD run: 64 = 16 chunks (A/B 16 / 64 / 128 / 256: 64 best)
-#endif
-#ifndef SE3ICP_NN_XCD
-#define SE3ICP_NN_XCD 2  // chunk -> block mapping of k_nn_prep / k_nn_group: 2 runs of chunks dealt round-robin over the XCDs (neighbouring chunks share target leaves in one L2; SE(3) NN -3 %), 1 one contiguous range per XCD (slower: the pairs load the XCDs unevenly), 0 none
-#endif
-#ifndef SE3ICP_NN_EJECT
-#define SE3ICP_NN_EJECT 0  // node visits after which a group wave hands its widest-ball lanes to k_nn_single (0: never; A/B 64 / 128 / 256: NN +31 / +9 / +4 %: the long waves are uniformly hard groups)
-#endif
-#ifndef SE3ICP_NN_SMALL
-#define SE3ICP_NN_SMALL 4  // groups of at most this many queries are searched one query at a time
-#endif
-#ifndef SE3ICP_NN_ORDER
-#define SE3ICP_NN_ORDER 0  // (A/B 4 / 8 / 16 classes: SE(3) NN -2 %, but the ordering launch costs as much; off) k_nn_group dispatches chunks in this many cost classes, costliest first (by the chunk's longest group wave of its last search); 0: tree order
-#endif
-#ifndef SE3ICP_NN_TWOLEVEL
-#define SE3ICP_NN_TWOLEVEL 0  // (A/B: SE(3) NN +1 %, kept off) k_nn_group: an interior node whose children are interior pushes its four grandchildren in one step (one box-load round trip per two levels)
-#endif
-#ifndef SE3ICP_NN_SINGLE_BLOCKS
-#define SE3ICP_NN_SINGLE_BLOCKS 4096  // grid of the one-query-per-wave kernels (4 waves per block, grid-strided)
-#endif
-#ifndef SE3ICP_NN_BIN
-#define SE3ICP_NN_BIN 0  // 1: k_nn_prep groups the searched queries by their previous match's target position (A/B: NN +22 %, prep +65 %)
-#endif
-#ifndef SE3ICP_NN_SPLIT
-#define SE3ICP_NN_SPLIT 1
-#endif
-#ifndef SE3ICP_NN_DENSE
-#define SE3ICP_NN_DENSE 256  // (A/B 64 / 128 / 256: 256 best by ~1 % of the loop)
-#endif
-#ifndef SE3ICP_NN_DENSE3
-#define SE3ICP_NN_DENSE3 256
-#endif
-#ifndef SE3ICP_NN_EXPAND
-#define SE3ICP_NN_EXPAND 1.0  // search widening, in units of the query's displacement this iteration
-#endif
+// one far more, but a group's latency bounds an iteration with few groups; A/B 64 / 128 /
+// 256 within 1 % of each other with one-wave group blocks)
+constexpr int kDense = 256;
+constexpr int kWpe = 4;        // waves per SIMD of k_nn_group (its natural 128 VGPRs; 5 measured +8 %)
+constexpr int kXcdRun = 256;   // group blocks per XCD run (16 chunks; runs dealt round-robin over the XCDs:
+                               // neighbouring chunks share target leaves in one L2, SE(3) NN -3 %)
+constexpr int kSmall = 4;      // groups of at most this many queries are searched one query at a time
+constexpr int kSingleBlocks = 4096;  // grid of the one-query-per-wave kernels (4 waves per block, grid-strided)
+constexpr double kExpand = 1.0;      // search widening, in units of the query's displacement this iteration
 
 template <int D>
 __device__ __forceinline__ double dist_f64(const double* a, const double* b) {
@@ -327,10 +285,9 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
         load_hist(v, it - 1, pair, Tp);
         pose_point(Tp, mt[0], mt[1], mt[2], Qp);
         const double dt = dist3_f64(Qt, Qp);
-        m = (float)(SE3ICP_NN_EXPAND * sqrt(a2 * rot_frob2(T, Tp) + dt * dt));
+        m = (float)(kExpand * sqrt(a2 * rot_frob2(T, Tp) + dt * dt));
     }
     v.cert[g].w = m;
-#if SE3ICP_NN_SEED
     // No previous match (a pair's first search): seed one from a greedy descent of the
     // target tree (the child whose f32 box bound is smaller, down to a leaf; a target of
     // that leaf).  The search only uses it for its first pruning threshold, so any target
@@ -354,12 +311,12 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
         const int li = h - ((1 << TR.L) - 1);
         const int ta = min(tree_first(ct.n, TR.L, li), ct.n - 1);
         const int cnt = max(tree_first(ct.n, TR.L, li + 1) - ta, 1);
-        // the nearest of SE3ICP_NN_SEED targets spread over the leaf
+        // the nearest of kSeedTargets targets spread over the leaf
         const float* tv = TR.tvec + ct.off;
         int best = ta;
         float bd = INFINITY;
-        for (int k = 0; k < SE3ICP_NN_SEED; ++k) {
-            const int t = ta + (2 * k + 1) * cnt / (2 * SE3ICP_NN_SEED);
+        for (int k = 0; k < kSeedTargets; ++k) {
+            const int t = ta + (2 * k + 1) * cnt / (2 * kSeedTargets);
             float d = 0.f;
 #pragma unroll
             for (int r = 0; r < D; ++r) {
@@ -371,7 +328,6 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
         }
         v.corr_idx[g] = TR.perm[ct.off + best];
     }
-#endif
     return false;
 }
 
@@ -380,14 +336,11 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
 // for k_nn_group: consecutive leaves' remaining queries share a 64-lane group as long as
 // they fit, a leaf is never split (with every query searched, a group is one leaf).
 // qlist[c][j][lane] = local tree position, qcount[c][j] = lanes of group j.
-#ifndef SE3ICP_NN_PREP_WPE
-#define SE3ICP_NN_PREP_WPE 8  // waves per SIMD of k_nn_prep: 8 = two 1024-thread blocks per CU (<= 64 VGPRs)
-#endif
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_PREP_WPE))) void k_nn_prep(View v) {
+// (8 waves per SIMD: two 1024-thread blocks per CU, <= 64 VGPRs)
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_nn_prep(View v) {
     constexpr int NL = kChunkQ / 64;  // leaves (groups) per chunk
     __shared__ int s_cnt[NL], s_slot[NL], s_base[NL], s_wc[NL], s_single;
-    const int c = SE3ICP_NN_XCD == 2 ? xcd_block_runs(blockIdx.x, gridDim.x, SE3ICP_NN_XCD_RUN / 4)
-                  : SE3ICP_NN_XCD ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int c = xcd_block_runs(blockIdx.x, gridDim.x, kXcdRun / 16);  // (k_nn_group's chunk runs)
     const int pair = c >> v.chunk_level;
     const PairDev* P = v.pairs + pair;
     const int phase = P->phase;
@@ -396,9 +349,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_
     __syncthreads();
     bool active = false;
     int x = 0, l = 0;
-#if SE3ICP_NN_BIN
-    unsigned tkey = 0xffffffffu;  // tree position of the previous match
-#endif
     if (phase != PHASE_IDLE) {
         const CloudDev cs = v.clouds[P->src], ct = v.clouds[P->tgt];
         const TreeRef TR = (phase == PHASE_SE3) ? v.t12 : v.t3;
@@ -412,12 +362,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_
                                           : !prep_settle<3>(v, TR, P, pair, ct, gx, g, 0.0);
             l = tree_node_of(x, cs.n, TR.GL) - (ci << (TR.GL - v.chunk_level));
             if (active) atomicAdd(&s_cnt[l], 1);
-#if SE3ICP_NN_BIN
-            if (active) {
-                const int prev = v.corr_idx[g];
-                tkey = (prev >= 0 && prev < ct.n) ? (unsigned)TR.pos[ct.off + prev] : 0x7fffffffu;
-            }
-#endif
         }
     }
     const unsigned long long m = __ballot(active);
@@ -440,7 +384,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_
         total = base;
         // a sparse chunk goes to the one-query-per-wave kernel instead (SE(3) list from the
         // front of sq_list, R3 from the back)
-        const bool dense = total >= (phase == PHASE_SE3 ? SE3ICP_NN_DENSE : SE3ICP_NN_DENSE3);
+        const bool dense = total >= kDense;
         s_single = -1;
         if ((int)!dense & (int)(total > 0)) s_single = atomicAdd(&v.flag_count[phase == PHASE_SE3 ? 1 : 2], total);
         for (int j = 0; j < NL; ++j) v.qcount[c * NL + j] = dense ? gcnt[j] : 0;
@@ -453,33 +397,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_
         }
     }
     __syncthreads();
-#if SE3ICP_NN_BIN
-    if (s_single < 0) {
-        // group the searched queries by the target tree position of their previous match:
-        // a wave's 64 lanes then want the same target leaves (bitonic sort of the chunk's
-        // (position, query) keys in LDS; groups of 64 consecutive keys)
-        __shared__ unsigned long long s_key[kChunkQ];
-        const int tid = threadIdx.x;
-        s_key[tid] = active ? (((unsigned long long)tkey << 32) | (unsigned)x) : ~0ull;
-        __syncthreads();
-        for (int kk = 2; kk <= kChunkQ; kk <<= 1) {
-            for (int j = kk >> 1; j > 0; j >>= 1) {
-                const int p = tid ^ j;
-                if (p > tid) {
-                    const unsigned long long a = s_key[tid], b = s_key[p];
-                    const bool up = (tid & kk) == 0;
-                    if ((a > b) == up) { s_key[tid] = b; s_key[p] = a; }
-                }
-                __syncthreads();
-            }
-        }
-        int total = 0;
-        for (int j = 0; j < NL; ++j) total += s_cnt[j];
-        if (tid < total) v.qlist[(size_t)c * kChunkQ + tid] = (int)(unsigned)s_key[tid];
-        if (tid < NL) v.qcount[c * NL + tid] = min(64, max(0, total - 64 * tid));
-        return;
-    }
-#endif
     if (active) {
         int r = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
         for (int w = 0; w < wid; ++w) r += s_wc[w];
@@ -491,63 +408,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_
             if (phase == PHASE_SE3) v.sq_list[sb + r] = gxs;
             else v.sq_list[v.ld - 1 - (sb + r)] = gxs;
         }
-    }
-}
-
-// Dispatch order of k_nn_group's chunks (one 1024-thread block): a stable partition into
-// SE3ICP_NN_ORDER classes by the cost each chunk's longest group wave had in the last
-// search (costliest class first, tree order within a class, so neighbouring chunks still
-// share target leaves in one L2).  A launch's time is set by its longest waves; started
-// first, they overlap the many short ones.  Costs are cleared for the next search; with
-// none recorded (a first search) the order is the tree order.  Results never depend on it.
-__global__ __launch_bounds__(1024) void k_nn_order(uint32_t* __restrict__ cost, int32_t* __restrict__ order, int n) {
-    constexpr int NC = SE3ICP_NN_ORDER > 0 ? SE3ICP_NN_ORDER : 1;
-    __shared__ unsigned s_max;
-    __shared__ int s_base[NC], s_wcnt[16][NC];
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    if (t == 0) s_max = 0u;
-    if (t < NC) s_base[t] = 0;
-    __syncthreads();
-    unsigned m = 0u;
-    for (int c = t; c < n; c += 1024) m = max(m, cost[c]);
-    atomicMax(&s_max, m);
-    __syncthreads();
-    const unsigned long long cmax = s_max;
-    auto cls_of = [&](unsigned x) __attribute__((always_inline)) {
-        return (int)min((unsigned long long)(NC - 1), ((cmax - x) * NC) / (cmax + 1));
-    };
-    for (int c = t; c < n; c += 1024) atomicAdd(&s_base[cls_of(cost[c])], 1);
-    __syncthreads();
-    if (t == 0) {
-        int acc = 0;
-        for (int k = 0; k < NC; ++k) { const int x = s_base[k]; s_base[k] = acc; acc += x; }
-    }
-    __syncthreads();
-    for (int c0 = 0; c0 < n; c0 += 1024) {
-        const int c = c0 + t;
-        const bool in = c < n;
-        int k = NC;
-        if (in) { k = cls_of(cost[c]); cost[c] = 0u; }
-        int rank = 0;
-#pragma unroll
-        for (int j = 0; j < NC; ++j) {
-            const unsigned long long b = __ballot(k == j);
-            if (lane == 0) s_wcnt[w][j] = __popcll(b);
-            if (k == j) rank = __builtin_amdgcn_mbcnt_hi((unsigned)(b >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b, 0u));
-        }
-        __syncthreads();
-        if (in) {
-            int pos = s_base[k] + rank;
-            for (int u = 0; u < w; ++u) pos += s_wcnt[u][k];
-            order[pos] = c;
-        }
-        __syncthreads();
-        if (t < NC) {
-            int tot = 0;
-            for (int u = 0; u < 16; ++u) tot += s_wcnt[u][t];
-            s_base[t] += tot;
-        }
-        __syncthreads();
     }
 }
 
@@ -590,46 +450,38 @@ __device__ __forceinline__ void single_one(const View& v, const PairDev* P, int 
                                            unsigned* n_box);
 
 template <int D>
-__global__ __launch_bounds__(64 * kGWaves) __attribute__((amdgpu_waves_per_eu(SE3ICP_NN_WPE))) void k_nn_group(View v) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kWpe))) void k_nn_group(View v) {
     constexpr int NV = (D + 3) / 4;
-    __shared__ float4 s_tile[kGWaves][kLeafMax * NV];
+    __shared__ float4 s_tile[kLeafMax * NV];
     // compacted leaf sweeps (12-D): the wave's query vectors, the list of lanes that want
     // the current leaf, and the per-query top-2 of the leaf
-    __shared__ float4 s_q[kGWaves][64 * NV];
-    __shared__ int s_wl[kGWaves][64];
-    __shared__ float s_r1[kGWaves][64], s_r2[kGWaves][64];
-    __shared__ int s_rb[kGWaves][64];
-    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // wave-uniform work item: group jg (64 listed queries) of chunk c; the pair record,
-    // node boxes and leaf ranges become scalar loads
-    // (SE3ICP_NN_SPLIT waves per group of the 12-D search, 64 / split queries each: more,
-    // shorter waves for a launch whose time is set by its longest waves)
-    constexpr int kSplit = D == 12 ? SE3ICP_NN_SPLIT : 1;
-    // (blocks of one XCD take consecutive chunks: a pair's target tree stays in that XCD's L2)
-    const int bx = SE3ICP_NN_XCD == 2 ? xcd_block_runs(blockIdx.x, gridDim.x, SE3ICP_NN_XCD_RUN * 4 / kGWaves)
-                   : SE3ICP_NN_XCD ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-    const int wi = __builtin_amdgcn_readfirstlane(bx * kGWaves + wid);
-    const int gq = wi / kSplit, q_lo = (wi % kSplit) * (64 / kSplit);
+    __shared__ float4 s_q[64 * NV];
+    __shared__ int s_wl[64];
+    __shared__ float s_r1[64], s_r2[64];
+    __shared__ int s_rb[64];
+    const int lane = threadIdx.x & 63;
+    // wave-uniform work item: group gi & 15 (64 listed queries) of chunk c; the pair record,
+    // node boxes and leaf ranges become scalar loads (blocks of one XCD take runs of
+    // consecutive chunks: a pair's target tree stays in that XCD's L2)
+    const int gq = __builtin_amdgcn_readfirstlane(xcd_block_runs(blockIdx.x, gridDim.x, kXcdRun));
     if ((gq >> 4) >= v.nchunks) return;
-    // chunk at dispatch position gq >> 4 (k_nn_order: the costliest chunks start first, so
-    // the launch does not end on a long wave that started late)
-    const int c = SE3ICP_NN_ORDER ? __builtin_amdgcn_readfirstlane(v.chunk_order[gq >> 4]) : (gq >> 4);
-    const int gi = (c << 4) | (gq & 15);
+    const int c = gq >> 4;
+    const int gi = gq;
     const int pair = c >> v.chunk_level;
     const PairDev* P = v.pairs + pair;
     const int phase = P->phase;
     if (phase != (D == 12 ? PHASE_SE3 : PHASE_R3)) return;
-    const int cnt_q = min(__builtin_amdgcn_readfirstlane(v.qcount[gi]) - q_lo, 64 / kSplit);
+    const int cnt_q = __builtin_amdgcn_readfirstlane(v.qcount[gi]);
     if (cnt_q <= 0) return;
     const CloudDev cs = v.clouds[P->src], ct = v.clouds[P->tgt];
     const TreeRef TR = (D == 12) ? v.t12 : v.t3;
-    if (cnt_q <= SE3ICP_NN_SMALL) {
+    if (cnt_q <= kSmall) {
         // a group of a few queries (a chunk's leftovers): each searched by all 64 lanes in
         // turn (k_nn_single's lane-parallel search) -- a lone query with a wide ball would
         // otherwise walk the tree one node per step and set the launch's time
         unsigned n_eval = 0, n_box = 0;
         for (int q = 0; q < cnt_q; ++q) {
-            const int gxq = __builtin_amdgcn_readfirstlane(cs.off + v.qlist[(size_t)gi * 64 + q_lo + q]);
+            const int gxq = __builtin_amdgcn_readfirstlane(cs.off + v.qlist[(size_t)gi * 64 + q]);
             const int gq = __builtin_amdgcn_readfirstlane(cs.off + TR.perm[gxq]);
             single_one<D>(v, P, pair, TR, ct, gxq, gq, lane, &n_eval, &n_box);
         }
@@ -637,12 +489,11 @@ __global__ __launch_bounds__(64 * kGWaves) __attribute__((amdgpu_waves_per_eu(SE
             unsigned long long* st = v.stats + kStatCols * (gi & 63) + (D == 12 ? 0 : 2);
             atomicAdd(st, 64ull * n_eval);
             atomicAdd(st + 1, 64ull * n_box);
-            if (SE3ICP_NN_ORDER) atomicMax(v.chunk_cost + c, n_box / 2u + n_eval / 8u);
         }
         return;
     }
     const bool valid = lane < cnt_q;
-    const int gx = cs.off + v.qlist[(size_t)gi * 64 + q_lo + (valid ? lane : 0)];  // source tree slot
+    const int gx = cs.off + v.qlist[(size_t)gi * 64 + (valid ? lane : 0)];  // source tree slot
     const int g = cs.off + TR.perm[gx];
     const float mrg = valid ? v.cert[g].w : 0.f;
 
@@ -671,11 +522,11 @@ __global__ __launch_bounds__(64 * kGWaves) __attribute__((amdgpu_waves_per_eu(SE
     const float* tv = TR.tvec + ct.off;
     const size_t ld = v.ld;
     if constexpr (D == 12) {
-        s_q[wid][lane * 3 + 0] = make_float4(q[0], q[1], q[2], q[3]);
-        s_q[wid][lane * 3 + 1] = make_float4(q[4], q[5], q[6], q[7]);
-        s_q[wid][lane * 3 + 2] = make_float4(q[8], q[9], q[10], q[11]);
+        s_q[lane * 3 + 0] = make_float4(q[0], q[1], q[2], q[3]);
+        s_q[lane * 3 + 1] = make_float4(q[4], q[5], q[6], q[7]);
+        s_q[lane * 3 + 2] = make_float4(q[8], q[9], q[10], q[11]);
     } else {
-        s_q[wid][lane] = make_float4(q[0], q[1], q[2], 0.f);
+        s_q[lane] = make_float4(q[0], q[1], q[2], 0.f);
     }
 
     // pruning threshold for the best / second-best f32 distances a1 <= a2: the certified
@@ -705,11 +556,10 @@ __global__ __launch_bounds__(64 * kGWaves) __attribute__((amdgpu_waves_per_eu(SE
     const float* box_lo = TR.lo + (size_t)P->tgt * TR.nnodes * D;
     const float* box_hi = TR.hi + (size_t)P->tgt * TR.nnodes * D;
     const int first_leaf = (1 << TR.L) - 1;
-    float4* tile = s_tile[wid];
+    float4* tile = s_tile;
     int stk = 0;  // DFS stack in a VGPR: lane i holds entry i (depth <= 2L+1 < 64)
     int sp = 1;
     unsigned n_eval = 0, n_box = 0;  // wave-uniform work counters (roofline accounting)
-    unsigned n_leaf = 0;             // leaves swept (the chunk cost)
 #ifdef SE3ICP_PROF
     unsigned n_want = 0, n_leafv = 0;
     unsigned long long c_leaf = 0, c_lload = 0;  // shader-clock cycles in leaf visits / their target loads
@@ -717,37 +567,7 @@ __global__ __launch_bounds__(64 * kGWaves) __attribute__((amdgpu_waves_per_eu(SE
     const unsigned n_valid = (unsigned)__popcll(__ballot(valid));
     const unsigned long long t_w0 = __builtin_amdgcn_s_memrealtime();
 #endif
-#if SE3ICP_NN_EJECT
-    // A wave still walking after SE3ICP_NN_EJECT node visits usually carries a query or a
-    // few with a far wider ball than the rest (an SE(3) element no target frame resembles):
-    // those lanes leave the group walk and go to the one-query-per-wave search (k_nn_single,
-    // next in the stream), which tests 64 nodes per instruction instead of one per step.
-    bool ejected = false;
-    unsigned next_check = 2u * SE3ICP_NN_EJECT;
-#endif
     while (sp > 0) {
-#if SE3ICP_NN_EJECT
-        if (n_box >= next_check) {
-            next_check += 2u * SE3ICP_NN_EJECT;
-            const bool live = (int)valid & (int)!ejected;
-            const float tmax = -wave_minf(live ? -thr : 0.f);
-            const bool ej = (int)live & (int)(tmax > 0.f) & (int)(thr >= 0.25f * tmax);
-            const unsigned long long em = __ballot(ej);
-            const int ne = __popcll(em);
-            if ((int)(ne > 0) & (int)(ne <= 16)) {
-                int base = 0;
-                if (lane == 0) base = atomicAdd(&v.flag_count[D == 12 ? 1 : 2], ne);
-                base = __shfl(base, 0, 64);
-                if (ej) {
-                    const int r = base + __builtin_amdgcn_mbcnt_hi((unsigned)(em >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)em, 0u));
-                    if (D == 12) v.sq_list[r] = gx;
-                    else v.sq_list[v.ld - 1 - r] = gx;
-                    ejected = true;
-                    thr = -1.f;
-                }
-            }
-        }
-#endif
         const int h = __builtin_amdgcn_readlane(stk, sp - 1);
         --sp;
         if (h >= first_leaf) {
@@ -758,7 +578,7 @@ __global__ __launch_bounds__(64 * kGWaves) __attribute__((amdgpu_waves_per_eu(SE
             // lanes whose own bound admits this leaf (box re-tested: the bounds shrank since the push)
             unsigned long long W = ~0ull;
             int w = 64;
-            if (D == 12 || SE3ICP_NN_COMPACT3) {
+            {
                 float lbh;
                 if constexpr (D == 12) lbh = box_lb12_u(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q2);
                 else lbh = box_lb_u<D>(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q);
@@ -766,7 +586,6 @@ __global__ __launch_bounds__(64 * kGWaves) __attribute__((amdgpu_waves_per_eu(SE
                 if (W == 0ull) continue;
                 w = __popcll(W);
             }
-            ++n_leaf;
 #ifdef SE3ICP_PROF
             n_want += __popcll(W & __ballot(valid));
             ++n_leafv;
@@ -786,7 +605,7 @@ __global__ __launch_bounds__(64 * kGWaves) __attribute__((amdgpu_waves_per_eu(SE
             const unsigned long long c_l1 = __builtin_amdgcn_s_memtime();
             c_lload += c_l1 - c_l0;
 #endif
-            if (w > (D == 12 ? SE3ICP_NN_COMPACT : SE3ICP_NN_COMPACT3)) {
+            if (w > kCompact) {
                 // every lane sweeps every target (broadcast LDS reads)
                 for (int j = 0; j < cnt; ++j) {
                     float acc;
@@ -810,23 +629,23 @@ __global__ __launch_bounds__(64 * kGWaves) __attribute__((amdgpu_waves_per_eu(SE
                 // up to 64), 4 targets per lane, then a top-2 merge over the LPQ lanes and
                 // into the query's own lane
                 if ((W >> lane) & 1ull)
-                    s_wl[wid][__builtin_amdgcn_mbcnt_hi((unsigned)(W >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)W, 0u))] = lane;
+                    s_wl[__builtin_amdgcn_mbcnt_hi((unsigned)(W >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)W, 0u))] = lane;
                 __builtin_amdgcn_wave_barrier();
-                constexpr int kL32 = 32 / SE3ICP_NN_TPL, kL64 = 64 / SE3ICP_NN_TPL;  // lanes per query
-                if (cnt <= 32) compact_sweep<D, kL32>(tile, s_q[wid], s_wl[wid], s_r1[wid], s_r2[wid], s_rb[wid], w, cnt, ta, lane);
-                else compact_sweep<D, kL64>(tile, s_q[wid], s_wl[wid], s_r1[wid], s_r2[wid], s_rb[wid], w, cnt, ta, lane);
+                constexpr int kL32 = 32 / kTPL, kL64 = 64 / kTPL;  // lanes per query
+                if (cnt <= 32) compact_sweep<D, kL32>(tile, s_q, s_wl, s_r1, s_r2, s_rb, w, cnt, ta, lane);
+                else compact_sweep<D, kL64>(tile, s_q, s_wl, s_r1, s_r2, s_rb, w, cnt, ta, lane);
                 __builtin_amdgcn_wave_barrier();
                 if ((W >> lane) & 1ull) {
-                    const float r1 = s_r1[wid][lane], r2 = s_r2[wid][lane];
-                    const int rb = s_rb[wid][lane];
+                    const float r1 = s_r1[lane], r2 = s_r2[lane];
+                    const int rb = s_rb[lane];
                     d2 = fminf(fmaxf(d1, r1), fminf(d2, r2));
                     i1 = r1 < d1 ? rb : i1;
                     d1 = fminf(d1, r1);
                 }
                 __builtin_amdgcn_wave_barrier();
                 {  // 64-lane evaluation slots issued
-                    const int qpi = 64 / (cnt <= 32 ? 32 / SE3ICP_NN_TPL : 64 / SE3ICP_NN_TPL);
-                    n_eval += SE3ICP_NN_TPL * ((w + qpi - 1) / qpi);
+                    const int qpi = 64 / (cnt <= 32 ? 32 / kTPL : 64 / kTPL);
+                    n_eval += kTPL * ((w + qpi - 1) / qpi);
                 }
             }
             if ((int)valid & (int)(d1 < INFINITY)) thr = fminf(thr, widen(d1, d2));
@@ -835,41 +654,6 @@ __global__ __launch_bounds__(64 * kGWaves) __attribute__((amdgpu_waves_per_eu(SE
 #endif
             continue;
         }
-#if SE3ICP_NN_TWOLEVEL
-        if (2 * h + 2 < first_leaf) {
-            // Both children are interior: test the four grandchildren (4h+3 .. 4h+6, one
-            // contiguous box run) instead, so the wave's dependent chain of box loads is one
-            // round trip per two levels.  A child's box lies inside its parent's, so a
-            // grandchild that passes implies its parent would have; exactness is unchanged
-            // (pruning stays conservative, leaves are re-tested when popped).
-            n_box += 4;
-            const int g0 = 4 * h + 3;
-            float lg[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if constexpr (D == 12) lg[k] = box_lb12_u(box_lo + (size_t)(g0 + k) * D, box_hi + (size_t)(g0 + k) * D, q2);
-                else lg[k] = box_lb_u<D>(box_lo + (size_t)(g0 + k) * D, box_hi + (size_t)(g0 + k) * D, q);
-            }
-            bool vg[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) vg[k] = __ballot(lg[k] * (1.f - 2e-6f) < thr) != 0ull;
-            // near-first order by lane 0's bounds: the nearer child (min of its two
-            // grandchildren), within it the nearer grandchild; pushed far-first (LIFO)
-            const int o = __builtin_amdgcn_readfirstlane(((fminf(lg[0], lg[1]) <= fminf(lg[2], lg[3])) ? 0 : 2) |
-                                                         ((lg[0] <= lg[1]) ? 0 : 4) | ((lg[2] <= lg[3]) ? 0 : 8));
-            const int cn = o & 2, cf = 2 - cn;  // first grandchild index of the near / far child
-            const int fn = (cn == 0) ? ((o >> 2) & 1) : ((o >> 3) & 1);  // near child's nearer grandchild (0/1)
-            const int ff = (cf == 0) ? ((o >> 2) & 1) : ((o >> 3) & 1);
-            const int order[4] = {cf + 1 - ff, cf + ff, cn + 1 - fn, cn + fn};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int gk = order[k];
-                const bool vk = gk == 0 ? vg[0] : gk == 1 ? vg[1] : gk == 2 ? vg[2] : vg[3];
-                if (vk) { stk = (lane == sp) ? g0 + gk : stk; ++sp; }
-            }
-            continue;
-        }
-#endif
         n_box += 2;
         const int hl = 2 * h + 1, hr = 2 * h + 2;
         float ll, lr;
@@ -895,7 +679,6 @@ __global__ __launch_bounds__(64 * kGWaves) __attribute__((amdgpu_waves_per_eu(SE
         atomicAdd(st, 64ull * n_eval);
         atomicAdd(st + 1, 64ull * n_box);
         // the wave's work (box-test steps + leaf sweeps): the chunk's cost for k_nn_order
-        if (SE3ICP_NN_ORDER) atomicMax(v.chunk_cost + c, n_box / 2u + 4u * n_leaf);
 #ifdef SE3ICP_PROF
         if (D == 12) {
             atomicAdd(v.stats + kStatCols * (gi & 63) + 8, (unsigned long long)n_want);
@@ -912,9 +695,6 @@ __global__ __launch_bounds__(64 * kGWaves) __attribute__((amdgpu_waves_per_eu(SE
         }
 #endif
     }
-#if SE3ICP_NN_EJECT
-    if (ejected) return;  // (searched again by k_nn_single)
-#endif
     if (!valid) return;
     // certification (see the header) and the stored distance
     const bool flag = (bool)((int)(i1 < 0) | (int)!(d2 - d1 > 2.f * f32_err(d2, na, nb, D)));
@@ -1074,18 +854,17 @@ __global__ __launch_bounds__(256) void k_nn_single(View v) {
 
 void launch_nn_prep(const View& v, hipStream_t s) {
     hipLaunchKernelGGL(k_nn_prep, dim3(v.nchunks), dim3(kChunkQ), 0, s, v);
-    if (SE3ICP_NN_ORDER) hipLaunchKernelGGL(k_nn_order, dim3(1), dim3(1024), 0, s, v.chunk_cost, v.chunk_order, v.nchunks);
 }
-// 16 groups of 64 per chunk, kGWaves groups per block
-// and the single-query kernel over a fixed grid (SE3ICP_NN_SINGLE_BLOCKS x 4 waves)
+// 16 groups of 64 per chunk, one wave per group
+// and the single-query kernel over a fixed grid (kSingleBlocks x 4 waves)
 void launch_nn_se3(const View& v, hipStream_t s) {
-    hipLaunchKernelGGL(k_nn_group<12>, dim3(v.nchunks * (kChunkQ / 64) * SE3ICP_NN_SPLIT / kGWaves), dim3(64 * kGWaves), 0,
+    hipLaunchKernelGGL(k_nn_group<12>, dim3(v.nchunks * (kChunkQ / 64)), dim3(64), 0,
                        s, v);
-    hipLaunchKernelGGL(k_nn_single<12>, dim3(SE3ICP_NN_SINGLE_BLOCKS), dim3(256), 0, s, v);
+    hipLaunchKernelGGL(k_nn_single<12>, dim3(kSingleBlocks), dim3(256), 0, s, v);
 }
 void launch_nn_r3(const View& v, hipStream_t s) {
-    hipLaunchKernelGGL(k_nn_group<3>, dim3(v.nchunks * (kChunkQ / 64) / kGWaves), dim3(64 * kGWaves), 0, s, v);
-    hipLaunchKernelGGL(k_nn_single<3>, dim3(SE3ICP_NN_SINGLE_BLOCKS), dim3(256), 0, s, v);
+    hipLaunchKernelGGL(k_nn_group<3>, dim3(v.nchunks * (kChunkQ / 64)), dim3(64), 0, s, v);
+    hipLaunchKernelGGL(k_nn_single<3>, dim3(kSingleBlocks), dim3(256), 0, s, v);
 }
 
 }  // namespace se3icp

@@ -497,9 +497,10 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(TreeView t, int l
 // position, the 22-bit key over its widest extent, the median by two 11-bit histograms,
 // the stable left / tie / right partition), with LDS histograms and one block scan instead
 // of device-wide passes.  A node's points are read as wave-contiguous 64-position chunks.
-#ifndef SE3ICP_TREE_WG_MIN
-#define SE3ICP_TREE_WG_MIN 64  // levels with at least this many nodes (over all clouds) use k_tree_level
-#endif
+// levels with at least this many nodes (over all clouds) use k_tree_level (32 / 64 / 128:
+// 64 best; one launch with a grid-barrier per node for the levels above measured slower:
+// ~17 us per cross-XCD node barrier)
+constexpr int kTreeWgMin = 64;
 constexpr int kLevThreads = 1024, kLevWaves = kLevThreads / 64;
 constexpr int kLevU = 16;  // loads in flight per thread in the passes over a node
 
@@ -744,10 +745,7 @@ __global__ __launch_bounds__(kLevThreads) void k_tree_level(TreeView t, int leve
 // inverse, the tree-ordered f32 (and f64) vectors, and the boxes of every leaf and inner
 // node below level G.  s_val holds level-G positions e (s_p[e]: the point); ties in the
 // wave sorts are broken by the point index, as when s_val held the points.
-#ifndef SE3ICP_LOCAL_MAX
-#define SE3ICP_LOCAL_MAX 4096
-#endif
-constexpr int kLocalMax = SE3ICP_LOCAL_MAX;  // power of two
+constexpr int kLocalMax = 4096;  // power of two
 constexpr int kWaveSortPer = 8;  // sub-nodes of <= 512 points: register sort by one wave
 constexpr int kLocalThreads = 512;
 static_assert(kLocalMax <= 4096, "wave-sort keys carry the position in 12 bits");
@@ -1264,7 +1262,7 @@ int build_trees(TreeView t, void* tmp, size_t tmp_bytes, uint32_t* qbuf, int32_t
     tc.perm = (G % 2 == 0) ? final_perm : perm_alt;
     int32_t* other = (G % 2 == 0) ? perm_alt : final_perm;
     int H = 0;  // levels of the multi-pass path (k_tree_bbox / k_part_*)
-    while (H < G && (t.nclouds << H) < SE3ICP_TREE_WG_MIN) ++H;
+    while (H < G && (t.nclouds << H) < kTreeWgMin) ++H;
     hipLaunchKernelGGL(k_tree_init, dim3(gfill), dim3(256), 0, s, tc, other, (1 << H) - 1);
     if (ps.overflow_words) hipLaunchKernelGGL(k_clear_words, dim3(256), dim3(256), 0, s, ps.overflow, ps.overflow_words);
     const int nblk = (t.npts + kPartElems - 1) / kPartElems;

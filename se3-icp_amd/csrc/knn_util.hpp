@@ -10,10 +10,6 @@
 namespace se3icp {
 namespace knn {
 
-#ifndef SE3ICP_LRF_ORDER
-#define SE3ICP_LRF_ORDER 2
-#endif
-
 __device__ __forceinline__ double l2_3(double ax, double ay, double az, double bx, double by, double bz) {
 #pragma clang fp contract(off)
     const double d0 = ax - bx, d1 = ay - by, d2 = az - bz;
@@ -29,32 +25,17 @@ __device__ __forceinline__ bool key_le(double da, int ia, double db, int ib) {
     return (bool)((int)(da < db) | ((int)(da == db) & (int)(ia <= ib)));
 }
 
-#ifndef SE3ICP_LRF_TIGHT
-#define SE3ICP_LRF_TIGHT 0
-#endif
-#ifndef SE3ICP_LRF_XCD
-#define SE3ICP_LRF_XCD 1
-#endif
-#ifndef SE3ICP_LRF_FASTSORT
-#define SE3ICP_LRF_FASTSORT 1
-#endif
-
 // Set bits of a wave-uniform 64-bit mask in outward order from position p (p may lie
-// outside [0, 64)): p, p+1, p-1, p+2, p-2, ... (ORDER 2), or ascending (ORDER 0).
+// outside [0, 64)): p, p+1, p-1, p+2, p-2, ... (nearest-first by a wave minimum per step
+// and plain ascending order were measured slower).
 // Neighbouring leaves in tree order are neighbours in space, so the bound tightens early.
 struct OutwardBits {
     unsigned long long up, dn;
     bool flip = false;
     __device__ OutwardBits(unsigned long long m, int p) {
-#if SE3ICP_LRF_ORDER == 2
         if (p < 0) { up = m; dn = 0ull; }
         else if (p >= 64) { up = 0ull; dn = m; }
         else { dn = m & ((1ull << p) - 1ull); up = m & ~((1ull << p) - 1ull); }
-#else
-        (void)p;
-        up = m;
-        dn = 0ull;
-#endif
     }
     __device__ int next() {
         const bool use_up = up != 0ull && (dn == 0ull || !flip);

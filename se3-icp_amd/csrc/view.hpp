@@ -82,8 +82,6 @@ struct View {
     int32_t nchunks;      // npairs << CL
     int32_t* qlist;       // [nchunks * kChunkQ] global slots of the searched queries, tree order
     int32_t* qcount;      // [nchunks][16] lanes of each group (0: none)
-    uint32_t* chunk_cost; // [nchunks] work of the chunk's longest group wave in its last search (k_nn_group)
-    int32_t* chunk_order; // [nchunks] dispatch order of k_nn_group: costliest chunks first (k_nn_order)
     int32_t* sq_list;     // [ld] queries of sparse chunks (global source tree slots) for k_nn_single:
                           // SE(3) phase from the front (count flag_count[1]), R3 from the back ([2])
     const double* hist;   // [kHist][npairs][12] pose T used at iteration k, row k % kHist
