@@ -749,6 +749,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
                 const double nw = std::floor(d[11] / 17592186044416.0), dt = d[11] - nw * 17592186044416.0;
                 std::fprintf(stderr, "[nn] iter %d: %.0f SE(3) group waves, mean %.1f us, summed %.1f ms (100 MHz clock)\n",
                              it, nw, nw > 0 ? dt / nw / 100.0 : 0.0, dt / 1e5);
+                std::fprintf(stderr, "[nn] iter %d: k_nn_prep span %.1f us\n", it, nn_prep_span());
                 std::fprintf(stderr, "[nn] iter %d: wave cycles in leaf visits %.1f %% (target loads %.1f %%), "
                              "%.0f cycles per leaf visit, %.0f per box-test step\n", it, 100.0 * d[12] / std::max(1.0, d[13]),
                              100.0 * d[14] / std::max(1.0, d[13]), d[12] / std::max(1.0, d[9]),
@@ -821,6 +822,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
             const double nw = std::max(1.0, std::floor(sum[11] / 17592186044416.0));
             const double mean = std::fmod(sum[11], 17592186044416.0) / nw;  // 100 MHz ticks
             const double sq = (double)stats[kStatCols + 10] / nw;
+            nn_prof_report();
             std::fprintf(stderr, "[prof] nn12: leaf visits %.0f; %.0f group waves, %.1f us each on average (sd %.1f, "
                          "longest %.1f us; 100 MHz clock)\n",
                          sum[9], nw, mean / 100.0, std::sqrt(std::max(0.0, sq - mean * mean)) / 100.0,

@@ -27,6 +27,8 @@
 //   and among the visited ones the gap d2 - d1 must exceed 2 err(d2).
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+
 #include "loopdev.hpp"
 #include "wave.hpp"
 #include "tree.hpp"
@@ -336,8 +338,17 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
 // for k_nn_group: consecutive leaves' remaining queries share a 64-lane group as long as
 // they fit, a leaf is never split (with every query searched, a group is one leaf).
 // qlist[c][j][lane] = local tree position, qcount[c][j] = lanes of group j.
+#ifdef SE3ICP_PROF
+// k_nn_prep block phases (100 MHz clock), summed over blocks: settle, pack, lists; blocks;
+// and the span of each launch (latest end - earliest start), summed over launches
+__device__ unsigned long long g_prep_prof[6];
+__device__ unsigned long long g_prep_span[2] = {~0ull, 0ull};
+#endif
 // (8 waves per SIMD: two 1024-thread blocks per CU, <= 64 VGPRs)
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_nn_prep(View v) {
+#ifdef SE3ICP_PROF
+    const unsigned long long tp0 = __builtin_amdgcn_s_memrealtime();
+#endif
     constexpr int NL = kChunkQ / 64;  // leaves (groups) per chunk
     __shared__ int s_cnt[NL], s_slot[NL], s_base[NL], s_wc[NL], s_single;
     const int c = xcd_block_runs(blockIdx.x, gridDim.x, kXcdRun / 16);  // (k_nn_group's chunk runs)
@@ -367,36 +378,48 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     const unsigned long long m = __ballot(active);
     if (lane == 0) s_wc[wid] = __popcll(m);
     __syncthreads();
-    if (threadIdx.x == 0) {  // greedy packing of whole leaves into groups of <= 64
-        int cur = 0, grp = 0, base = 0, total = 0;
-        int gcnt[NL];
+#ifdef SE3ICP_PROF
+    const unsigned long long tp1 = __builtin_amdgcn_s_memrealtime();
+#endif
+    if (wid == 0) {
+        // greedy packing of whole leaves into groups of <= 64: the 16 leaf counts in a VGPR,
+        // the sequential pass in scalar registers (no LDS round trip per leaf)
+        const int cnt_l = lane < NL ? s_cnt[lane] : 0;
+        int cur = 0, grp = 0, base = 0;
+        int slot_l = 0, base_l = 0, gcnt_l = 0;
 #pragma unroll
-        for (int j = 0; j < NL; ++j) gcnt[j] = 0;
         for (int j = 0; j < NL; ++j) {
-            const int n = s_cnt[j];
+            const int n = __builtin_amdgcn_readlane(cnt_l, j);
             if (cur + n > 64) { ++grp; cur = 0; }
-            s_slot[j] = 64 * grp + cur;
-            s_base[j] = base;
-            gcnt[grp] += n;
+            if (lane == j) { slot_l = 64 * grp + cur; base_l = base; }
+            if (lane == grp) gcnt_l += n;
             cur += n;
             base += n;
         }
-        total = base;
+        const int total = base;
         // a sparse chunk goes to the one-query-per-wave kernel instead (SE(3) list from the
         // front of sq_list, R3 from the back)
         const bool dense = total >= kDense;
-        s_single = -1;
-        if ((int)!dense & (int)(total > 0)) s_single = atomicAdd(&v.flag_count[phase == PHASE_SE3 ? 1 : 2], total);
-        for (int j = 0; j < NL; ++j) v.qcount[c * NL + j] = dense ? gcnt[j] : 0;
-        if (phase != PHASE_IDLE) {  // work counters: queries / searched queries per phase
-            unsigned long long* st = v.stats + kStatCols * (c & 63) + (phase == PHASE_SE3 ? 4 : 6);
-            const CloudDev cs = v.clouds[P->src];
-            const int ci = c & ((1 << v.chunk_level) - 1);
-            atomicAdd(st, (unsigned long long)(tree_first(cs.n, v.chunk_level, ci + 1) - tree_first(cs.n, v.chunk_level, ci)));
-            atomicAdd(st + 1, (unsigned long long)total);
+        if (lane < NL) {
+            s_slot[lane] = slot_l;
+            s_base[lane] = base_l;
+            v.qcount[c * NL + lane] = dense ? gcnt_l : 0;
+        }
+        if (lane == 0) {
+            s_single = ((int)!dense & (int)(total > 0)) ? atomicAdd(&v.flag_count[phase == PHASE_SE3 ? 1 : 2], total) : -1;
+            if (phase != PHASE_IDLE) {  // work counters: queries / searched queries per phase
+                unsigned long long* st = v.stats + kStatCols * (c & 63) + (phase == PHASE_SE3 ? 4 : 6);
+                const CloudDev cs = v.clouds[P->src];
+                const int ci = c & ((1 << v.chunk_level) - 1);
+                atomicAdd(st, (unsigned long long)(tree_first(cs.n, v.chunk_level, ci + 1) - tree_first(cs.n, v.chunk_level, ci)));
+                atomicAdd(st + 1, (unsigned long long)total);
+            }
         }
     }
     __syncthreads();
+#ifdef SE3ICP_PROF
+    const unsigned long long tp2 = __builtin_amdgcn_s_memrealtime();
+#endif
     if (active) {
         int r = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
         for (int w = 0; w < wid; ++w) r += s_wc[w];
@@ -409,6 +432,18 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
             else v.sq_list[v.ld - 1 - (sb + r)] = gxs;
         }
     }
+#ifdef SE3ICP_PROF
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long tp3 = __builtin_amdgcn_s_memrealtime();
+        atomicAdd(&g_prep_prof[0], tp1 - tp0);
+        atomicAdd(&g_prep_prof[1], tp2 - tp1);
+        atomicAdd(&g_prep_prof[2], tp3 - tp2);
+        atomicAdd(&g_prep_prof[3], 1ull);
+        atomicMin(&g_prep_span[0], tp0);
+        atomicMax(&g_prep_span[1], tp3);
+    }
+#endif
 }
 
 // Results of a searched query (one lane): the recheck flag, the certificate, the
@@ -852,6 +887,27 @@ __global__ __launch_bounds__(256) void k_nn_single(View v) {
 
 }  // namespace
 
+void nn_prof_report() {
+#ifdef SE3ICP_PROF
+    unsigned long long h[6];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_prep_prof), sizeof(h)) != hipSuccess) return;
+    if (h[3])
+        std::fprintf(stderr, "[prof] k_nn_prep per block: settle %.2f pack %.2f lists %.2f us (%llu blocks)\n",
+                     h[0] / 100.0 / h[3], h[1] / 100.0 / h[3], h[2] / 100.0 / h[3], h[3]);
+    const unsigned long long z[6] = {0, 0, 0, 0, 0, 0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_prep_prof), z, sizeof(z));
+#endif
+}
+#ifdef SE3ICP_PROF
+// span of the last k_nn_prep launch (us), reset for the next
+double nn_prep_span() {
+    unsigned long long h[2];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_prep_span), sizeof(h)) != hipSuccess) return 0.0;
+    const unsigned long long z[2] = {~0ull, 0ull};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_prep_span), z, sizeof(z));
+    return h[1] > h[0] ? (h[1] - h[0]) / 100.0 : 0.0;
+}
+#endif
 void launch_nn_prep(const View& v, hipStream_t s) {
     hipLaunchKernelGGL(k_nn_prep, dim3(v.nchunks), dim3(kChunkQ), 0, s, v);
 }

@@ -138,6 +138,10 @@ void launch_knn_big(const View& v, int write_knn, int k_min, const int32_t* qlis
 // certificate still holds and lists the rest, k_nn_group sweeps those 64 per wavefront
 // through the target kd-tree (12-D in the SE(3) phase, 3-D in the R3 phase)
 void launch_nn_prep(const View& v, hipStream_t s);
+void nn_prof_report();  // (SE3ICP_PROF builds: k_nn_prep block phases, then reset)
+#ifdef SE3ICP_PROF
+double nn_prep_span();  // span of the last k_nn_prep launch (us)
+#endif
 void launch_nn_se3(const View& v, hipStream_t s);
 void launch_nn_r3(const View& v, hipStream_t s);
 void launch_recheck(const View& v, int nblocks, hipStream_t s);
