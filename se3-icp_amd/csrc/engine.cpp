@@ -255,7 +255,7 @@ int Engine::build_tree(int D, const float* vec, hipStream_t s, const double* vec
     const size_t nb = (size_t)nclouds_ * nnodes * D;
     if (!ensure<uint32_t>(tb.blo, nb) || !ensure<uint32_t>(tb.bhi, nb) || !ensure<float>(tb.lo, nb) ||
         !ensure<float>(tb.hi, nb) || !ensure<float>(tb.scr, (size_t)D * ld_) ||
-        (vec64 && !ensure<double>(tb.vec64, (size_t)D * ld_)) ||
+        (vec64 && !ensure<double>(tb.vec64, (size_t)3 * ld_)) ||
         (vec64 && D == 3 && !ensure<double4>(tb.vec64a, (size_t)ld_)))
         return SE3ICP_ERR_OUT_OF_MEMORY;
     std::vector<int32_t> host_n(nclouds_);

@@ -218,9 +218,19 @@ __device__ __forceinline__ void load_hist(const View& v, int iter, int pair, dou
 // f64 source element / point at global tree slot gx (the tree-ordered f64 copy: queries of
 // a chunk read contiguous memory)
 template <int D>
-__device__ __forceinline__ void load_m0(const View& v, const TreeRef& TR, int gx, double* m) {
+__device__ __forceinline__ void load_m0(const View& v, const TreeRef& TR, int gx, int g, double* m) {
+    if constexpr (D == 12) {  // the point's 96-B frame row (the 12-D tree keeps only the translation rows in tree order)
+        const double2* r2 = reinterpret_cast<const double2*>(v.fr64 + (size_t)g * 12);
 #pragma unroll
-    for (int r = 0; r < D; ++r) m[r] = TR.tvec64[(size_t)r * v.ld + gx];
+        for (int k = 0; k < 6; ++k) {
+            const double2 x = r2[k];
+            m[2 * k] = x.x;
+            m[2 * k + 1] = x.y;
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < D; ++r) m[r] = TR.tvec64[(size_t)r * v.ld + gx];
+    }
 }
 template <int D>
 __device__ __forceinline__ void pose_m0(const double* T, const double* m, double* q) {
@@ -253,7 +263,7 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
                                             const CloudDev& ct, int gx, int g, double a2) {
     double mt[3], T[12], Qt[3];
 #pragma unroll
-    for (int r = 0; r < 3; ++r) mt[r] = TR.tvec64[(size_t)(D - 3 + r) * v.ld + gx];
+    for (int r = 0; r < 3; ++r) mt[r] = TR.tvec64[(size_t)r * v.ld + gx];  // (3 rows: points / translations)
     load_T(P, T);
     pose_point(T, mt[0], mt[1], mt[2], Qt);
     const double rot2 = 3.0 * a2 * (1.0 + 1e-12);  // |rotation columns|^2 (12-D), 0 (3-D)
@@ -296,7 +306,7 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
     // is valid; a near one spares the group walk the nodes an infinite threshold opens.
     if ((int)(v.corr_idx[g] < 0) & (int)(ct.n > 0)) {
         double m0[D], Q[D];
-        load_m0<D>(v, TR, gx, m0);
+        load_m0<D>(v, TR, gx, g, m0);
         pose_m0<D>(T, m0, Q);
         float qf[D];
 #pragma unroll
@@ -474,8 +484,8 @@ __device__ __forceinline__ void nn_finish(const View& v, const PairDev* P, int p
     // the stored distance needs the translation part of the query only (ISR.cpp:465-468)
     double Tm[12], Q12[12];
     load_T(P, Tm);
-    const double* m = TR.tvec64 + gx;
-    pose_point(Tm, m[(size_t)(D - 3) * v.ld], m[(size_t)(D - 2) * v.ld], m[(size_t)(D - 1) * v.ld], Q12 + D - 3);
+    const double* m = TR.tvec64 + gx;  // (3 rows: points / translations)
+    pose_point(Tm, m[0], m[v.ld], m[2 * (size_t)v.ld], Q12 + D - 3);
     v.corr_dist[g] = stored_dist(v, D == 12 ? PHASE_SE3 : PHASE_R3, ct, Q12, i1);
 }
 
@@ -539,7 +549,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kWpe))) void
         double Tm[12], Q[D];
         load_T(P, Tm);
         double m0[D];
-        load_m0<D>(v, TR, gx, m0);
+        load_m0<D>(v, TR, gx, g, m0);
         pose_m0<D>(Tm, m0, Q);
         double n2 = 0;
 #pragma unroll
@@ -751,7 +761,7 @@ __device__ __forceinline__ void single_one(const View& v, const PairDev* P, int 
     {
         double Tm[12], m0[D], Q[D];
         load_T(P, Tm);
-        load_m0<D>(v, TR, gx, m0);
+        load_m0<D>(v, TR, gx, g, m0);
         pose_m0<D>(Tm, m0, Q);
         double n2 = 0;
 #pragma unroll

@@ -497,10 +497,12 @@ __global__ __launch_bounds__(kPartThreads) void k_part_scatter(TreeView t, int l
 // position, the 22-bit key over its widest extent, the median by two 11-bit histograms,
 // the stable left / tie / right partition), with LDS histograms and one block scan instead
 // of device-wide passes.  A node's points are read as wave-contiguous 64-position chunks.
-// levels with at least this many nodes (over all clouds) use k_tree_level (32 / 64 / 128:
-// 64 best; one launch with a grid-barrier per node for the levels above measured slower:
-// ~17 us per cross-XCD node barrier)
-constexpr int kTreeWgMin = 64;
+// levels with at least this many nodes (over all clouds) use k_tree_level (32 / 64 / 128
+// within noise of each other at C4; 32 leaves only the root level to the nine-launch
+// multi-pass path: 16 tree launches per tree; 16 was slower -- a 120k-point root in one
+// workgroup; one launch with a grid barrier per node for the top levels measured slower
+// too: ~17 us per cross-XCD node barrier)
+constexpr int kTreeWgMin = 32;
 constexpr int kLevThreads = 1024, kLevWaves = kLevThreads / 64;
 constexpr int kLevU = 16;  // loads in flight per thread in the passes over a node
 
@@ -1050,14 +1052,12 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
 #pragma unroll
             for (int d = 0; d < D; ++d) t.tvec[(size_t)d * ld + g] = v[d];
             if (want64) {
-                if constexpr (D == 12) {
-                    const double2* r64 = reinterpret_cast<const double2*>(t.vec64 + (size_t)src * 12);
-#pragma unroll
-                    for (int k = 0; k < 6; ++k) {
-                        const double2 w = r64[k];
-                        t.tvec64[(size_t)(2 * k) * ld + g] = w.x;
-                        t.tvec64[(size_t)(2 * k + 1) * ld + g] = w.y;
-                    }
+                if constexpr (D == 12) {  // the translation rows only (the loop reads the frames by point)
+                    const double* r64 = t.vec64 + (size_t)src * 12 + 9;
+                    const double2 w01 = *reinterpret_cast<const double2*>(r64);
+                    t.tvec64[g] = w01.x;
+                    t.tvec64[ld + g] = w01.y;
+                    t.tvec64[2 * ld + g] = r64[2];
                 } else {
                     double w[3] = {0.0, 0.0, 0.0};
 #pragma unroll
@@ -1071,9 +1071,9 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
         for (int d = 0; d < D; ++d) {
             float lo = in ? v[d] : INFINITY, hi = in ? v[d] : -INFINITY;
 #pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) {
-                lo = fminf(lo, __shfl_xor(lo, o, 64));
-                hi = fmaxf(hi, __shfl_xor(hi, o, 64));
+            for (int o = 32; o >= 1; o >>= 1) {  // (DPP / swizzle / permlane exchanges)
+                lo = fminf(lo, xor_lane(lo, o));
+                hi = fmaxf(hi, xor_lane(hi, o));
             }
             if (lo <= hi) {
                 lo = lo - (fabsf(lo) * 4.8e-7f + 1e-30f);
@@ -1126,14 +1126,9 @@ __global__ __launch_bounds__(256) void k_tree_finish(TreeView t) {
                 t.tvec[(size_t)(4 * k + 2) * t.ld + g] = x.z;
                 t.tvec[(size_t)(4 * k + 3) * t.ld + g] = x.w;
             }
-            if (want64) {
-                const double2* r64 = reinterpret_cast<const double2*>(t.vec64 + (size_t)src * 12);
-#pragma unroll
-                for (int k = 0; k < 6; ++k) {
-                    const double2 x = r64[k];
-                    t.tvec64[(size_t)(2 * k) * t.ld + g] = x.x;
-                    t.tvec64[(size_t)(2 * k + 1) * t.ld + g] = x.y;
-                }
+            if (want64) {  // the translation rows only
+                const double* r64 = t.vec64 + (size_t)src * 12 + 9;
+                for (int k = 0; k < 3; ++k) t.tvec64[(size_t)k * t.ld + g] = r64[k];
             }
         } else {
             for (int d = 0; d < t.D; ++d) t.tvec[(size_t)d * t.ld + g] = t.vec[(size_t)d * t.ld + src];

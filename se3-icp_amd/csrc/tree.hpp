@@ -28,7 +28,8 @@ struct TreeView {
     int32_t* pos;      // [ld] point (global slot) -> local tree position
     float* tvec;       // [D][ld] vectors in tree order
     const double* vec64;  // optional f64 vectors (original order, the layout of vec) ...
-    double* tvec64;       // ... copied into tree order (coalesced leaf / query-chunk loads)
+    double* tvec64;       // ... copied into tree order (coalesced leaf / query-chunk loads): [3][ld], the
+                          // points (3-D) or the translation rows (12-D: the loop reads whole frames by point)
     double4* tpt64;       // 3-D: the tree-ordered f64 points as (x, y, z, 0) records (one line per gather)
     int32_t vec64_sources_only;  // copy the f64 vectors of even (source) clouds only
     uint32_t* blo;     // [nclouds][nnodes][D] build scratch (orderable bits)

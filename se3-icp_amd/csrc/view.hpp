@@ -32,7 +32,7 @@ struct TreeRef {
     const int32_t* perm;  // [ld] tree position (cloud.off + x) -> local point index
     const int32_t* pos;   // [ld] point (cloud.off + i) -> local tree position
     const float* tvec;    // [D][ld] vectors in tree order
-    const double* tvec64; // [D][ld] f64 vectors in tree order (3-D trees only)
+    const double* tvec64; // [3][ld] f64 in tree order: the points (3-D), the frames' translation rows (12-D)
     const double4* tpt64; // [ld] the same, one (x, y, z, 0) record per point (3-D trees: the setup's gathers)
     const float* lo;      // [nclouds][nnodes][D]
     const float* hi;
