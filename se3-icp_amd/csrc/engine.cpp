@@ -750,6 +750,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
                 std::fprintf(stderr, "[nn] iter %d: %.0f SE(3) group waves, mean %.1f us, summed %.1f ms (100 MHz clock)\n",
                              it, nw, nw > 0 ? dt / nw / 100.0 : 0.0, dt / 1e5);
                 std::fprintf(stderr, "[nn] iter %d: k_nn_prep span %.1f us\n", it, nn_prep_span());
+                nn_wave_report(it);
                 std::fprintf(stderr, "[nn] iter %d: wave cycles in leaf visits %.1f %% (target loads %.1f %%), "
                              "%.0f cycles per leaf visit, %.0f per box-test step\n", it, 100.0 * d[12] / std::max(1.0, d[13]),
                              100.0 * d[14] / std::max(1.0, d[13]), d[12] / std::max(1.0, d[9]),

@@ -27,6 +27,7 @@
 //   and among the visited ones the gap d2 - d1 must exceed 2 err(d2).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 
 #include "loopdev.hpp"
@@ -353,6 +354,10 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
 // and the span of each launch (latest end - earliest start), summed over launches
 __device__ unsigned long long g_prep_prof[6];
 __device__ unsigned long long g_prep_span[2] = {~0ull, 0ull};
+// SE(3) group waves by duration (25 us bins, the last open): count and summed ticks; and
+// the launch span (earliest wave start, latest wave end)
+__device__ unsigned long long g_wave_hist[2][41];
+__device__ unsigned long long g_wave_span[2] = {~0ull, 0ull};
 #endif
 // (8 waves per SIMD: two 1024-thread blocks per CU, <= 64 VGPRs)
 __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_nn_prep(View v) {
@@ -734,6 +739,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kWpe))) void
                                         ((unsigned long long)min(n_leafv, 0x3fffu) << 6) | (n_valid % 64u));
             atomicAdd(v.stats + kStatCols + 10, dt * dt);                      // (spread)
             atomicAdd(v.stats + kStatCols * (gi & 63) + 11, (1ull << 44) + dt);  // waves, wave time
+            const int hb = min((int)(dt / 2500ull), 40);
+            atomicAdd(&g_wave_hist[0][hb], 1ull);
+            atomicAdd(&g_wave_hist[1][hb], dt);
+            atomicMin(&g_wave_span[0], t_w0);
+            atomicMax(&g_wave_span[1], t_w0 + dt);
             atomicAdd(v.stats + kStatCols * (gi & 63) + 12, c_leaf);   // shader cycles in leaf visits,
             atomicAdd(v.stats + kStatCols * (gi & 63) + 14, c_lload);  // in their target loads,
             atomicAdd(v.stats + kStatCols * (gi & 63) + 13, __builtin_amdgcn_s_memtime() - c_w0);  // in the wave
@@ -909,6 +919,24 @@ void nn_prof_report() {
 #endif
 }
 #ifdef SE3ICP_PROF
+// the SE(3) group waves since the last call: duration histogram (25 us bins: count, share of
+// the summed wave time) and the span from the first wave start to the last wave end; reset
+void nn_wave_report(int it) {
+    unsigned long long h[2][41], sp[2];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_wave_hist), sizeof(h)) != hipSuccess) return;
+    if (hipMemcpyFromSymbol(sp, HIP_SYMBOL(g_wave_span), sizeof(sp)) != hipSuccess) return;
+    double tot = 0, n = 0;
+    for (int b = 0; b < 41; ++b) { tot += (double)h[1][b]; n += (double)h[0][b]; }
+    std::fprintf(stderr, "[nn] iter %d: wave span %.1f us; summed wave time / 4096 slots %.1f us; durations (25 us bins):",
+                 it, sp[1] > sp[0] ? (sp[1] - sp[0]) / 100.0 : 0.0, tot / 100.0 / 4096.0);
+    for (int b = 0; b < 41; ++b)
+        if (h[0][b]) std::fprintf(stderr, " %d:%llu/%.1f%%", 25 * b, h[0][b], 100.0 * (double)h[1][b] / std::max(tot, 1.0));
+    std::fprintf(stderr, "\n");
+    unsigned long long z[2][41] = {};
+    const unsigned long long zs[2] = {~0ull, 0ull};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wave_hist), z, sizeof(z));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wave_span), zs, sizeof(zs));
+}
 // span of the last k_nn_prep launch (us), reset for the next
 double nn_prep_span() {
     unsigned long long h[2];

@@ -140,7 +140,8 @@ void launch_knn_big(const View& v, int write_knn, int k_min, const int32_t* qlis
 void launch_nn_prep(const View& v, hipStream_t s);
 void nn_prof_report();  // (SE3ICP_PROF builds: k_nn_prep block phases, then reset)
 #ifdef SE3ICP_PROF
-double nn_prep_span();  // span of the last k_nn_prep launch (us)
+double nn_prep_span();        // span of the last k_nn_prep launch (us)
+void nn_wave_report(int it);  // SE(3) group-wave durations since the last call
 #endif
 void launch_nn_se3(const View& v, hipStream_t s);
 void launch_nn_r3(const View& v, hipStream_t s);
