@@ -51,12 +51,6 @@ constexpr int kCap = 192; // candidates buffered per query (u32: cut key | candi
 // 16-lane bank group on 16 distinct slots of the 256-B bank row (conflict-free), and the
 // lane-major ds_read_b32 of an unaligned run is 4-way instead of 16-way
 constexpr int kStride = 196;
-#ifndef SE3ICP_LRF8_PREFETCH
-#define SE3ICP_LRF8_PREFETCH 1
-#endif
-#ifndef SE3ICP_LRF8_FMERGE
-#define SE3ICP_LRF8_FMERGE 1
-#endif
 constexpr int kLeaves = 64;              // leaves one wave may scan: candidate id = (list index << 6) | lane
 constexpr unsigned kIdBits = 0xfffu;     // low bits of a list entry: the candidate id
 // bound of the accept-all phase: every finite key (a lane past the leaf's end carries an
@@ -327,7 +321,6 @@ __device__ __forceinline__ bool final_group(unsigned* lists, const int* leaf_slo
     bool unsorted = false;
     {
         unsigned k32[16];
-#if SE3ICP_LRF8_FMERGE
         // fmode (wave-uniform): 0 a full sort; 1 the sorted prefix list[0 .. mv) (the last
         // tightening's kept set) merged with the tail appended since (<= 64 entries, sorted
         // first), as tighten_group_sorted merges; 2 the tail is empty (already in order)
@@ -355,10 +348,6 @@ __device__ __forceinline__ bool final_group(unsigned* lists, const int* leaf_slo
                 stage8<16, 128, 1>(k32, l);
             }
         }
-#else
-        load_head<16>(list, nbg, l, k32);
-        sort8<16>(k32, l);
-#endif
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
             const int e = l * 16 + s;
@@ -800,7 +789,6 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(6))) vo
     if (mode == 1 && !fb_wave) {
         __builtin_amdgcn_wave_barrier();
         int fmode = 0;
-#if SE3ICP_LRF8_FMERGE
         {
             int dmax = 0;
             bool anyz = false;
@@ -812,7 +800,6 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(6))) vo
             }
             fmode = anyz || dmax > 64 ? 0 : dmax == 0 ? 2 : 1;
         }
-#endif
         const bool exact = final_group(lists, leaves, P4, T.perm, qg.x, qg.y, qg.z, cl.off, g, l, nbg, mvv, fmode,
                                        min(nbg, max(kk, kn) + 1));
         fb_q = (bool)((int)!exact | (int)(nTop < Kw));
@@ -847,16 +834,10 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(6))) vo
             const int hi = min(rz, kk - 1);
             // (each iteration loads the next one's point first: the loads overlap the sums;
             // the last prefetch re-reads rank hi)
-            #if SE3ICP_LRF8_PREFETCH
             p3 pn = ld3(P4, (int)rl[max(min(1 + l, hi), 0)]);
-#endif
             for (int rk = 1 + l; rk <= hi; rk += 8) {
-                #if SE3ICP_LRF8_PREFETCH
                 const p3 p = pn;
                 pn = ld3(P4, (int)rl[min(rk + 8, hi)]);
-#else
-                const p3 p = ld3(P4, (int)rl[rk]);
-#endif
                 const double vx = p.x - qg.x, vy = p.y - qg.y, vz = p.z - qg.z;
                 if (rk < rz) { x[0] += vx; x[1] += vy; x[2] += vz; }
                 x[3] += vx; x[4] += vy; x[5] += vz;
@@ -887,16 +868,10 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(6))) vo
 #pragma unroll
         for (int i = 0; i < 9; ++i) x[i] = 0.0;
         if ((int)mine & (int)want_n) {  // EstimateNormals (ISR.cpp:643, :43): ranks 0 .. kn-1, self included
-            #if SE3ICP_LRF8_PREFETCH
             p3 pn = ld3(P4, (int)rl[max(min(l, kn - 1), 0)]);
-#endif
             for (int r = l; r < kn; r += 8) {
-                #if SE3ICP_LRF8_PREFETCH
                 const p3 p = pn;
                 pn = ld3(P4, (int)rl[min(r + 8, kn - 1)]);
-#else
-                const p3 p = ld3(P4, (int)rl[r]);
-#endif
                 const double px = p.x, py = p.y, pz = p.z;
                 x[0] += px; x[1] += py; x[2] += pz;
                 x[3] += px * px; x[4] += px * py; x[5] += px * pz;
@@ -1008,16 +983,10 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(6))) vo
             const double nx = pj[P8_ZN], ny = pj[P8_ZN + 1], nz = pj[P8_ZN + 2];
             const double R = pj[P8_R];
             const int kkq = (int)pj[P8_KK];
-            #if SE3ICP_LRF8_PREFETCH
             p3 pn = ld3(P4, (int)rl[max(min(1 + l, kkq - 1), 0)]);
-#endif
             for (int r = 1 + l; r < kkq; r += 8) {  // ranks 1 .. kk-1
-                #if SE3ICP_LRF8_PREFETCH
                 const p3 p = pn;
                 pn = ld3(P4, (int)rl[min(r + 8, kkq - 1)]);
-#else
-                const p3 p = ld3(P4, (int)rl[r]);
-#endif
                 const double vx = p.x - qg.x, vy = p.y - qg.y, vz = p.z - qg.z;
                 x6[0] += vx; x6[1] += vy; x6[2] += vz;
                 const double an = nx * vx + ny * vy + nz * vz;
