@@ -97,6 +97,9 @@ class Engine {
     bool profile_ = false;
     std::mutex mu_;
     hipStream_t stream_ = nullptr;
+    // the loop's second stream: the one-query-per-wave NN grids run on it beside the group
+    // grids (independent queries), forked after k_nn_prep and joined before k_recheck
+    hipStream_t side_ = nullptr;
     KernelTimes ktimes_;
 
     // geometry of the current batch
@@ -155,6 +158,7 @@ class Engine {
     // loop iterations in flight: kernel-time events and launched NN phases per ring slot
     static constexpr int kLoopRing = 4, kLoopEv = 7;
     hipEvent_t loop_ev_[kLoopRing * kLoopEv];
+    hipEvent_t fork_ev_[kLoopRing] = {}, join_ev_[kLoopRing] = {};  // (no timing)
     int loop_flags_[kLoopRing] = {};
     bool loop_detail_[kLoopRing] = {};
 };

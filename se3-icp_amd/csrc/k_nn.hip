@@ -956,6 +956,14 @@ void launch_nn_se3(const View& v, hipStream_t s) {
                        s, v);
     hipLaunchKernelGGL(k_nn_single<12>, dim3(kSingleBlocks), dim3(256), 0, s, v);
 }
+void launch_nn_group(const View& v, int D, hipStream_t s) {
+    if (D == 12) hipLaunchKernelGGL(k_nn_group<12>, dim3(v.nchunks * (kChunkQ / 64)), dim3(64), 0, s, v);
+    else hipLaunchKernelGGL(k_nn_group<3>, dim3(v.nchunks * (kChunkQ / 64)), dim3(64), 0, s, v);
+}
+void launch_nn_single(const View& v, int D, hipStream_t s) {
+    if (D == 12) hipLaunchKernelGGL(k_nn_single<12>, dim3(kSingleBlocks), dim3(256), 0, s, v);
+    else hipLaunchKernelGGL(k_nn_single<3>, dim3(kSingleBlocks), dim3(256), 0, s, v);
+}
 void launch_nn_r3(const View& v, hipStream_t s) {
     hipLaunchKernelGGL(k_nn_group<3>, dim3(v.nchunks * (kChunkQ / 64)), dim3(64), 0, s, v);
     hipLaunchKernelGGL(k_nn_single<3>, dim3(kSingleBlocks), dim3(256), 0, s, v);

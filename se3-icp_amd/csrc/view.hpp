@@ -145,6 +145,9 @@ void nn_wave_report(int it);  // SE(3) group-wave durations since the last call
 #endif
 void launch_nn_se3(const View& v, hipStream_t s);
 void launch_nn_r3(const View& v, hipStream_t s);
+// the two grids of a phase (D = 12 or 3) separately: the group grid, the one-query-per-wave grid
+void launch_nn_group(const View& v, int D, hipStream_t s);
+void launch_nn_single(const View& v, int D, hipStream_t s);
 void launch_recheck(const View& v, int nblocks, hipStream_t s);
 void launch_trim(const View& v, hipStream_t s);
 // reduce + (k_reduce_final) per-pair solve and loop state machine; next_phase[p] receives
