@@ -5,7 +5,7 @@
 # Usage: tools/profile_round.sh <tag>   -> gpurun_out/{bench,prof,pmc_*}_<tag>
 TAG=${1:-r01}
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
-B="python3 bench.py --steps 3 --warmup 1 --cpu-baseline off"
+B="python3 bench.py --steps 3 --warmup 1 --cpu-baseline off --secondary off"
 SQ1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU"
 SQ2="SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_SALU SQ_WAIT_INST_LDS"
 exec tools/gpu_step.sh \
