@@ -309,10 +309,11 @@ __device__ __forceinline__ p3 ld3(const double4* __restrict__ P4, int i) {
 // cut does not separate; the full keys ((f32 of the exact f64 distance, nanoflann's
 // arithmetic) << 32 | tree slot) of that order are put right by three odd-even
 // transposition passes and checked, and the tree slots are written back over the list in
-// rank order.  Returns false (the query goes to the exact kernel) when the order is still
-// wrong, or when two of the ranks the sums use share an f32 key and either their f64
-// distances differ or their point indices are out of order (the exact order is (f64
-// distance, point index): the reference's kNN and the exact kernel's).
+// rank order.  Two adjacent ranks the sums use that share an f32 key are put in the exact
+// order -- (f64 distance, point index): the reference's kNN and the exact kernel's -- by a
+// swap when no neighbouring rank shares their key.  Returns false (the query goes to the
+// exact kernel) when the order is still wrong, or when a run of three or more ranks shares
+// an f32 key and is not already in the exact order.
 __device__ __forceinline__ bool final_group(unsigned* lists, const int* leaf_slot, const double4* __restrict__ P4,
                                             const int32_t* __restrict__ perm, double qx, double qy, double qz, int off,
                                             int g, int l, int nbg, int mv, int fmode, int lim) {
@@ -391,17 +392,25 @@ __device__ __forceinline__ bool final_group(unsigned* lists, const int* leaf_slo
 #pragma unroll
     for (int s = 0; s + 1 < 16; ++s) unsorted |= k[s + 1] < k[s];
     unsorted |= (l < 7) && nx < k[15];
-    // adjacent ranks among the first lim sharing an f32 key (bit s: ranks l*16+s, +1)
-    unsigned tied = 0u;
+    // adjacent ranks sharing an f32 key (bit s: ranks l*16+s and +1): tall over the list,
+    // tied among the first lim (the ranks the sums use, and the one after them)
+    unsigned tall = 0u;
 #pragma unroll
     for (int s = 0; s + 1 < 16; ++s) {
         const int e = l * 16 + s;
-        if ((int)(e + 1 < lim) & (int)((unsigned)(k[s] >> 32) == (unsigned)(k[s + 1] >> 32))) tied |= 1u << s;
+        if ((int)(e + 1 < nbg) & (int)((unsigned)(k[s] >> 32) == (unsigned)(k[s + 1] >> 32))) tall |= 1u << s;
     }
     {
         const int e = l * 16 + 15;
-        if ((int)(l < 7) & (int)(e + 1 < lim) & (int)((unsigned)(k[15] >> 32) == (unsigned)(nx >> 32))) tied |= 1u << 15;
+        if ((int)(l < 7) & (int)(e + 1 < nbg) & (int)((unsigned)(k[15] >> 32) == (unsigned)(nx >> 32))) tall |= 1u << 15;
     }
+    const int nlim = lim - 1 - l * 16;  // bits s < nlim have e + 1 < lim
+    unsigned tied = tall & (nlim >= 16 ? 0xffffu : nlim > 0 ? (1u << nlim) - 1u : 0u);
+    // a pair is isolated when neither neighbouring pair is tied (across the lanes of the group too)
+    const unsigned tprev = (unsigned)__shfl((int)tall, me - 1, 64), tnext = (unsigned)__shfl((int)tall, me + 1, 64);
+    const unsigned tall_lo = (tall << 1) | (l > 0 ? (tprev >> 15) & 1u : 0u);   // bit s: pair s-1 tied
+    const unsigned tall_hi = (tall >> 1) | (l < 7 ? (tnext & 1u) << 15 : 0u);   // bit s: pair s+1 tied
+    const unsigned isolated = ~(tall_lo | tall_hi);
     __builtin_amdgcn_wave_barrier();
     {
         unsigned sl[16];
@@ -412,12 +421,29 @@ __device__ __forceinline__ bool final_group(unsigned* lists, const int* leaf_slo
     __builtin_amdgcn_wave_barrier();
     bool bad = unsorted;
     while (tied) {  // rare: the tree slots of the tied ranks, now in rank order in the list
-        const int e = l * 16 + __builtin_ctz(tied);
+        const int sb = __builtin_ctz(tied);
+        const int e = l * 16 + sb;
         tied &= tied - 1u;
         const int a = (int)list[e], b = (int)list[e + 1];
         const p3 pa = ld3(P4, a), pb = ld3(P4, b);
-        bad |= l2_3(qx, qy, qz, pa.x, pa.y, pa.z) != l2_3(qx, qy, qz, pb.x, pb.y, pb.z);
-        bad |= perm[a] > perm[b];
+        const double da = l2_3(qx, qy, qz, pa.x, pa.y, pa.z), db = l2_3(qx, qy, qz, pb.x, pb.y, pb.z);
+        // the exact order is (f64 distance, point index); an isolated pair is put right by a
+        // swap (its neighbours' f32 keys differ, so their ranks are settled), a longer run of
+        // equal f32 keys goes to the exact kernel
+        const bool wrong = (bool)((int)(da > db) | ((int)(da == db) & (int)(perm[a] > perm[b])));
+        // (a run that continues past the checked ranks: which of its members fall inside is
+        // not settled here)
+        bad |= (bool)((int)(e + 2 >= lim) & (int)((tall_hi >> sb) & 1u));
+        if (wrong) {
+            if ((isolated >> sb) & 1u) {
+                list[e] = (unsigned)b;
+                list[e + 1] = (unsigned)a;
+            } else {
+                bad = true;
+            }
+        } else if (!((isolated >> sb) & 1u)) {
+            bad |= da != db;  // (a run of three or more with distinct f64 distances)
+        }
     }
     const bool ok = !(bool)(unsigned)((__ballot(bad) >> (8 * g)) & 0xffull);
     return ok;
