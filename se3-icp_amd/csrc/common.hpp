@@ -9,7 +9,7 @@
 //                    reference's packing [R00 R10 R20 R01 R11 R21 R02 R12 R22 t0 t1 t2]
 //                    (ISR.cpp:450-453, 613-624)
 //     fr32 [12][ld]  f32 copy of target frames for the SE(3) sweep
-//     nrm64[3][ld], cov64[6][ld] (xx xy xz yy yz zz), conf64[ld]
+//     nrm64[3][ld], conf64[ld] (GICP covariances are recomputed from nrm64 where used)
 // Source clouds are never rewritten inside the loop: the current pose T of a pair
 // is applied on the fly (query = T * M0), see DESIGN.md "Pose on the fly".
 #pragma once

@@ -180,8 +180,11 @@ __device__ __forceinline__ void store_frame_rows(double* fr64, float* fr32, int 
 }
 
 // GetRotationFromE1ToX (ISR.cpp:4-14) and Cov = Rx diag(eps,1,1) Rx^T (ISR.cpp:46-51),
-// returned as the 6 unique entries (xx xy xz yy yz zz).
+// returned as the 6 unique entries (xx xy xz yy yz zz).  k_reduce recomputes it from the
+// stored normal for every correspondence (no covariance array); no FMA contraction, so
+// every call site rounds the same way.
 __device__ inline void gicp_cov_from_normal(d3 n, double eps, double out[6]) {
+#pragma clang fp contract(off)
     double R[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
     const double c = n.x;  // e1 . n
     if (!(c < -0.99)) {

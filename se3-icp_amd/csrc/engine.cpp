@@ -126,7 +126,7 @@ Engine::~Engine() {
     if (!ok_) return;
     (void)hipSetDevice(dev_);
     DevBuf* all[] = {&d_clouds_, &d_setup_, &d_pairs_, &d_cloud_of_, &d_inptr_, &d_in_, &d_xyz64_, &d_xyz32_,
-                     &d_fr64_, &d_fr32_, &d_nrm64_, &d_cov64_, &d_conf64_, &d_knn_,
+                     &d_fr64_, &d_fr32_, &d_nrm64_, &d_conf64_, &d_knn_,
                      &d_corr_idx_, &d_corr_dist_, &d_flag_list_, &d_flag_count_, &d_trim_key_, &d_red_partial_,
                      &d_red_out_, &d_work_, &d_wb_, &d_wn_, &d_chunks_, &d_partial_, &d_centers_,
                      &d_rechecked_, &d_keys0_, &d_vals1_, &d_sort_tmp_, &d_stats_,
@@ -182,7 +182,7 @@ int Engine::alloc_points(int64_t ntot, int kmax, bool knn_list) {
     const size_t L = (size_t)ld_;
     bool ok = ensure<int32_t>(d_cloud_of_, L) && ensure<double>(d_in_, 3 * L) && ensure<double>(d_xyz64_, 3 * L) &&
               ensure<float>(d_xyz32_, 3 * L) && ensure<double>(d_fr64_, 12 * L) && ensure<float>(d_fr32_, 12 * L) &&
-              ensure<double>(d_nrm64_, 3 * L) && ensure<double>(d_cov64_, 6 * L) && ensure<double>(d_conf64_, L) &&
+              ensure<double>(d_nrm64_, 3 * L) && ensure<double>(d_conf64_, L) &&
               (!knn_list || ensure<int32_t>(d_knn_, L * kmax_)) && ensure<int32_t>(d_corr_idx_, L) && ensure<float>(d_corr_dist_, L) &&
               ensure<int32_t>(d_flag_list_, L) && ensure<int32_t>(d_flag_count_, 4) &&
               ensure<uint32_t>(d_keys0_, L) &&
@@ -212,7 +212,6 @@ View Engine::view() const {
     v.fr64 = (double*)d_fr64_.p;
     v.fr32 = (float*)d_fr32_.p;
     v.nrm64 = (double*)d_nrm64_.p;
-    v.cov64 = (double*)d_cov64_.p;
     v.conf64 = (double*)d_conf64_.p;
     v.knn = knn_list_ ? (int32_t*)d_knn_.p : nullptr;
     v.corr_idx = (int32_t*)d_corr_idx_.p;

@@ -582,12 +582,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(5))) void k
             v.nrm64[gp] = nm.x;
             v.nrm64[v.ld + gp] = nm.y;
             v.nrm64[2 * (size_t)v.ld + gp] = nm.z;
-            if (v.setup[c].want_cov) {
-                double cv[6];
-                gicp_cov_from_normal(nm, 1e-3, cv);
-#pragma unroll
-                for (int r = 0; r < 6; ++r) v.cov64[(size_t)r * v.ld + gp] = cv[r];
-            }
         }
         if ((b_flags & 1) && wid == 0) {
             pb[PK_ZN] = zn.x;

@@ -360,12 +360,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             v.nrm64[gp] = nm.x;
             v.nrm64[v.ld + gp] = nm.y;
             v.nrm64[2 * (size_t)v.ld + gp] = nm.z;
-            if (st.want_cov) {
-                double cv[6];
-                gicp_cov_from_normal(nm, 1e-3, cv);
-#pragma unroll
-                for (int r = 0; r < 6; ++r) v.cov64[(size_t)r * v.ld + gp] = cv[r];
-            }
         }
         // ------------------------------------------------------------ TOLDI axes (ISR.cpp:286-306)
         const double nx = __shfl(zn.x, 0, 64), ny = __shfl(zn.y, 0, 64), nz = __shfl(zn.z, 0, 64);

@@ -18,6 +18,7 @@
 #include <climits>
 #include <cmath>
 
+#include "devmath.hpp"
 #include "loopdev.hpp"
 #include "pairmath.hpp"
 #include "wave.hpp"
@@ -519,12 +520,13 @@ __global__ __launch_bounds__(256) void k_reduce(View v) {
                 nrows = 1;
             } else {
                 // Cs = R Cs0 R^T (PointCloud::Transform on covariances, ISR.cpp:706)
+                // (both covariances from the stored normals, ISR.cpp:33-52: 3 loads instead of 6)
                 double C0[3][3];
                 {
-                    const double* cv = v.cov64;
-                    const size_t ld = v.ld;
-                    C0[0][0] = cv[g]; C0[0][1] = C0[1][0] = cv[ld + g]; C0[0][2] = C0[2][0] = cv[2 * ld + g];
-                    C0[1][1] = cv[3 * ld + g]; C0[1][2] = C0[2][1] = cv[4 * ld + g]; C0[2][2] = cv[5 * ld + g];
+                    double c6[6];
+                    gicp_cov_from_normal(d3{v.nrm64[g], v.nrm64[v.ld + g], v.nrm64[2 * (size_t)v.ld + g]}, 1e-3, c6);
+                    C0[0][0] = c6[0]; C0[0][1] = C0[1][0] = c6[1]; C0[0][2] = C0[2][0] = c6[2];
+                    C0[1][1] = c6[3]; C0[1][2] = C0[2][1] = c6[4]; C0[2][2] = c6[5];
                 }
                 double RC[3][3], M[3][3];
 #pragma unroll
@@ -532,9 +534,8 @@ __global__ __launch_bounds__(256) void k_reduce(View v) {
 #pragma unroll
                     for (int b = 0; b < 3; ++b) RC[a][b] = T[a * 4] * C0[0][b] + T[a * 4 + 1] * C0[1][b] + T[a * 4 + 2] * C0[2][b];
                 {
-                    const double* cv = v.cov64;
-                    const size_t ld = v.ld;
-                    const double Ct[6] = {cv[gt], cv[ld + gt], cv[2 * ld + gt], cv[3 * ld + gt], cv[4 * ld + gt], cv[5 * ld + gt]};
+                    double Ct[6];
+                    gicp_cov_from_normal(d3{v.nrm64[gt], v.nrm64[v.ld + gt], v.nrm64[2 * (size_t)v.ld + gt]}, 1e-3, Ct);
                     const int map[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
 #pragma unroll
                     for (int a = 0; a < 3; ++a)

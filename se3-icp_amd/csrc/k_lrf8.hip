@@ -983,12 +983,6 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(6))) vo
         v.nrm64[gp] = nm.x;
         v.nrm64[v.ld + gp] = nm.y;
         v.nrm64[2 * (size_t)v.ld + gp] = nm.z;
-        if (setup[cc].want_cov) {
-            double cv[6];
-            gicp_cov_from_normal(nm, 1e-3, cv);
-#pragma unroll
-            for (int r = 0; r < 6; ++r) v.cov64[(size_t)r * v.ld + gp] = cv[r];
-        }
     };
     // The 3x3 problems of the block's 32 queries, one lane each: wave 0 the TOLDI ones
     // (cyclic Jacobi), wave 1 the normals at the same time.

@@ -13,7 +13,7 @@ struct CloudSetup {
     int32_t k_knn;      // length of the kNN list to compute (0: none)
     int32_t k_lrf;      // TOLDI k (0: no frames)
     int32_t k_nrm;      // EstimateNormals k (0: no normals)
-    int32_t want_cov;   // GICP covariances from normals
+    int32_t want_cov;   // GICP: covariances from the normals (computed where k_reduce uses them)
     int32_t want_conf;  // lounge confidences (run_se3_icp_with_cf)
     int32_t is_target;
     int32_t cf_target;  // 12-D search rows take translation from the points (ISR.cpp:834-836)
@@ -54,7 +54,6 @@ struct View {
     double* fr64;  // [ld][12] SE(3) 12-vectors of every point (rows: gathered by point)
     float* fr32;   // [ld][12] their f32 copies (the 12-D trees' input)
     double* nrm64;
-    double* cov64;
     double* conf64;
     int32_t* knn;
     // per-cloud f32 error-bound norms (float bits, atomicMax)
