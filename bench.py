@@ -395,7 +395,10 @@ def lrf_roofline(ktot, kms, steps, k):
 # its correspondence's float distance (the trim key, 4 B); a kept one also its target index
 # (4), both f64 points (2 x 24), and per estimator the target normal (pt2pl, 24), both GICP
 # covariances (2 x 48), the two cf confidences (2 x 8)
-REDUCE_BYTES_KEPT = {"pt2pt": 56, "pt2pl": 80, "gicp": 152, "gicp_cf": 168}
+# per kept correspondence: index 4 + distance 4 + source and target points 2 x 24, plus the
+# target normal 24 (pt2pl) or both normals 2 x 24 (GICP: the covariances are recomputed
+# from them, ISR.cpp:33-52) and both confidences 2 x 8 (cf)
+REDUCE_BYTES_KEPT = {"pt2pt": 56, "pt2pl": 80, "gicp": 104, "gicp_cf": 120}
 
 
 def reduce_roofline(res, pairs, W, red_ms):
