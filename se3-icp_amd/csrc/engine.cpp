@@ -127,7 +127,7 @@ Engine::~Engine() {
     (void)hipSetDevice(dev_);
     DevBuf* all[] = {&d_clouds_, &d_setup_, &d_pairs_, &d_cloud_of_, &d_inptr_, &d_in_, &d_xyz64_, &d_xyz32_,
                      &d_fr64_, &d_fr32_, &d_nrm64_, &d_conf64_, &d_knn_,
-                     &d_corr_idx_, &d_corr_dist_, &d_flag_list_, &d_flag_count_, &d_trim_key_, &d_red_partial_,
+                     &d_corr_idx_, &d_corr_dist_, &d_flag_count_, &d_trim_key_, &d_red_partial_,
                      &d_red_out_, &d_work_, &d_wb_, &d_wn_, &d_chunks_, &d_partial_, &d_centers_,
                      &d_rechecked_, &d_keys0_, &d_vals1_, &d_sort_tmp_, &d_stats_,
                      &d_qlist_, &d_qcount_, &d_hist_, &d_cert_, &d_sqlist_, &d_state_, &d_trim_cand_, &d_trim_ctr_, &d_scales_, &d_trim_hist_,
@@ -184,7 +184,7 @@ int Engine::alloc_points(int64_t ntot, int kmax, bool knn_list) {
               ensure<float>(d_xyz32_, 3 * L) && ensure<double>(d_fr64_, 12 * L) && ensure<float>(d_fr32_, 12 * L) &&
               ensure<double>(d_nrm64_, 3 * L) && ensure<double>(d_conf64_, L) &&
               (!knn_list || ensure<int32_t>(d_knn_, L * kmax_)) && ensure<int32_t>(d_corr_idx_, L) && ensure<float>(d_corr_dist_, L) &&
-              ensure<int32_t>(d_flag_list_, L) && ensure<int32_t>(d_flag_count_, 4) &&
+              ensure<int32_t>(d_flag_count_, 4) &&
               ensure<uint32_t>(d_keys0_, L) &&
               ensure<int32_t>(d_vals1_, L) && ensure<unsigned long long>(d_stats_, kStatCols * kStatSlots) &&
               ensure<float4>(d_cert_, L) &&
@@ -217,7 +217,6 @@ View Engine::view() const {
     v.corr_idx = (int32_t*)d_corr_idx_.p;
     v.corr_dist = (float*)d_corr_dist_.p;
     v.stats = (unsigned long long*)d_stats_.p;
-    v.flag_list = (int32_t*)d_flag_list_.p;
     v.flag_count = (int32_t*)d_flag_count_.p;
     v.trim_key = (uint64_t*)d_trim_key_.p;
     v.trim_cand = (unsigned long long*)d_trim_cand_.p;
@@ -669,7 +668,6 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     HIPCHK(hipMemsetAsync(d_trim_ctr_.p, 0, sizeof(unsigned) * 4 * npairs, s));
     HIPCHK(hipMemsetAsync(d_trim_hist_.p, 0, sizeof(unsigned) * 4096 * npairs, s));
     View v = view();
-    const int recheck_blocks = 512;
     double nn_ms = 0;
     // Iteration `it` is queued while iteration it-1 still runs; the host then waits for
     // it-1 and reads how many pairs iteration it has (counted by it-1's k_reduce_final).
@@ -715,7 +713,8 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
             if (do_r3) launch_nn_r3(v, s);
         }
         if (detail) HIPCHK(hipEventRecord(ev[3], s));
-        launch_recheck(v, recheck_blocks, s);
+        // (no recheck stage: the NN grids re-resolve their uncertified queries inline; the
+        // ev[3] -> ev[4] bracket stays empty and time_recheck reads ~0)
         if (detail) HIPCHK(hipEventRecord(ev[4], s));
         if (any_trim) launch_trim(v, s);
         if (detail) HIPCHK(hipEventRecord(ev[5], s));
@@ -1012,7 +1011,7 @@ int Engine::estimate_normals(const double* xyz, int64_t n, int k, double* normal
 
 // Exact 1-NN of arbitrary query vectors among data vectors (3 or 12 dims): the vectors
 // are placed in the source/target slots of a one-pair batch with the identity pose, the
-// kd-trees are built over them, and the loop's NN + recheck kernels run once.
+// kd-trees are built over them, and the loop's NN kernels (with their inline f64 recheck) run once.
 int Engine::nn(const double* query, int64_t nq, const double* data, int64_t nd, int dim, int32_t* idx, double* d2,
                int32_t* num_rechecked) {
     if (!ok_) return SE3ICP_ERR_NO_DEVICE;
@@ -1087,7 +1086,6 @@ int Engine::nn(const double* query, int64_t nq, const double* data, int64_t nd, 
     launch_nn_prep(v, s);
     if (dim == 12) launch_nn_se3(v, s);
     else launch_nn_r3(v, s);
-    launch_recheck(v, 512, s);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(idx, d_corr_idx_.p, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, s));
     int32_t rech = 0;

@@ -30,106 +30,8 @@ namespace {
 
 using namespace loopdev;
 
-// ------------------------------------------------------------------ recheck (exact f64)
-// One wavefront per flagged query: exact f64 1-NN over the target kd-tree of the phase.
-// The f32 node boxes were inflated to bound the f64 vectors (k_tree.hip), so a box
-// lower bound computed in f64 against the f64 query prunes exactly; boxes whose bound
-// equals the best distance are still opened (a lower index may tie).  Seeded with the
-// f32 winner that k_nn_group stored in corr_idx.
-template <int D>
-__device__ __forceinline__ void recheck_one(const View& v, const PairDev* P, const CloudDev& ct, int g, int lane) {
-    const bool cf = P->cf != 0;
-    const TreeRef TR = (D == 12) ? v.t12 : v.t3;
-    double T[12], Q[D], qs[D];
-    load_T(P, T);
-    query_f64<D>(v, T, g, Q);
-#pragma unroll
-    for (int r = 0; r < D; ++r) qs[r] = (D == 3) ? Q[r] - P->f32_center[r] : Q[r];
-    auto dist = [&](int j) __attribute__((always_inline)) {
-        if constexpr (D == 12) {
-            double b[12];
-            target12(v, ct, cf, j, b);
-            return l2_nanoflann12(Q, b);
-        } else {
-            const int gt = ct.off + j;
-            const double b[3] = {v.xyz64[gt], v.xyz64[v.ld + gt], v.xyz64[2 * (size_t)v.ld + gt]};
-            return l2_nanoflann3(Q, b);
-        }
-    };
-    const float* box_lo = TR.lo + (size_t)P->tgt * TR.nnodes * D;
-    const float* box_hi = TR.hi + (size_t)P->tgt * TR.nnodes * D;
-    auto lbound = [&](int h) __attribute__((always_inline)) {
-        double s = 0.0;
-#pragma unroll
-        for (int r = 0; r < D; ++r) {
-            const double e = fmax(fmax((double)box_lo[h * D + r] - qs[r], qs[r] - (double)box_hi[h * D + r]), 0.0);
-            s += e * e;
-        }
-        return s * (1.0 - 1e-12);
-    };
-    int bi = v.corr_idx[g];
-    if (bi < 0 || bi >= ct.n) bi = 0;
-    double bd = dist(bi);
-    const int first_leaf = (1 << TR.L) - 1;
-    // Lane-parallel box tests (64 nodes per instruction): the nodes of level A = L - 6
-    // (<= 64 leaves below each), then the leaves under each node that can still hold a
-    // point at or below the best distance (<=: a lower index may tie); open leaves are
-    // swept a point per lane.  Seeded with the f32 winner, few boxes stay open.
-    const int sh = TR.L > 6 ? 6 : TR.L;
-    const int A = TR.L - sh, nA = 1 << A, firstA = nA - 1;
-    for (int c0 = 0; c0 < nA; c0 += 64) {
-        const int ai = c0 + lane;
-        const double lbA = ai < nA ? lbound(firstA + ai) : DBL_MAX;
-        unsigned long long mA = __ballot(lbA <= bd);
-        while (mA) {
-            const int j = __builtin_ctzll(mA);
-            mA &= mA - 1ull;
-            if (!(__shfl(lbA, j, 64) <= bd)) continue;
-            const int l0 = (c0 + j) << sh;
-            const int li = l0 + lane;
-            const double lbL = lane < (1 << sh) ? lbound(first_leaf + li) : DBL_MAX;
-            unsigned long long mL = __ballot(lbL <= bd);
-            while (mL) {
-                const int t = __builtin_ctzll(mL);
-                mL &= mL - 1ull;
-                if (!(__shfl(lbL, t, 64) <= bd)) continue;
-                const int ta = tree_first(ct.n, TR.L, l0 + t), tb = tree_first(ct.n, TR.L, l0 + t + 1);
-                double d = DBL_MAX;
-                int jj = INT_MAX;
-                if (lane < tb - ta) {
-                    jj = TR.perm[ct.off + ta + lane];
-                    d = dist(jj);
-                }
-#pragma unroll
-                for (int o = 32; o >= 1; o >>= 1) {
-                    const double od = xor_lane(d, o);
-                    const int oj = xor_lane(jj, o);
-                    const bool tk = (bool)((int)(od < d) | ((int)(od == d) & (int)(oj < jj)));
-                    d = tk ? od : d;
-                    jj = tk ? oj : jj;
-                }
-                if ((int)(d < bd) | ((int)(d == bd) & (int)(jj < bi))) { bd = d; bi = jj; }
-            }
-        }
-    }
-    if (lane == 0) {
-        v.corr_idx[g] = bi;
-        v.corr_dist[g] = stored_dist(v, P->phase, ct, Q, bi);
-    }
-}
-
-__global__ __launch_bounds__(256) void k_recheck(View v) {
-    const int cnt = *v.flag_count;
-    const int lane = threadIdx.x & 63;
-    const int w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
-    for (int f = w0; f < cnt; f += gridDim.x * 4) {
-        const int g = v.flag_list[f];
-        const PairDev* P = v.pairs + (v.cloud_of[g] >> 1);
-        const CloudDev ct = v.clouds[P->tgt];
-        if (P->phase == PHASE_SE3) recheck_one<12>(v, P, ct, g, lane);
-        else if (P->phase == PHASE_R3) recheck_one<3>(v, P, ct, g, lane);
-    }
-}
+// (recheck: the NN kernels re-resolve their uncertified queries in f64 inline,
+// loopdev.hpp recheck_one)
 
 // ------------------------------------------------------------------ trim
 __device__ __forceinline__ unsigned long long trim_key_of(const float* dist, int base, int i) {
@@ -678,9 +580,6 @@ __global__ __launch_bounds__(256) void k_reduce_final(View v, const int32_t* pai
 
 }  // namespace
 
-void launch_recheck(const View& v, int nblocks, hipStream_t s) {
-    hipLaunchKernelGGL(k_recheck, dim3(nblocks), dim3(256), 0, s, v);
-}
 void launch_trim(const View& v, hipStream_t s) {
     hipLaunchKernelGGL(k_trim_window, dim3(v.npairs * kTrimBlocks), dim3(256), 0, s, v);
     hipLaunchKernelGGL(k_trim, dim3(v.npairs), dim3(1024), 0, s, v);

@@ -463,15 +463,14 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
 
 // Results of a searched query (one lane): the recheck flag, the certificate, the
 // correspondence and its stored distance.
+// A flagged query (uncertified f32 arg-min) is re-resolved in f64 by the calling wave right
+// after (recheck_one), which then writes its corr_idx / corr_dist.
 template <int D>
 __device__ __forceinline__ void nn_finish(const View& v, const PairDev* P, int pair, const TreeRef& TR,
                                           const CloudDev& ct, int gx, int g, bool flag, float d1, float d2, int i1,
                                           float thr, float na, float nb) {
-    if ((int)flag & (int)(ct.n > 1)) {
-        const int at = atomicAdd(v.flag_count, 1);
-        v.flag_list[at] = g;
-        atomicAdd(&v.pair_rechecked[pair], 1);
-    }
+    const bool rc = (bool)((int)flag & (int)(ct.n > 1));
+    if (rc) atomicAdd(&v.pair_rechecked[pair], 1);
     // certificate for the next iterations (k_nn_prep): exact match distance <= sqrt(d1 + err),
     // every other target >= min(d2 - err(d2), thr): visited ones by the top-2, unvisited
     // ones because every box skipped had a bound >= thr at the time (thr only decreases)
@@ -483,6 +482,7 @@ __device__ __forceinline__ void nn_finish(const View& v, const PairDev* P, int p
         v.cert[g] = make_float4(sqrtf(d1 + f32_err(d1, na, nb, D)) * (1.f + 1e-6f),
                                 sqrtf(fmaxf(l2, 0.f)) * (1.f - 1e-6f), __int_as_float(P->iter), 0.f);
     }
+    if (rc) return;
     // tree position -> target index; a NaN query keeps the reference's zero-initialised index
     i1 = (i1 < 0) ? 0 : TR.perm[ct.off + i1];
     v.corr_idx[g] = i1;
@@ -750,10 +750,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kWpe))) void
         }
 #endif
     }
-    if (!valid) return;
-    // certification (see the header) and the stored distance
-    const bool flag = (bool)((int)(i1 < 0) | (int)!(d2 - d1 > 2.f * f32_err(d2, na, nb, D)));
-    nn_finish<D>(v, P, pair, TR, ct, gx, g, flag, d1, d2, i1, thr, na, nb);
+    // certification (see the header) and the stored distance; the uncertified queries are
+    // re-resolved in f64 by the whole wave, one after the other (few: ~0.4 % of queries)
+    const bool flag = (bool)((int)valid & ((int)(i1 < 0) | (int)!(d2 - d1 > 2.f * f32_err(d2, na, nb, D))));
+    if (valid) nn_finish<D>(v, P, pair, TR, ct, gx, g, flag, d1, d2, i1, thr, na, nb);
+    unsigned long long fm = __ballot((int)flag & (int)(ct.n > 1));
+    const int seed = i1 < 0 ? 0 : TR.perm[ct.off + i1];
+    while (fm) {
+        const int j = __builtin_ctzll(fm);
+        fm &= fm - 1ull;
+        recheck_one<D>(v, P, ct, __shfl(g, j, 64), __shfl(seed, j, 64), lane);
+    }
 }
 
 // ------------------------------------------------------------------ one wavefront per query
@@ -876,9 +883,9 @@ __device__ __forceinline__ void single_one(const View& v, const PairDev* P, int 
         const unsigned long long win = __ballot((int)(a1 == d1) & (int)(b1 >= 0));
         if (win) i1 = __shfl(b1, __builtin_ctzll(win), 64);
     }
-    if (lane != 0) return;
-    const bool flag = (bool)((int)(i1 < 0) | (int)!(d2 - d1 > 2.f * f32_err(d2, na, nb, D)));
-    nn_finish<D>(v, P, pair, TR, ct, gx, g, flag, d1, d2, i1, thr, na, nb);
+    const bool flag = (bool)((int)(i1 < 0) | (int)!(d2 - d1 > 2.f * f32_err(d2, na, nb, D)));  // (wave-uniform)
+    if (lane == 0) nn_finish<D>(v, P, pair, TR, ct, gx, g, flag, d1, d2, i1, thr, na, nb);
+    if ((int)flag & (int)(ct.n > 1)) recheck_one<D>(v, P, ct, g, i1 < 0 ? 0 : TR.perm[ct.off + i1], lane);
 }
 
 // grid-stride over the single-query list of the phase: SE(3) entries from the front,

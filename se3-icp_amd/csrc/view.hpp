@@ -61,8 +61,7 @@ struct View {
     int32_t* corr_idx;
     float* corr_dist;
     unsigned long long* stats;  // [4] NN work counters: se3 dist evals, se3 box tests, r3 dist evals, r3 box tests
-    int32_t* flag_list;
-    int32_t* flag_count;  // [3] recheck list, single-query lists (SE(3), R3)
+    int32_t* flag_count;  // [3] (unused), single-query lists (SE(3), R3)
     uint64_t* trim_key;   // [npairs] cut key, then [npairs] k_trim window state
     unsigned long long* trim_cand;  // [npairs][kTrimList] k_trim window keys
     unsigned* trim_ctr;   // [npairs][4] k_trim counters (zero between launches)
@@ -147,7 +146,6 @@ void launch_nn_r3(const View& v, hipStream_t s);
 // the two grids of a phase (D = 12 or 3) separately: the group grid, the one-query-per-wave grid
 void launch_nn_group(const View& v, int D, hipStream_t s);
 void launch_nn_single(const View& v, int D, hipStream_t s);
-void launch_recheck(const View& v, int nblocks, hipStream_t s);
 void launch_trim(const View& v, hipStream_t s);
 // reduce + (k_reduce_final) per-pair solve and loop state machine; next_phase[p] receives
 // pair p's phase in the next iteration (PHASE_IDLE: finished)
