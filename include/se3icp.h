@@ -221,6 +221,8 @@ int64_t se3icp_random_downsample(const double* xyz, int64_t n, double ratio, uin
 /* ------------------------------------------------------------- diagnostics
  * Not part of the reference boundary: per-kernel GPU times (HIP events) of the
  * last batch on `device`, used by bench.py for the roofline figures.
+ * (recheck_ms: ~0 since ABI 3's inline recheck -- the f64 re-resolution runs inside
+ * the NN grids and is part of nn_se3_ms / nn_r3_ms.)
  * out[24] = {nn_se3_ms, nn_r3_ms, recheck_ms, trim_ms, reduce_ms, setup_ms,
  *            nn_se3_launches, nn_r3_launches, se3_dist_evals, se3_box_tests,
  *            r3_dist_evals, r3_box_tests,   (evals/tests counted per lane)
