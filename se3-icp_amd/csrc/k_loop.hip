@@ -533,34 +533,37 @@ __global__ __launch_bounds__(256) void k_reduce(View v) {
 // So the slot is the only value the host may read without ordering: any host read of
 // other device state after finish() must stay stream-ordered (an async copy on the stream,
 // then a sync), as the engine's result copies are.
-__global__ __launch_bounds__(256) void k_reduce_final(View v, const int32_t* pair_wb, const int32_t* pair_wn,
+constexpr int kFinThreads = 512;                    // (the solve's ~220 VGPRs allow two waves per SIMD)
+constexpr int kFinChunks = kFinThreads / kRedVals;  // 18 interleaved chunks of block partials
+__global__ __launch_bounds__(kFinThreads) void k_reduce_final(View v, const int32_t* pair_wb, const int32_t* pair_wn,
                                                       PairState* state, double* hist, int32_t* next_phase) {
     const int p = blockIdx.x;
-    if ((int)(p == 0) & (int)(threadIdx.x < 3)) v.flag_count[threadIdx.x] = 0;  // recheck / single-query lists
+    if ((int)(p == 0) & (int)(threadIdx.x < 3)) v.flag_count[threadIdx.x] = 0;  // single-query lists
     PairDev* P = v.pairs + p;
     if (P->phase == PHASE_IDLE) {
         if (threadIdx.x == 0) next_phase[p] = PHASE_IDLE;
         return;
     }
-    __shared__ double part[8][kRedVals];
+    __shared__ double part[kFinChunks][kRedVals];
     __shared__ double tot[kRedVals];
     const int i = threadIdx.x % kRedVals, s = threadIdx.x / kRedVals;
     const int wb = pair_wb[p], wn = pair_wn[p];
-    if (s < 8) {  // four independent chains per lane: four loads in flight
+    if (s < kFinChunks) {  // four independent chains per lane: four loads in flight
+        constexpr int C = kFinChunks;
         double s4[4] = {0.0, 0.0, 0.0, 0.0};
         const double* rp = v.red_partial + (size_t)wb * kRedVals + i;
         int b = s;
-        for (; b + 24 < wn; b += 32)
+        for (; b + 3 * C < wn; b += 4 * C)
 #pragma unroll
-            for (int u = 0; u < 4; ++u) s4[u] += rp[(size_t)(b + 8 * u) * kRedVals];
-        for (; b < wn; b += 8) s4[0] += rp[(size_t)b * kRedVals];
+            for (int u = 0; u < 4; ++u) s4[u] += rp[(size_t)(b + C * u) * kRedVals];
+        for (; b < wn; b += C) s4[0] += rp[(size_t)b * kRedVals];
         part[s][i] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
     }
     __syncthreads();
     if (threadIdx.x < kRedVals) {
         double sum = 0;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) sum += part[k][threadIdx.x];
+        for (int k = 0; k < kFinChunks; ++k) sum += part[k][threadIdx.x];
         v.red_out[(size_t)p * kRedVals + threadIdx.x] = sum;
         tot[threadIdx.x] = sum;
     }
@@ -587,7 +590,7 @@ void launch_trim(const View& v, hipStream_t s) {
 void launch_reduce(const View& v, const int32_t* pair_wb, const int32_t* pair_wn, PairState* state, double* hist,
                    int32_t* next_phase, hipStream_t s) {
     hipLaunchKernelGGL(k_reduce, dim3(v.nwork), dim3(256), 0, s, v);
-    hipLaunchKernelGGL(k_reduce_final, dim3(v.npairs), dim3(256), 0, s, v, pair_wb, pair_wn, state, hist, next_phase);
+    hipLaunchKernelGGL(k_reduce_final, dim3(v.npairs), dim3(kFinThreads), 0, s, v, pair_wb, pair_wn, state, hist, next_phase);
 }
 
 }  // namespace se3icp
