@@ -341,7 +341,8 @@ def nn_roofline(ktot, kms):
         "bound": "valu",
         "note": "f32 VALU kd-tree sweep (leaf distance sweeps + box tests; no MFMA issued), priced against the "
                 "f32 vector peak; a launch is the group + single-query kernel pair, bracketed by HIP events on the "
-                "engine's stream (rocprof lists the two kernels separately; their averages add up to avg_launch_ms)",
+                "engine's stream (rocprof lists the two kernels separately; their averages add up to avg_launch_ms); "
+                "the time includes the inline f64 recheck of the ~0.4 % uncertified queries, whose flops are not counted",
         "achieved": round(achieved, 3),
         "peak": FP32_PEAK_TFLOPS,
         "unit": "TFLOP/s",
