@@ -49,8 +49,9 @@ WORKLOADS = {
                            number_of_nn_for_LRF=90),
                desc="C2: se3_pt2pt on the reference's synthetic bunny problems (benchmark_synthetic.cpp:91-160 with "
                     "its own mt19937 / normal_distribution / RandomDownSample streams, noise var 0.005) at "
-                    "RandomDownSample(0.2) of stanford_bunny.ply x50 = 41,670 pts per cloud (BASELINE '~40k'; the "
-                    "driver itself uses 0.02), B_SYN:356-363 params, 8 cases per GPU",
+                    "RandomDownSample(0.2) of stanford_bunny.ply x50 = 41,670 pts per cloud (BASELINE.json configs[1]: "
+                    "'synthetic easy_data, ~40k pts'; the driver itself samples 0.02 and has the 'moderate' ranges "
+                    "active, B_SYN:111-112), 'easy' ranges (B_SYN:107-108), B_SYN:356-363 params, 8 cases per GPU",
                data="stanford_bunny.ply (tests/golden) -> se3icp_synthetic_reference_device, generated on the GPU"),
     "C3": dict(method="se3_pt2pl", ppg=32, run="se3", variant="pt2pl",
                params=dict(estimated_overlap=0.75, max_num_se3_iterations=10, mse_switch_error=5e-5,
@@ -75,40 +76,53 @@ def rot_err_deg(A, B):
     return float(np.degrees(np.arccos(np.clip((np.trace(R) - 1) / 2, -1, 1))))
 
 
-def pmc_traffic(kernel_substr: str):
-    """HBM bytes per launch of a kernel from the newest committed PMC summary (profiles/*pmc*.json),
-    written by tools/pmc_summary.py from separate rocprofv3 --pmc passes."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
-    for f in reversed(files):
+def _pmc_files(workload: str):
+    """Committed PMC summaries of one workload, newest first: profiles/*pmc*.json whose
+    "workload" field names it (files written before round 4 carry none and are C4's)."""
+    out = []
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")), reverse=True):
         try:
             d = json.load(open(f))
         except Exception:
             continue
-        for k, v in d.get("kernels", {}).items():
-            if kernel_substr in k and v.get("hbm_bytes_per_launch") is not None:
-                return float(v["hbm_bytes_per_launch"]), os.path.relpath(f, ROOT)
+        if d.get("workload", "C4") == workload:
+            out.append((f, d))
+    return out
+
+
+def pmc_traffic(kernel_substrs, workload: str):
+    """HBM bytes per launch, summed over the named kernels, from the newest committed PMC
+    summary of THIS workload (tools/pmc_summary.py, separate rocprofv3 --pmc passes);
+    (None, None) when that summary lacks any of the kernels."""
+    if isinstance(kernel_substrs, str):
+        kernel_substrs = [kernel_substrs]
+    for f, d in _pmc_files(workload)[:1]:
+        tot = 0.0
+        for sub in kernel_substrs:
+            hit = [v for k, v in d.get("kernels", {}).items() if sub in k and v.get("hbm_bytes_per_launch") is not None]
+            if not hit:
+                return None, None
+            tot += float(hit[0]["hbm_bytes_per_launch"])
+        return tot, os.path.relpath(f, ROOT)
     return None, None
 
 
-def pmc_counter(kernel_substr: str, counter: str):
-    """One PMC counter per dispatch of a kernel from the newest committed PMC summary."""
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
-    for f in reversed(files):
-        try:
-            d = json.load(open(f))
-        except Exception:
-            continue
+def pmc_counter(kernel_substr: str, counter: str, workload: str):
+    """One PMC counter per dispatch of a kernel from the newest committed PMC summary of THIS
+    workload, with the file it came from."""
+    for f, d in _pmc_files(workload)[:1]:
         for k, v in d.get("kernels", {}).items():
             c = v.get("counters_per_dispatch", {})
             if kernel_substr in k and counter in c:
-                return float(c[counter])
-    return None
+                return float(c[counter]), os.path.relpath(f, ROOT)
+    return None, None
 
 
 C2_SETUPS = {"easy": (5.0, np.pi / 4), "moderate": (10.0, np.pi / 2)}  # B_SYN:106-108, :111-112
 
 
-def make_pairs(wl: str, total: int, first: int, count: int, n_az: int, c2_setup: str = "easy", device: int = 0):
+def make_pairs(wl: str, total: int, first: int, count: int, n_az: int, c2_setup: str = "easy", device: int = 0,
+               c2_cloud: str = "downsample"):
     """The rank's pairs [first, first + count) of a `total`-pair sequence, with ground truths."""
     from se3icp import datasets
     if wl == "C4":
@@ -118,9 +132,12 @@ def make_pairs(wl: str, total: int, first: int, count: int, n_az: int, c2_setup:
         # rank draws the whole sequence and keeps its block), written by the GPU
         u = np.load(os.path.join(ROOT, "tests", "golden", "bunny_unique_f32.npy"))
         ids = np.load(os.path.join(ROOT, "tests", "golden", "bunny_vertex_ids.npy"))
-        cloud = u[ids].astype(np.float64) * 50.0
+        if c2_cloud == "unique":  # BASELINE.md's C2 row (rounds 1-2): the 34,834 unique vertices, all kept
+            cloud, ratio = u.astype(np.float64) * 50.0, 1.0
+        else:
+            cloud, ratio = u[ids].astype(np.float64) * 50.0, 0.2
         tr, rr = C2_SETUPS[c2_setup]
-        src, tgt, T = datasets.synthetic_reference_gpu(cloud, total, ratio=0.2, noise_var=0.005, t_range=tr,
+        src, tgt, T = datasets.synthetic_reference_gpu(cloud, total, ratio=ratio, noise_var=0.005, t_range=tr,
                                                        r_range=rr, device=device)
         return ([(src[i], tgt[i]) for i in range(first, first + count)], [T[i] for i in range(first, first + count)])
     seed = 3 if wl == "C3" else 5
@@ -142,10 +159,19 @@ def main():
     ap.add_argument("--dump-poses", default="", help="rank 0 writes the gathered per-pair poses (.npy)")
     ap.add_argument("--c2-setup", choices=sorted(C2_SETUPS), default="easy",
                     help="C2 transform ranges: BASELINE's easy_data (B_SYN:106-108) or the driver's active moderate ones")
+    ap.add_argument("--c2-cloud", choices=["downsample", "unique"], default="downsample",
+                    help="C2 cloud: RandomDownSample(0.2) of the 208,353-vertex bunny (41,670 pts, round 3 on) or "
+                         "BASELINE.md's 34,834 unique vertices (rounds 1-2); the bench line's workload is then 'C2u'")
     ap.add_argument("--secondary", choices=["auto", "off"], default="auto",
                     help="C4 at N=1: also time the whole 64-pair batch on this GPU (strong-scaling anchor)")
     args = ap.parse_args()
-    W = WORKLOADS[args.workload]
+    W = dict(WORKLOADS[args.workload])
+    if args.workload == "C2" and args.c2_setup != "easy":
+        W["desc"] = W["desc"].replace("'easy' ranges (B_SYN:107-108)", "'moderate' ranges (B_SYN:111-112)")
+    if args.workload == "C2" and args.c2_cloud == "unique":
+        W["desc"] = ("C2u: se3_pt2pt on the reference's synthetic bunny problems over the 34,834 unique vertices of "
+                     "stanford_bunny.ply x50, all kept (BASELINE.md's C2 row; the rounds-1-2 definition), noise var "
+                     "0.005, 'easy' ranges, B_SYN:356-363 params, 8 cases per GPU")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -179,7 +205,7 @@ def main():
     P = args.pairs_per_gpu or W["ppg"]
     t0 = time.time()
     first, count = sharding.shard(world * P, world, rank)  # weak scaling: P pairs per rank
-    pairs, gts = make_pairs(args.workload, world * P, first, count, args.n_az, args.c2_setup, devi)
+    pairs, gts = make_pairs(args.workload, world * P, first, count, args.n_az, args.c2_setup, devi, args.c2_cloud)
     npts = [p[0].shape[0] for p in pairs] + [p[1].shape[0] for p in pairs]
     log(f"rank {rank}: {args.workload} generated {count} pairs in {time.time() - t0:.1f}s, points/cloud "
         f"min {min(npts)} mean {np.mean(npts):.0f} max {max(npts)}")
@@ -262,9 +288,10 @@ def main():
                     "box_tests_per_query": round(ktot.get("lrf_box_tests", 0.0) / nq, 2),
                     "candidates_per_query": round(ktot.get("lrf_candidates", 0.0) / nq, 2),
                     "exact_kernel_queries_per_step": ktot.get("lrf_fallback", 0.0) / args.steps}
-        roof_nn = nn_roofline(ktot, kms)
-        roof_lrf = lrf_roofline(ktot, kms, args.steps, W["params"]["number_of_nn_for_LRF"])
-        roof_red = reduce_roofline(last, pairs, W, kms["reduce_ms"] / args.steps)
+        wl = args.workload if args.c2_cloud == "downsample" else f"{args.workload}u"
+        roof_nn = nn_roofline(ktot, kms, wl)
+        roof_lrf = lrf_roofline(ktot, kms, args.steps, W["params"]["number_of_nn_for_LRF"], wl)
+        roof_red = reduce_roofline(last, pairs, W, kms["reduce_ms"] / args.steps, wl)
         # the bench line's roofline is the step's dominant kernel by GPU time; the other
         # named kernel is reported beside it
         nn_step = roof_nn["avg_launch_ms"] * roof_nn["launches"] / args.steps
@@ -317,7 +344,7 @@ def main():
         dist.destroy_process_group()
 
 
-def nn_roofline(ktot, kms):
+def nn_roofline(ktot, kms, wl):
     """The loop's dominant NN launch (k_nn_group + k_nn_single of the phase with more time):
     work actually issued, counted on the device — lane x target distance evaluations
     (3D flop: D sub + D FMA) and lane x box tests (4D flop: 2D sub/max + D FMA)."""
@@ -333,16 +360,17 @@ def nn_roofline(ktot, kms):
     flops = evals * flop_dist + boxes * flop_box
     achieved = flops / (t_ms / 1000.0) / 1e12 if t_ms > 0 else 0.0
     nl = max(1.0, nl)
-    t_g, src = pmc_traffic(f"k_nn_group<{D}>")
-    t_s, _ = pmc_traffic(f"k_nn_single<{D}>")
-    traffic = (t_g + t_s) if (t_g is not None and t_s is not None) else t_g
+    traffic, src = pmc_traffic([f"k_nn_group<{D}>", f"k_nn_single<{D}>"], wl)
     return {
         "kernel": kname,
         "bound": "valu",
         "note": "f32 VALU kd-tree sweep (leaf distance sweeps + box tests; no MFMA issued), priced against the "
-                "f32 vector peak; a launch is the group + single-query kernel pair, bracketed by HIP events on the "
-                "engine's stream (rocprof lists the two kernels separately; their averages add up to avg_launch_ms); "
-                "the time includes the inline f64 recheck of the ~0.4 % uncertified queries, whose flops are not counted",
+                "f32 vector peak.  A launch is the group grid (main stream) and the single-query grid (side "
+                "stream, forked after k_nn_prep) running side by side; avg_launch_ms is their SPAN, first start "
+                "to last end (HIP events: the fork event on the main stream to a marker after the join), which "
+                "is what tools/nn_span.py computes per launch pair from the committed kernel trace (rocprof's "
+                "per-kernel averages overlap and do not add up to it).  The time includes the inline f64 "
+                "recheck of the ~0.4 % uncertified queries, whose flops are not counted",
         "achieved": round(achieved, 3),
         "peak": FP32_PEAK_TFLOPS,
         "unit": "TFLOP/s",
@@ -356,20 +384,28 @@ def nn_roofline(ktot, kms):
     }
 
 
-def lrf_roofline(ktot, kms, steps, k):
+def busy_fraction(quad_cycles, t_ms):
+    """VALU issue busy: SQ_ACTIVE_INST_VALU (quad-cycles, summed over the chip's SIMDs) x 4
+    over the SIMD-cycles of t_ms.  Above 1 the counter and the time cannot be from the same
+    launch (a counter of another workload or build): refused (None)."""
+    if not quad_cycles or t_ms <= 0:
+        return None
+    b = quad_cycles * 4.0 / (N_SIMDS * CLOCK_GHZ * 1e6 * t_ms)
+    return round(b, 3) if b <= 1.0 else None
+
+
+def lrf_roofline(ktot, kms, steps, k, wl):
     """k_lrf, the setup's fused kNN-k + TOLDI + normals kernel, one launch per step, priced
     with SURVEY.md §8(d)'s TOLDI unit: k neighbour gathers of 24 B (f64 xyz) per point."""
     t_ms = kms["lrf_ms"] / steps
     q = ktot.get("lrf_queries", 0.0) / steps
     bpp = 24.0 * k
     achieved = q * bpp / (t_ms / 1000.0) / 1e9 if t_ms > 0 else 0.0
-    t8, src = pmc_traffic("k_lrf8")
-    tx, _ = pmc_traffic("k_lrf(")  # the exact kernel over the hand-over list
-    traffic = (t8 + tx) if (t8 is not None and tx is not None) else t8
+    traffic, src = pmc_traffic(["k_lrf8", "k_lrf("], wl)  # k_lrf: the exact kernel over the hand-over list
     # what does bound it: the VALU issue of k_lrf8 (SQ_ACTIVE_INST_VALU counts quad-cycles per
     # SIMD, summed over the chip's 1,024 SIMDs) over this launch pair's measured time
-    av = pmc_counter("k_lrf8", "SQ_ACTIVE_INST_VALU")
-    valu_busy = round(av * 4.0 / (N_SIMDS * CLOCK_GHZ * 1e6 * t_ms), 3) if (av and t_ms > 0) else None
+    av, _ = pmc_counter("k_lrf8", "SQ_ACTIVE_INST_VALU", wl)
+    insts, _ = pmc_counter("k_lrf8", "SQ_INSTS_VALU", wl)
     return {
         "kernel": "k_lrf8 + k_lrf (hand-overs)",
         "bound": "hbm",
@@ -377,8 +413,9 @@ def lrf_roofline(ktot, kms, steps, k):
                 "per wavefront) and the exact one-query-per-wavefront k_lrf for the points it hands over, one HIP-event "
                 "bracket; algorithmic bytes = k neighbour gathers x 24 B per point (SURVEY.md §8d); the kernels are "
                 "VALU-issue bound, not HBM bound (valu_issue_busy: the fraction of the launch the SIMDs spend issuing "
-                "VALU, from the committed PMC pass; DESIGN.md §5)",
-        "valu_issue_busy": valu_busy,
+                "VALU, from this workload's committed PMC pass; DESIGN.md §5)",
+        "valu_issue_busy": busy_fraction(av, t_ms),
+        "valu_insts_per_point": round(insts / q, 1) if (insts and q) else None,
         "achieved": round(achieved, 2),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
@@ -393,38 +430,41 @@ def lrf_roofline(ktot, kms, steps, k):
 
 
 # HBM bytes k_reduce reads per source point of an active pair in one iteration: every point
-# its correspondence's float distance (the trim key, 4 B); a kept one also its target index
-# (4), both f64 points (2 x 24), and per estimator the target normal (pt2pl, 24), both GICP
-# covariances (2 x 48), the two cf confidences (2 x 8)
-# per kept correspondence: index 4 + distance 4 + source and target points 2 x 24, plus the
-# target normal 24 (pt2pl) or both normals 2 x 24 (GICP: the covariances are recomputed
-# from them, ISR.cpp:33-52) and both confidences 2 x 8 (cf)
+# its correspondence's float distance (the trim key, 4 B); a kept correspondence also its
+# target index 4, both f64 points 2 x 24, plus the target normal 24 (pt2pl) or both normals
+# 2 x 24 (GICP: the covariances are recomputed from them, ISR.cpp:33-52) and both
+# confidences 2 x 8 (cf)
 REDUCE_BYTES_KEPT = {"pt2pt": 56, "pt2pl": 80, "gicp": 104, "gicp_cf": 120}
 
 
-def reduce_roofline(res, pairs, W, red_ms):
+def reduce_roofline(res, pairs, W, red_ms, wl):
     """k_reduce + k_reduce_final (the per-iteration estimator sums, ISR.cpp:689-703 / 57-110,
     and the device-side solve) against HBM: algorithmic bytes of every iteration of every
-    pair (REDUCE_BYTES_KEPT per kept correspondence, 4 B per trimmed one) over their time."""
+    pair (REDUCE_BYTES_KEPT per kept correspondence, 4 B per trimmed one) over their time.
+    A step launches the pair max(num_iterations) + 1 times (the loop stops on an empty
+    iteration, whose launches return at once), as the kernel trace counts them."""
     key = "gicp_cf" if W["run"] == "cf" else W["variant"]
     ratio = np.float32(W["params"].get("estimated_overlap", 1.0))
-    tot, corr, launches = 0.0, 0.0, 0
+    tot, corr, iters = 0.0, 0.0, 0
     for r, (s, _) in zip(res, pairs):
         ns = s.shape[0]
         k = int(np.floor(ratio * np.float32(ns)))
         k = ns if k >= ns else k
         tot += r.num_iterations * (k * REDUCE_BYTES_KEPT[key] + (ns - k) * 4)
         corr += r.num_iterations * k
-        launches = max(launches, r.num_iterations)
+        iters = max(iters, r.num_iterations)
+    launches = iters + 1
     achieved = tot / (red_ms / 1000.0) / 1e9 if red_ms > 0 else 0.0
-    traffic, src = pmc_traffic("k_reduce(")
+    traffic, src = pmc_traffic(["k_reduce(", "k_reduce_final("], wl)
     return {"kernel": "k_reduce + k_reduce_final", "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "avg_launch_ms": round(red_ms / max(1, launches), 4),
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "avg_launch_ms": round(red_ms / launches, 4),
             "launches": launches, "bytes_per_unit": {"kept_correspondence": REDUCE_BYTES_KEPT[key], "trimmed": 4},
-            "units_per_launch": {"kept_correspondences": round(corr / max(1, launches))},
+            "units_per_launch": {"kept_correspondences": round(corr / launches),
+                                 "algorithmic_bytes": round(tot / launches)},
             "traffic": traffic, "traffic_source": src,
-            "note": "one launch pair per loop iteration for every active pair of the batch; the 28 sums per pair are "
-                    "then solved on the device (k_reduce_final)"}
+            "note": "one launch pair per loop iteration for every active pair of the batch (HIP events around the "
+                    "two kernels in the profiled step); the 28 sums per pair are then solved on the device "
+                    "(k_reduce_final); traffic = both kernels' PMC bytes per launch from this workload's pass"}
 
 
 def bench_batch64(args, W, params, dev, devi, steps=3):
@@ -489,21 +529,28 @@ def host_info():
 
 def cpu_baseline(pairs, gpu_res, W, gpu_value, gpu_params=None, devi=0, budget_s=25.0):
     """BASELINE.md §2 protocol: the oracle (C++/OpenMP restatement of the reference, kd-tree
-    NN) on the host cores — all physical cores, the cgroup's CPU share when it is smaller,
-    and 1 thread; 1 warm-up pair, then the median of 3 repeats of a sample of the rank's
-    pairs (a repeat set is cut short once a thread count has used `budget_s`)."""
+    NN) on the host cores — as many threads as the host lets this process use (the smallest
+    of physical cores, cgroup CPU quota and affinity mask, named in `threads_limited_by`) and
+    1 thread; 1 warm-up pair, then the median of 3 repeats of a sample of the rank's pairs (a
+    repeat set is cut short once a thread count has used `budget_s`).  The ideal full host
+    (1-thread rate x every physical core) is reported as speedup_vs_1thread_x_physical_cores."""
     from oracle import refcpu
     info = host_info()
     run = {"se3": refcpu.RUN_SE3_ICP, "cf": refcpu.RUN_SE3_ICP_CF}[W["run"]]
     p = refcpu.default_params(**W["params"])
     phys = int(info["physical_cores"])
-    counts = [phys]
+    # the host's usable cores: physical cores, the cgroup's CPU quota and the affinity mask,
+    # whichever is smallest (more OpenMP threads than that only measures oversubscription)
     quota = info.get("cgroup_cpu_quota")
-    if quota and int(quota) < phys:
-        counts.append(int(quota))
-    counts.append(1)
+    limits = {"physical_cores": phys, "affinity_cpus": int(info["affinity_cpus"])}
+    if quota:
+        limits["cgroup_cpu_quota"] = max(1, int(quota))
+    limit_name = min(limits, key=lambda k: limits[k])
+    usable = limits[limit_name]
+    info["threads_limit"] = {"threads": usable, "limited_by": limit_name, "limits": limits}
+    counts = [usable, 1] if usable > 1 else [1]
     log(f"cpu baseline: host {info.get('model')} sockets {info.get('sockets')} physical {phys} "
-        f"nproc {info['nproc']} cgroup quota {quota}; thread counts {counts}")
+        f"nproc {info['nproc']} cgroup quota {quota}; {usable} threads ({limit_name}) and 1")
 
     def reg(i):
         s, t = pairs[i]
@@ -511,7 +558,7 @@ def cpu_baseline(pairs, gpu_res, W, gpu_value, gpu_params=None, devi=0, budget_s
         r = refcpu.register(s, t, run, W["variant"], p)
         return r, time.perf_counter() - t0
 
-    refcpu.set_num_threads(counts[-2] if len(counts) > 2 else counts[0])
+    refcpu.set_num_threads(counts[0])
     first, t_warm = reg(0)  # warm-up pair (page-in, OpenMP pool); also the parity sample
     log(f"cpu baseline: warm-up pair {t_warm:.2f}s")
     # sample: enough pairs that one multi-thread repeat takes >= ~2 s
@@ -557,6 +604,7 @@ def cpu_baseline(pairs, gpu_res, W, gpu_value, gpu_params=None, devi=0, budget_s
     one = [r for r in runs if r["threads"] == 1][0]
     npts = int(np.mean([pr[0].shape[0] + pr[1].shape[0] for pr in pairs]) / 2)
     base = {"value": best["iter_per_s"], "unit": "ICP iterations/s", "cores": best["threads"], "kind": "port",
+            "threads_limited_by": limit_name,
             "sample": f"{best['pairs']} of the rank's pairs (~{npts} pts/cloud, {W['method']}, same params) end to "
                       f"end incl. setup, median of {best['repeats']} repeats after 1 warm-up pair; "
                       f"{best['pairs_per_s']} pairs/s",

@@ -724,16 +724,20 @@ void init_gicp(Cloud& c, double eps) {
 struct Corr { int q, m; float dist; };
 
 // [3P] PCL CorrespondenceRejectorTrimmed::getRemainingCorrespondences (float ratio,
-// floor(ratio*N), sort by distance).  Unstable-sort ties are broken by query index.
+// nvalid = max(floor(ratio*N), nr_min_correspondences_ = 0)).  When nvalid >= N the input
+// is copied unchanged (query order: the estimator then sums in query order); otherwise it
+// is sorted by distance and cut to nvalid.  Unstable-sort ties are broken by query index.
 std::vector<Corr> trim(const std::vector<Corr>& in, double overlap) {
     float ratio = std::min(1.0f, std::max(0.0f, (float)overlap));
     std::vector<Corr> out = in;
     if (in.empty()) return out;
-    unsigned nvalid = (unsigned)std::floor(ratio * (float)in.size());
+    const unsigned nr_min_correspondences = 0;  // PCL's default, never set at ISR.cpp:634-635
+    const unsigned nvalid = std::max((unsigned)std::floor(ratio * (float)in.size()), nr_min_correspondences);
+    if (nvalid >= out.size()) return out;
     std::sort(out.begin(), out.end(), [](const Corr& a, const Corr& b) {
         return a.dist < b.dist || (a.dist == b.dist && a.q < b.q);
     });
-    if (nvalid < out.size()) out.resize(nvalid);
+    out.resize(nvalid);
     return out;
 }
 

@@ -118,6 +118,7 @@ int Engine::init() {
     HIPCHK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
     for (auto& e : fork_ev_) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto& e : join_ev_) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto& e : join3_ev_) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (const char* e = std::getenv("SE3ICP_NN_TRACE")) nn_trace_ = std::atoi(e) != 0;
     return 0;
 }
@@ -150,6 +151,8 @@ Engine::~Engine() {
     for (auto& e : fork_ev_)
         if (e) (void)hipEventDestroy(e);
     for (auto& e : join_ev_)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& e : join3_ev_)
         if (e) (void)hipEventDestroy(e);
     if (side_) (void)hipStreamDestroy(side_);
     if (h_state_) (void)hipHostFree(h_state_);
@@ -694,23 +697,31 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         const bool t_se3 = detail || (do_se3 && nn_events_);
         if (detail) HIPCHK(hipEventRecord(ev[0], s));
         launch_nn_prep(v, s);
-        // the single-query grids on the side stream, beside the group grids (same-box A/B:
-        // loop -0.13 ms/step); the stage timing of profiled steps keeps them on the main stream
-        const bool fork = !t_se3 && !detail;
-        if (fork) {
-            HIPCHK(hipEventRecord(fork_ev_[it % kLoopRing], s));
-            HIPCHK(hipStreamWaitEvent(side_, fork_ev_[it % kLoopRing], 0));
-            if (do_se3) launch_nn_single(v, 12, side_);
-            if (do_r3) launch_nn_single(v, 3, side_);
-            HIPCHK(hipEventRecord(join_ev_[it % kLoopRing], side_));
-            if (do_se3) launch_nn_group(v, 12, s);
-            if (do_r3) launch_nn_group(v, 3, s);
-            HIPCHK(hipStreamWaitEvent(s, join_ev_[it % kLoopRing], 0));
-        } else {
-            if (t_se3) HIPCHK(hipEventRecord(ev[1], s));
-            if (do_se3) launch_nn_se3(v, s);
-            if (t_se3) HIPCHK(hipEventRecord(ev[2], s));
-            if (do_r3) launch_nn_r3(v, s);
+        // The single-query grids run on the side stream, beside the group grids (same-box
+        // A/B: loop -0.13 ms/step), in every configuration.  The fork event doubles as the
+        // start of the SE(3) NN bracket when that stage is timed; the bracket ends once both
+        // SE(3) grids are done (main stream after the SE(3) join), so it measures the span
+        // of the two-stream launch pair, first start to last end.
+        const int slot = it % kLoopRing;
+        hipEvent_t fork = t_se3 ? ev[1] : fork_ev_[slot];
+        HIPCHK(hipEventRecord(fork, s));
+        HIPCHK(hipStreamWaitEvent(side_, fork, 0));
+        if (do_se3) {
+            launch_nn_single(v, 12, side_);
+            HIPCHK(hipEventRecord(join_ev_[slot], side_));
+        }
+        if (do_r3) {
+            launch_nn_single(v, 3, side_);
+            HIPCHK(hipEventRecord(join3_ev_[slot], side_));
+        }
+        if (do_se3) {
+            launch_nn_group(v, 12, s);
+            HIPCHK(hipStreamWaitEvent(s, join_ev_[slot], 0));
+        }
+        if (t_se3) HIPCHK(hipEventRecord(ev[2], s));
+        if (do_r3) {
+            launch_nn_group(v, 3, s);
+            HIPCHK(hipStreamWaitEvent(s, join3_ev_[slot], 0));
         }
         if (detail) HIPCHK(hipEventRecord(ev[3], s));
         // (no recheck stage: the NN grids re-resolve their uncertified queries inline; the

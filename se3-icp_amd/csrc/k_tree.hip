@@ -1059,11 +1059,12 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
             for (int d = 0; d < D; ++d) t.tvec[(size_t)d * ld + g] = v[d];
             if (want64) {
                 if constexpr (D == 12) {  // the translation rows only (the loop reads the frames by point)
+                    // (byte offset 96*src + 72 is 8 mod 16: three 8-B loads, no double2)
                     const double* r64 = t.vec64 + (size_t)src * 12 + 9;
-                    const double2 w01 = *reinterpret_cast<const double2*>(r64);
-                    t.tvec64[g] = w01.x;
-                    t.tvec64[ld + g] = w01.y;
-                    t.tvec64[2 * ld + g] = r64[2];
+                    const double w0 = r64[0], w1 = r64[1], w2 = r64[2];
+                    t.tvec64[g] = w0;
+                    t.tvec64[ld + g] = w1;
+                    t.tvec64[2 * ld + g] = w2;
                 } else {
                     double w[3] = {0.0, 0.0, 0.0};
 #pragma unroll

@@ -152,6 +152,9 @@ def test_trim_count_is_pcl_float_floor(ratio, n, expected):
     d = np.random.default_rng(0).random(n).astype(np.float32)
     kept = refcpu.trim(d, ratio)
     assert len(kept) == expected
-    if expected:
+    if expected == n:
+        # PCL copies the input unchanged when nothing is cut: query order, not distance order
+        assert (kept == np.arange(n)).all()
+    elif expected:
         assert d[kept].max() <= np.sort(d)[expected - 1]
         assert (np.diff(d[kept]) >= 0).all()

@@ -2,8 +2,15 @@
 """Summarise rocprofv3 outputs into profiles/: per-kernel dispatch stats and PMC counters.
 
 Usage:
-  tools/pmc_summary.py --out profiles/r01_pmc.json  --pmc-dir gpurun_out/pmc_fetch gpurun_out/pmc_write ...
-  tools/pmc_summary.py --stats-md profiles/r01_kernel_stats.md --trace-dir gpurun_out/prof
+  tools/pmc_summary.py --workload C4 --command "<cmd>" --out profiles/r04_C4_pmc.json \
+      --pmc-dir gpurun_out/pmc_fetch gpurun_out/pmc_write ...
+  tools/pmc_summary.py --workload C4 --command "<cmd>" --stats-md profiles/r04_C4_kernel_stats.md \
+      --trace-dir gpurun_out/prof
+
+The stats summary also lists, per loop NN launch pair (k_nn_group<D> on the main stream and
+k_nn_single<D> on the side stream, the n-th dispatch of each), the SPAN from the first start
+to the last end -- what bench.py's roofline_other times with HIP events -- since the two
+kernels overlap and their averages do not add up to it.
 
 Each --pmc-dir holds one separate `rocprofv3 --pmc <counters> --output-format csv` pass
 (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950).  HBM bytes per launch follow
@@ -53,16 +60,34 @@ def pmc(dirs):
 
 def stats_md(dirs):
     agg = collections.defaultdict(list)
+    spans = collections.defaultdict(list)  # kernel -> [(start, end)] in time order
     for d in dirs:
         for r in _rows(d, "*kernel_trace.csv"):
-            t = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-            agg[r["Kernel_Name"]].append(t)
+            t0, t1 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            agg[r["Kernel_Name"]].append(t1 - t0)
+            spans[r["Kernel_Name"]].append((t0, t1))
     tot = sum(sum(v) for v in agg.values()) or 1
     lines = ["| kernel | calls | total ms | avg us | % |", "|---|---:|---:|---:|---:|"]
     for k, v in sorted(agg.items(), key=lambda kv: -sum(kv[1])):
         lines.append(f"| `{k[:110]}` | {len(v)} | {sum(v) / 1e6:.3f} | {sum(v) / len(v) / 1e3:.2f} | "
                      f"{100.0 * sum(v) / tot:.1f} |")
-    return "\n".join(lines) + "\n"
+    out = "\n".join(lines) + "\n"
+    pair_lines = []
+    for D in (12, 3):
+        g = sorted(v for k, vs in spans.items() if f"k_nn_group<{D}>" in k for v in vs)
+        s = sorted(v for k, vs in spans.items() if f"k_nn_single<{D}>" in k for v in vs)
+        if not g or len(g) != len(s):
+            continue
+        sp = [max(a[1], b[1]) - min(a[0], b[0]) for a, b in zip(g, s)]
+        ov = [max(0, min(a[1], b[1]) - max(a[0], b[0])) for a, b in zip(g, s)]
+        pair_lines.append(f"| k_nn_group<{D}> + k_nn_single<{D}> | {len(sp)} | {sum(sp) / 1e6:.3f} | "
+                          f"{sum(sp) / len(sp) / 1e3:.2f} | {sum(ov) / len(ov) / 1e3:.2f} |")
+    if pair_lines:
+        out += ("\n## NN launch pairs (group grid + single-query grid on two streams)\n\n"
+                "span = last end - first start of the n-th dispatch of each kernel; overlap = time both ran\n\n"
+                "| launch pair | pairs | total span ms | avg span us | avg overlap us |\n|---|---:|---:|---:|---:|\n"
+                + "\n".join(pair_lines) + "\n")
+    return out
 
 
 def main():
@@ -72,9 +97,11 @@ def main():
     ap.add_argument("--trace-dir", nargs="*", default=[])
     ap.add_argument("--stats-md")
     ap.add_argument("--command", default="")
+    ap.add_argument("--workload", default="C4", help="bench.py --workload of the profiled command (bench.py keys "
+                                                      "the PMC lookups by it)")
     a = ap.parse_args()
     if a.out:
-        res = {"command": a.command, "passes": a.pmc_dir,
+        res = {"command": a.command, "workload": a.workload, "passes": a.pmc_dir,
                "hbm_formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 bytes (gfx950 FETCH_SIZE reports 1/2)",
                "kernels": pmc(a.pmc_dir)}
         with open(a.out, "w") as f:
@@ -82,7 +109,8 @@ def main():
         print(f"wrote {a.out}: {len(res['kernels'])} kernels")
     if a.stats_md:
         with open(a.stats_md, "w") as f:
-            f.write(f"# rocprofv3 --kernel-trace --stats\n\ncommand: `{a.command}`\n\n" + stats_md(a.trace_dir))
+            f.write(f"# rocprofv3 --kernel-trace --stats ({a.workload})\n\ncommand: `{a.command}`\n\n"
+                    + stats_md(a.trace_dir))
         print(f"wrote {a.stats_md}")
 
 
