@@ -194,6 +194,7 @@ constexpr int kXcdRun = 256;   // group blocks per XCD run (16 chunks; runs deal
                                // neighbouring chunks share target leaves in one L2, SE(3) NN -3 %)
 constexpr int kSmall = 4;      // groups of at most this many queries are searched one query at a time
 constexpr int kSingleBlocks = 4096;  // grid of the one-query-per-wave kernels (4 waves per block, grid-strided)
+static_assert(kSingleBlocks % 8 == 0, "k_nn_single deals the list to the 8 XCDs in whole eighths of its grid");
 constexpr double kExpand = 1.0;      // search widening, in units of the query's displacement this iteration
 
 template <int D>
@@ -325,7 +326,7 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
         const int ta = min(tree_first(ct.n, TR.L, li), ct.n - 1);
         const int cnt = max(tree_first(ct.n, TR.L, li + 1) - ta, 1);
         // the nearest of kSeedTargets targets spread over the leaf
-        const float* tv = TR.tvec + ct.off;
+        const float* tv = TR.tvec + tree_tv_ix<D>(0, ct.off, 0);  // (the cloud's first slot)
         int best = ta;
         float bd = INFINITY;
         for (int k = 0; k < kSeedTargets; ++k) {
@@ -333,7 +334,7 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
             float d = 0.f;
 #pragma unroll
             for (int r = 0; r < D; ++r) {
-                const float e = qf[r] - tv[(size_t)r * v.ld + t];
+                const float e = qf[r] - tv[tree_tv_ix<D>(v.ld, t, r)];
                 d = fmaf(e, e, d);
             }
             best = d < bd ? t : best;
@@ -569,7 +570,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kWpe))) void
     f32x2 q2[(D + 1) / 2];
 #pragma unroll
     for (int r = 0; r < D / 2; ++r) q2[r] = f32x2{q[2 * r], q[2 * r + 1]};
-    const float* tv = TR.tvec + ct.off;
+    const float* tv = TR.tvec + tree_tv_ix<D>(0, ct.off, 0);  // (the cloud's first slot)
     const size_t ld = v.ld;
     if constexpr (D == 12) {
         s_q[lane * 3 + 0] = make_float4(q[0], q[1], q[2], q[3]);
@@ -596,7 +597,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kWpe))) void
             float s = 0.f;
 #pragma unroll
             for (int r = 0; r < D; ++r) {
-                const float e = q[r] - tv[(size_t)r * ld + tp];
+                const float e = q[r] - tv[tree_tv_ix<D>(ld, tp, r)];
                 s = fmaf(e, e, s);
             }
             thr = widen(s, INFINITY);
@@ -643,11 +644,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kWpe))) void
 #endif
             __builtin_amdgcn_wave_barrier();
             if (lane < cnt) {
-                float e[NV * 4];
-#pragma unroll
-                for (int r = 0; r < NV * 4; ++r) e[r] = (r < D) ? tv[(size_t)r * ld + ta + lane] : 0.f;
-#pragma unroll
-                for (int k = 0; k < NV; ++k) tile[lane * NV + k] = make_float4(e[4 * k], e[4 * k + 1], e[4 * k + 2], e[4 * k + 3]);
+                if constexpr (D == 12) {  // the leaf's rows: one contiguous run, three 16-B loads per lane
+                    const float4* r = reinterpret_cast<const float4*>(tv + (size_t)(ta + lane) * 12);
+                    const float4 a = r[0], b = r[1], c = r[2];
+                    tile[lane * 3] = a;
+                    tile[lane * 3 + 1] = b;
+                    tile[lane * 3 + 2] = c;
+                } else {
+                    tile[lane] = make_float4(tv[ta + lane], tv[ld + ta + lane], tv[2 * ld + ta + lane], 0.f);
+                }
             }
             __builtin_amdgcn_wave_barrier();
 #ifdef SE3ICP_PROF
@@ -799,7 +804,7 @@ __device__ __forceinline__ void single_one(const View& v, const PairDev* P, int 
         const float t = fmaxf(a1, fminf(e * e, a2));
         return t + 3.f * f32_err(t, na, nb, D);
     };
-    const float* tv = TR.tvec + ct.off;
+    const float* tv = TR.tvec + tree_tv_ix<D>(0, ct.off, 0);  // (the cloud's first slot)
     const size_t ld = v.ld;
     float thr = INFINITY;
     {  // seed with the previous match
@@ -809,7 +814,7 @@ __device__ __forceinline__ void single_one(const View& v, const PairDev* P, int 
             float s = 0.f;
 #pragma unroll
             for (int r = 0; r < D; ++r) {
-                const float e = q[r] - tv[(size_t)r * ld + tp];
+                const float e = q[r] - tv[tree_tv_ix<D>(ld, tp, r)];
                 s = fmaf(e, e, s);
             }
             thr = widen(s, INFINITY);
@@ -847,14 +852,8 @@ __device__ __forceinline__ void single_one(const View& v, const PairDev* P, int 
                 float d = INFINITY;
                 if (lane < tb - ta) {
                     const int x = ta + lane;
-                    if constexpr (D == 12) {
-                        f32x2 e, s2;
-#pragma unroll
-                        for (int r = 0; r < 6; ++r) {
-                            e = q2[r] - f32x2{tv[(size_t)(2 * r) * ld + x], tv[(size_t)(2 * r + 1) * ld + x]};
-                            s2 = (r == 0) ? e * e : __builtin_elementwise_fma(e, e, s2);
-                        }
-                        d = s2.x + s2.y;
+                    if constexpr (D == 12) {  // the target's 48-B row (the broadcast sweep's arithmetic)
+                        d = dist12(q2, reinterpret_cast<const float4*>(tv + (size_t)x * 12));
                     } else {
                         float e, acc;
                         e = q[0] - tv[x]; acc = e * e;
@@ -868,15 +867,21 @@ __device__ __forceinline__ void single_one(const View& v, const PairDev* P, int 
                 a2 = __builtin_amdgcn_fmed3f(a1, a2, d);
                 b1 = lt ? ta + lane : b1;
                 a1 = lt ? d : a1;
-                // wave top-2: the smallest lane best, then the smallest of the other lanes'
-                // bests and the winner's second (ties between lanes: d2 = d1)
+                // the pruning threshold needs only the wave's best: one wave minimum per leaf;
+                // the second-best (which could cap the widened radius below (sqrt(d1) + 2m)^2)
+                // is left out here -- a wider ball, never a wrong answer -- and the wave's
+                // top-2 is formed once, after the search, from the lanes' own top-2
                 d1 = wave_minf(a1);
-                const unsigned long long win = __ballot(a1 == d1);
-                const float other = wave_minf(a1 == d1 ? a2 : a1);
-                d2 = __popcll(win) > 1 ? d1 : other;
-                if (d1 < INFINITY) thr = fminf(thr, widen(d1, d2));
+                if (d1 < INFINITY) thr = fminf(thr, widen(d1, INFINITY));
             }
         }
+    }
+    {  // wave top-2: the smallest lane best, then the smallest of the other lanes' bests and
+       // the winner's second (ties between lanes: d2 = d1)
+        d1 = wave_minf(a1);
+        const unsigned long long win = __ballot(a1 == d1);
+        const float other = wave_minf(a1 == d1 ? a2 : a1);
+        d2 = __popcll(win) > 1 ? d1 : other;
     }
     int i1 = -1;
     {
@@ -889,14 +894,20 @@ __device__ __forceinline__ void single_one(const View& v, const PairDev* P, int 
 }
 
 // grid-stride over the single-query list of the phase: SE(3) entries from the front,
-// R3 entries from the back (counters flag_count[1], [2])
+// R3 entries from the back (counters flag_count[1], [2]).  The list holds each sparse
+// chunk's queries together (nearby points: they read the same target leaves), so every XCD
+// takes one contiguous eighth of it (blocks are dealt to the XCDs round-robin): neighbouring
+// queries' leaf reads meet in one L2 instead of being fetched by all eight.
 template <int D>
 __global__ __launch_bounds__(256) void k_nn_single(View v) {
     const int lane = threadIdx.x & 63;
-    const int w0 = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
     const int nq = __builtin_amdgcn_readfirstlane(v.flag_count[D == 12 ? 1 : 2]);
+    const int xcd = blockIdx.x & 7, nbx = gridDim.x >> 3;  // (gridDim.x: a multiple of 8)
+    const int seg = (nq + 7) >> 3;
+    const int f_end = min(nq, (xcd + 1) * seg);
+    const int w0 = __builtin_amdgcn_readfirstlane(xcd * seg + (int)(blockIdx.x >> 3) * 4 + (int)(threadIdx.x >> 6));
     unsigned n_eval = 0, n_box = 0;
-    for (int f = w0; f < nq; f += gridDim.x * 4) {
+    for (int f = w0; f < f_end; f += nbx * 4) {
         const int gx = __builtin_amdgcn_readfirstlane(D == 12 ? v.sq_list[f] : v.sq_list[v.ld - 1 - f]);
         const int pair = v.cloud_of[gx] >> 1;
         const PairDev* P = v.pairs + pair;

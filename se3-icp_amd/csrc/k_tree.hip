@@ -1055,8 +1055,14 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
         if (in) {
             t.perm[g] = p;
             t.pos[src] = A + x;
+            if constexpr (D == 12) {
+                float4* o = reinterpret_cast<float4*>(t.tvec + (size_t)g * 12);
 #pragma unroll
-            for (int d = 0; d < D; ++d) t.tvec[(size_t)d * ld + g] = v[d];
+                for (int k = 0; k < 3; ++k) o[k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+            } else {
+#pragma unroll
+                for (int d = 0; d < D; ++d) t.tvec[(size_t)d * ld + g] = v[d];
+            }
             if (want64) {
                 if constexpr (D == 12) {  // the translation rows only (the loop reads the frames by point)
                     // (byte offset 96*src + 72 is 8 mod 16: three 8-B loads, no double2)
@@ -1125,14 +1131,9 @@ __global__ __launch_bounds__(256) void k_tree_finish(TreeView t) {
         const bool want64 = (t.tvec64 != nullptr) & !((t.vec64_sources_only != 0) & ((t.cloud_of[g] & 1) != 0));
         if (t.D == 12) {  // one 48-B and one 96-B row per point (16-B loads)
             const float4* r32 = reinterpret_cast<const float4*>(t.vec + (size_t)src * 12);
+            float4* o = reinterpret_cast<float4*>(t.tvec + (size_t)g * 12);
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const float4 x = r32[k];
-                t.tvec[(size_t)(4 * k) * t.ld + g] = x.x;
-                t.tvec[(size_t)(4 * k + 1) * t.ld + g] = x.y;
-                t.tvec[(size_t)(4 * k + 2) * t.ld + g] = x.z;
-                t.tvec[(size_t)(4 * k + 3) * t.ld + g] = x.w;
-            }
+            for (int k = 0; k < 3; ++k) o[k] = r32[k];
             if (want64) {  // the translation rows only
                 const double* r64 = t.vec64 + (size_t)src * 12 + 9;
                 for (int k = 0; k < 3; ++k) t.tvec64[(size_t)k * t.ld + g] = r64[k];
@@ -1164,7 +1165,7 @@ __global__ __launch_bounds__(256) void k_tree_leafbox(TreeView t) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
         float lo = INFINITY, hi = -INFINITY;
-        if (valid) lo = hi = t.tvec[(size_t)d * t.ld + cl.off + a + lane];
+        if (valid) lo = hi = t.tvec[tree_tv_ix<D>(t.ld, cl.off + a + lane, d)];
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) {
             lo = fminf(lo, __shfl_xor(lo, o, 64));

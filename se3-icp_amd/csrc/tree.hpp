@@ -26,7 +26,7 @@ struct TreeView {
     const float* vec;  // input vectors, original order: 12-D [ld][12] rows, 3-D [3][ld] columns
     int32_t* perm;     // [ld] tree position (global slot) -> local point index
     int32_t* pos;      // [ld] point (global slot) -> local tree position
-    float* tvec;       // [D][ld] vectors in tree order
+    float* tvec;       // vectors in tree order: 3-D [3][ld] columns, 12-D [ld][12] rows (tree_tv_ix)
     const double* vec64;  // optional f64 vectors (original order, the layout of vec) ...
     double* tvec64;       // ... copied into tree order (coalesced leaf / query-chunk loads): [3][ld], the
                           // points (3-D) or the translation rows (12-D: the loop reads whole frames by point)
@@ -54,6 +54,14 @@ __host__ __device__ __forceinline__ int tree_heap(int level, int i) { return (1 
 // points columns
 __device__ __forceinline__ size_t tree_in_ix(const TreeView& t, int d, int p) {
     return t.D == 12 ? (size_t)p * 12 + d : (size_t)d * t.ld + p;
+}
+
+// element d of the tree-ordered vector at global tree slot x: the 12-D vectors are 48-B
+// rows (a leaf's 64 targets are one contiguous 3-KB run: three 16-B loads per lane instead
+// of twelve strided ones), the 3-D points columns
+template <int D>
+__host__ __device__ __forceinline__ size_t tree_tv_ix(size_t ld, int x, int d) {
+    return D == 12 ? (size_t)x * 12 + d : (size_t)d * ld + x;
 }
 
 inline int tree_depth_for(int max_n) {

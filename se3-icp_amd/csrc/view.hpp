@@ -31,7 +31,7 @@ struct TreeRef {
     int32_t nnodes;   // heap slots per cloud
     const int32_t* perm;  // [ld] tree position (cloud.off + x) -> local point index
     const int32_t* pos;   // [ld] point (cloud.off + i) -> local tree position
-    const float* tvec;    // [D][ld] vectors in tree order
+    const float* tvec;    // vectors in tree order: 3-D [3][ld] columns, 12-D [ld][12] rows (tree_tv_ix)
     const double* tvec64; // [3][ld] f64 in tree order: the points (3-D), the frames' translation rows (12-D)
     const double4* tpt64; // [ld] the same, one (x, y, z, 0) record per point (3-D trees: the setup's gathers)
     const float* lo;      // [nclouds][nnodes][D]
