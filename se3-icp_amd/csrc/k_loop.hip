@@ -457,36 +457,52 @@ __global__ __launch_bounds__(256) void k_reduce(View v) {
                 Mi[2][1] = M[0][1] * M[2][0] - M[0][0] * M[2][1];
                 Mi[2][2] = M[0][0] * M[1][1] - M[0][1] * M[1][0];
                 const double det = M[0][0] * Mi[0][0] + M[0][1] * Mi[1][0] + M[0][2] * Mi[2][0];
-                const double idet = 1.0 / det;
-                // J^T J = G^T M^-1 G and J^T r = G^T M^-1 d are invariant to the choice of
-                // W with W^T W = M^-1; the reference uses W = M^-1/2 (ISR.cpp:78), here
-                // W = L^T with M^-1 = L L^T (Cholesky), which needs no matrix square root.
-                double A[3][3];
-#pragma unroll
-                for (int a = 0; a < 3; ++a)
-#pragma unroll
-                    for (int b = 0; b < 3; ++b) A[a][b] = 0.5 * (Mi[a][b] + Mi[b][a]) * idet;
-                // Cholesky A = L L^T; rows of L^T G are 3 weighted Jacobian rows
-                const double l00 = sqrt(A[0][0]);
-                const double l10 = A[1][0] / l00, l20 = A[2][0] / l00;
-                const double l11 = sqrt(A[1][1] - l10 * l10);
-                const double l21 = (A[2][1] - l20 * l10) / l11;
-                const double l22 = sqrt(A[2][2] - l20 * l20 - l21 * l21);
-                const double Lt[3][3] = {{l00, l10, l20}, {0, l11, l21}, {0, 0, l22}};
-                // G = [-[vs]x, I]
-                const double G[3][6] = {{0, vs[2], -vs[1], 1, 0, 0}, {-vs[2], 0, vs[0], 0, 1, 0}, {vs[1], -vs[0], 0, 0, 0, 1}};
-                const double d[3] = {vs[0] - vt[0], vs[1] - vt[1], vs[2] - vt[2]};
-#pragma unroll
-                for (int a = 0; a < 3; ++a) {
-#pragma unroll
-                    for (int b = 0; b < 6; ++b) J[a][b] = Lt[a][0] * G[0][b] + Lt[a][1] * G[1][b] + Lt[a][2] * G[2][b];
-                    r[a] = Lt[a][0] * d[0] + Lt[a][1] * d[1] + Lt[a][2] * d[2];
-                }
-                nrows = 3;
                 if (P->cf) {
                     const double wc = (v.conf64[g] + v.conf64[gt]) / 2.0;  // ISR.cpp:913
                     wgt = wc * wc;
                 }
+                // J^T J = G^T M^-1 G and J^T r = G^T M^-1 d for every W with W^T W = M^-1
+                // (the reference's W = M^-1/2, ISR.cpp:78, is one of them), so the sums are
+                // formed from A = w^2 M^-1 and G = [S | I], S = -[vs]x, without a matrix root
+                // or factor: J^T J = [[S^T A S, S^T A], [A S, A]], J^T r = [S^T A d; A d].
+                const double sc = wgt / det;
+                double A[3][3];
+#pragma unroll
+                for (int a = 0; a < 3; ++a)
+#pragma unroll
+                    for (int b = 0; b < 3; ++b) A[a][b] = 0.5 * (Mi[a][b] + Mi[b][a]) * sc;
+                const double S[3][3] = {{0, vs[2], -vs[1]}, {-vs[2], 0, vs[0]}, {vs[1], -vs[0], 0}};
+                const double d[3] = {vs[0] - vt[0], vs[1] - vt[1], vs[2] - vt[2]};
+                double B[3][3];  // A S
+#pragma unroll
+                for (int a = 0; a < 3; ++a)
+#pragma unroll
+                    for (int b = 0; b < 3; ++b) B[a][b] = A[a][0] * S[0][b] + A[a][1] * S[1][b] + A[a][2] * S[2][b];
+                double H[6][6];
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+#pragma unroll
+                    for (int b = a; b < 3; ++b) H[a][b] = S[0][a] * B[0][b] + S[1][a] * B[1][b] + S[2][a] * B[2][b];
+#pragma unroll
+                    for (int b = 0; b < 3; ++b) {
+                        H[a][3 + b] = B[b][a];     // (S^T A)[a][b] = (A S)[b][a]
+                        H[3 + a][3 + b] = A[a][b];
+                    }
+                }
+                double Ad[3];
+#pragma unroll
+                for (int a = 0; a < 3; ++a) Ad[a] = A[a][0] * d[0] + A[a][1] * d[1] + A[a][2] * d[2];
+                int k = 0;
+#pragma unroll
+                for (int a = 0; a < 6; ++a)
+#pragma unroll
+                    for (int b = a; b < 6; ++b) acc[k++] += H[a][b];
+#pragma unroll
+                for (int a = 0; a < 3; ++a) {
+                    acc[21 + a] += S[0][a] * Ad[0] + S[1][a] * Ad[1] + S[2][a] * Ad[2];
+                    acc[24 + a] += Ad[a];
+                }
+                nrows = 0;
             }
 #pragma unroll
             for (int rr = 0; rr < 3; ++rr) {
@@ -548,16 +564,24 @@ __global__ __launch_bounds__(kFinThreads) void k_reduce_final(View v, const int3
     __shared__ double tot[kRedVals];
     const int i = threadIdx.x % kRedVals, s = threadIdx.x / kRedVals;
     const int wb = pair_wb[p], wn = pair_wn[p];
-    if (s < kFinChunks) {  // four independent chains per lane: four loads in flight
-        constexpr int C = kFinChunks;
-        double s4[4] = {0.0, 0.0, 0.0, 0.0};
+    if (s < kFinChunks) {  // eight independent chains per lane: eight loads in flight
+        constexpr int C = kFinChunks, U = 8;
+        double s8[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) s8[u] = 0.0;
         const double* rp = v.red_partial + (size_t)wb * kRedVals + i;
         int b = s;
-        for (; b + 3 * C < wn; b += 4 * C)
+        for (; b + (U - 1) * C < wn; b += U * C) {
+            double x[U];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) s4[u] += rp[(size_t)(b + C * u) * kRedVals];
-        for (; b < wn; b += C) s4[0] += rp[(size_t)b * kRedVals];
-        part[s][i] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+            for (int u = 0; u < U; ++u) x[u] = rp[(size_t)(b + C * u) * kRedVals];
+#pragma unroll
+            for (int u = 0; u < U; ++u) s8[u] += x[u];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (b + C * u < wn) s8[u] += rp[(size_t)(b + C * u) * kRedVals];
+        part[s][i] = ((s8[0] + s8[1]) + (s8[2] + s8[3])) + ((s8[4] + s8[5]) + (s8[6] + s8[7]));
     }
     __syncthreads();
     if (threadIdx.x < kRedVals) {

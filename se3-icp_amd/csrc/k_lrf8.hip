@@ -71,11 +71,11 @@ static_assert(kCap >= kParkAt + 2 * P8_N && kStride >= kCap, "the park overlays 
 // lane ^ m within a group of eight lanes (m = 1..7 as used by the networks)
 __device__ __forceinline__ unsigned gx(unsigned x, int m) {
     switch (m) {
-    case 1: return (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-    case 2: return (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-    case 3: return (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x1B, 0xF, 0xF, false);   // quad_perm [3,2,1,0]
+    case 1: return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
+    case 2: return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
+    case 3: return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x1B, 0xF, 0xF, true);   // quad_perm [3,2,1,0]
     case 4: return (unsigned)__builtin_amdgcn_ds_swizzle((int)x, 0x101F);                      // xor 4
-    case 7: return (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    case 7: return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, true);  // row_half_mirror
     default: return (unsigned)__shfl_xor((int)x, m, 64);
     }
 }
@@ -85,9 +85,20 @@ __device__ __forceinline__ double gxd(double x, int m) {
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
+// the median of (a, b, x): min(a, b) for x = 0, max(a, b) for x = ~0u -- a cross-lane
+// compare-exchange in one instruction after the partner's value is fetched (instead of a
+// min, a max and a lane select)
+__device__ __forceinline__ unsigned med3u(unsigned a, unsigned b, unsigned x) {
+    unsigned r;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(x));
+    return r;
+}
+
 // Ascending bitonic sort of the 8*PER keys of a group of eight lanes (element e =
 // l*PER + s in k[s] of group lane l), every comparator ascending (each merge starts with
-// the "flip" step e <-> e ^ (KK-1)): an in-register compare-exchange is a min and a max.
+// the "flip" step e <-> e ^ (KK-1)): an in-register compare-exchange is a min and a max,
+// a cross-lane one the partner's value (DPP / swizzle) and a med3 against 0 (the lower
+// lane keeps the min) or ~0 (the upper lane keeps the max).
 // Stages are instantiated at compile time (template recursion) so that every register
 // index is a constant.
 template <int PER, int KK, int JD>
@@ -105,13 +116,13 @@ __device__ __forceinline__ void stage8(unsigned (&k)[PER], int l) {
             }
         } else {
             constexpr int lm = KK / PER - 1;
-            const bool lower = (l & (KK / PER / 2)) == 0;
+            const unsigned x = (l & (KK / PER / 2)) == 0 ? 0u : ~0u;  // lower lane: min
 #pragma unroll
             for (int s = 0; s < PER / 2; ++s) {
                 const int t = PER - 1 - s;
                 const unsigned a = gx(k[t], lm), b = gx(k[s], lm);
-                k[s] = lower ? min(k[s], a) : max(k[s], a);
-                k[t] = lower ? min(k[t], b) : max(k[t], b);
+                k[s] = med3u(k[s], a, x);
+                k[t] = med3u(k[t], b, x);
             }
         }
     } else if constexpr (JD < PER) {
@@ -126,12 +137,9 @@ __device__ __forceinline__ void stage8(unsigned (&k)[PER], int l) {
         }
     } else {
         constexpr int lm = JD / PER;
-        const bool lower = (l & lm) == 0;
+        const unsigned x = (l & lm) == 0 ? 0u : ~0u;  // lower lane: min
 #pragma unroll
-        for (int s = 0; s < PER; ++s) {
-            const unsigned p = gx(k[s], lm);
-            k[s] = lower ? min(k[s], p) : max(k[s], p);
-        }
+        for (int s = 0; s < PER; ++s) k[s] = med3u(k[s], gx(k[s], lm), x);
     }
 }
 template <int PER, int N, int KK = 2, int JD = 0>

@@ -12,8 +12,8 @@ namespace se3icp {
 
 __device__ __forceinline__ unsigned xor_lane(unsigned x, int m) {
     switch (m) {
-    case 1: return (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-    case 2: return (unsigned)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+    case 1: return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
+    case 2: return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
     case 4: return (unsigned)__builtin_amdgcn_ds_swizzle((int)x, 0x101F);  // and 0x1f, xor 4
     case 8: return (unsigned)__builtin_amdgcn_ds_swizzle((int)x, 0x201F);
     case 16: {

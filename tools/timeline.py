@@ -28,9 +28,8 @@ def load(d):
 
 
 def short(name):
-    n = name.split("(")[0]
-    n = n.replace("se3icp::(anonymous namespace)::", "").replace("void ", "")
-    return n
+    n = name.replace("se3icp::(anonymous namespace)::", "").replace("void ", "")
+    return n.split("(")[0]
 
 
 def main():
