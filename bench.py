@@ -345,31 +345,29 @@ def main():
 
 
 def nn_roofline(ktot, kms, wl):
-    """The loop's dominant NN launch (k_nn_group + k_nn_single of the phase with more time):
+    """The loop's dominant NN launch (k_nn_search of the phase with more time):
     work actually issued, counted on the device — lane x target distance evaluations
     (3D flop: D sub + D FMA) and lane x box tests (4D flop: 2D sub/max + D FMA)."""
     dom = max(["nn_se3_ms", "nn_r3_ms"], key=lambda k: kms[k])
     if dom == "nn_se3_ms":
         D, evals, boxes, nl, kname = 12, ktot["se3_dist_evals"], ktot["se3_box_tests"], ktot["nn_se3_launches"], \
-            "k_nn_group<12> + k_nn_single<12>"
+            "k_nn_search<12>"
     else:
         D, evals, boxes, nl, kname = 3, ktot["r3_dist_evals"], ktot["r3_box_tests"], ktot["nn_r3_launches"], \
-            "k_nn_group<3> + k_nn_single<3>"
+            "k_nn_search<3>"
     t_ms = kms[dom]
     flop_dist, flop_box = 3 * D, 4 * D
     flops = evals * flop_dist + boxes * flop_box
     achieved = flops / (t_ms / 1000.0) / 1e12 if t_ms > 0 else 0.0
     nl = max(1.0, nl)
-    traffic, src = pmc_traffic([f"k_nn_group<{D}>", f"k_nn_single<{D}>"], wl)
+    traffic, src = pmc_traffic([f"k_nn_search<{D}>"], wl)
     return {
         "kernel": kname,
         "bound": "valu",
         "note": "f32 VALU kd-tree sweep (leaf distance sweeps + box tests; no MFMA issued), priced against the "
-                "f32 vector peak.  A launch is the group grid (main stream) and the single-query grid (side "
-                "stream, forked after k_nn_prep) running side by side; avg_launch_ms is their SPAN, first start "
-                "to last end (HIP events: the fork event on the main stream to a marker after the join), which "
-                "is what tools/nn_span.py computes per launch pair from the committed kernel trace (rocprof's "
-                "per-kernel averages overlap and do not add up to it).  The time includes the inline f64 "
+                "f32 vector peak.  A launch is one grid: one-query-per-wave searches of the sparse chunks' "
+                "queries, then the 64-query groups; avg_launch_ms is its HIP-event time in the profiled step "
+                "(the kernel's rocprof average in the committed trace).  The time includes the inline f64 "
                 "recheck of the ~0.4 % uncertified queries, whose flops are not counted",
         "achieved": round(achieved, 3),
         "peak": FP32_PEAK_TFLOPS,

@@ -144,10 +144,8 @@ int se3icp_register_batch(int device, int32_t n_pairs, const double* const* src_
 /* Same, with all clouds already resident in HBM: d_src_xyz / d_tgt_xyz are
  * device pointers to the concatenation of every pair's AoS xyz; the host arrays
  * src_off/tgt_off (n_pairs+1 entries) give each pair's point range.
- * `hip_stream` is a hipStream_t (NULL = the engine's own stream).  The loop also runs the
- * single-query NN grids on an internal second stream, forked from and joined back into
- * `hip_stream` by events each iteration, so work queued on `hip_stream` before the call
- * is ordered before all of the batch's kernels. */
+ * `hip_stream` is a hipStream_t (NULL = the engine's own stream); every kernel of the batch
+ * runs on it, so work queued on `hip_stream` before the call is ordered before them. */
 int se3icp_register_batch_device(int device, int32_t n_pairs, const double* d_src_xyz, const int64_t* src_off,
                                  const double* d_tgt_xyz, const int64_t* tgt_off, int method,
                                  const se3icp_params* params, se3icp_result* results, void* hip_stream);

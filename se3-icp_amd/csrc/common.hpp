@@ -51,10 +51,19 @@ struct PairDev {
     int32_t _pad;
 };
 
-// Static work table: one entry per 256-query block of every pair.
+// k_reduce: threads per block, queries per thread (all of a thread's loads are issued
+// before its first term; measured at C4: 2 per thread 146 VGPRs, 1,024-thread blocks: both
+// slower than 256 x 1) and queries per block
+constexpr int kRedThreads = 256;
+constexpr int kRedPer = 1;
+constexpr int kRedQ = kRedThreads * kRedPer;
+
+// Static work table of k_reduce: one entry per kRedQ-query block of every pair.
 struct BlockWork {
     int32_t pair;
-    int32_t q0;            // first local query index of the block
+    int32_t q0, q1;        // local query range [q0, q1) of the block
+    int32_t s_off, t_off;  // global slots of the pair's source / target cloud
+    int32_t _pad[3];
 };
 
 }  // namespace se3icp

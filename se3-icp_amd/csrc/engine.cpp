@@ -77,16 +77,20 @@ hipError_t spin_wait(hipEvent_t e) {
     }
 }
 
-// Wait until k_reduce_final has written every pair's next phase into the coherent host
-// slot (cleared to -1 before the iteration was queued): the loop needs no per-iteration
-// end event, whose marker leaves the GPU idle ~5 us.  A stream that completed (or failed)
-// with a slot still unwritten is reported instead of waited on.
+// Wait until every pair's phase of the next iteration is in the coherent host slot
+// (cleared to -1 before the iteration was queued; written by the next k_nn_prep, or by
+// k_reduce_final without look-ahead): the loop needs no per-iteration end event, whose
+// marker leaves the GPU idle ~5 us.  The stream is queried only after 20 ms without the slot
+// (a stream that completed or failed with it unwritten is reported, not waited on):
+// hipStreamQuery itself puts a marker into the stream, which held the GPU idle ~6 us per
+// iteration when it was called every 1,024 polls (round 3).
 hipError_t spin_phases(const volatile int32_t* slot, int n, hipStream_t s) {
+    auto next = std::chrono::steady_clock::now() + std::chrono::milliseconds(20);
     for (unsigned spins = 0;; ++spins) {
         int left = 0;
         for (int p = 0; p < n; ++p) left += slot[p] < 0;
         if (left == 0) return hipSuccess;
-        if ((spins & 1023u) == 1023u) {
+        if ((spins & 1023u) == 1023u && std::chrono::steady_clock::now() >= next) {
             const hipError_t r = hipStreamQuery(s);
             if (r == hipSuccess) {
                 left = 0;
@@ -94,6 +98,7 @@ hipError_t spin_phases(const volatile int32_t* slot, int n, hipStream_t s) {
                 return left == 0 ? hipSuccess : hipErrorUnknown;
             }
             if (r != hipErrorNotReady) return r;
+            next = std::chrono::steady_clock::now() + std::chrono::milliseconds(20);
         }
     }
 }
@@ -115,10 +120,6 @@ int Engine::init() {
     HIPCHK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
     for (auto& e : ev_) HIPCHK(hipEventCreate(&e));
     for (auto& e : loop_ev_) HIPCHK(hipEventCreate(&e));
-    HIPCHK(hipStreamCreateWithFlags(&side_, hipStreamNonBlocking));
-    for (auto& e : fork_ev_) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    for (auto& e : join_ev_) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    for (auto& e : join3_ev_) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (const char* e = std::getenv("SE3ICP_NN_TRACE")) nn_trace_ = std::atoi(e) != 0;
     return 0;
 }
@@ -148,13 +149,6 @@ Engine::~Engine() {
         if (e) (void)hipEventDestroy(e);
     for (auto& e : loop_ev_)
         if (e) (void)hipEventDestroy(e);
-    for (auto& e : fork_ev_)
-        if (e) (void)hipEventDestroy(e);
-    for (auto& e : join_ev_)
-        if (e) (void)hipEventDestroy(e);
-    for (auto& e : join3_ev_)
-        if (e) (void)hipEventDestroy(e);
-    if (side_) (void)hipStreamDestroy(side_);
     if (h_state_) (void)hipHostFree(h_state_);
     if (h_phase_) (void)hipHostFree(h_phase_);
     if (stream_) (void)hipStreamDestroy(stream_);
@@ -190,7 +184,7 @@ int Engine::alloc_points(int64_t ntot, int kmax, bool knn_list) {
               ensure<int32_t>(d_flag_count_, 4) &&
               ensure<uint32_t>(d_keys0_, L) &&
               ensure<int32_t>(d_vals1_, L) && ensure<unsigned long long>(d_stats_, kStatCols * kStatSlots) &&
-              ensure<float4>(d_cert_, L) &&
+              ensure<NNCert>(d_cert_, L) &&
               ensure<int32_t>(d_sqlist_, L);
     for (TreeBufs* t : {&t3_, &t12_})
         ok = ok && ensure<int32_t>(t->perm, L) && ensure<int32_t>(t->pos, L);
@@ -252,7 +246,7 @@ View Engine::view() const {
     v.qcount = (int32_t*)d_qcount_.p;
     v.sq_list = (int32_t*)d_sqlist_.p;
     v.hist = (const double*)d_hist_.p;
-    v.cert = (float4*)d_cert_.p;
+    v.cert = (NNCert*)d_cert_.p;
     return v;
 }
 
@@ -512,7 +506,7 @@ int Engine::setup_chunks(int npairs, hipStream_t s) {
         !ensure<double>(d_hist_, (size_t)kHist * npairs * 12))
         return SE3ICP_ERR_OUT_OF_MEMORY;
     if (pinned(h_hist_, h_hist_cap_, (size_t)npairs * 12)) return SE3ICP_ERR_OUT_OF_MEMORY;
-    HIPCHK(hipMemsetAsync(d_cert_.p, 0xff, sizeof(float4) * ld_, s));  // iteration -1: no certificate
+    HIPCHK(hipMemsetAsync(d_cert_.p, 0xff, sizeof(NNCert) * ld_, s));  // iteration -1: no certificate
     return 0;
 }
 
@@ -549,13 +543,18 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     npairs_ = npairs;
     int64_t ntot = 0;
     for (int p = 0; p < npairs; ++p) ntot += ns[p] + nt[p];
-    // work table of the per-correspondence kernels: one entry per 256 queries of every pair
+    // work table of k_reduce: one entry per kRedQ queries of every pair
+    int64_t soff = 0;
     h_work_.clear();
     h_wb_.assign(npairs, 0);
     h_wn_.assign(npairs, 0);
     for (int p = 0; p < npairs; ++p) {
         h_wb_[p] = (int32_t)h_work_.size();
-        for (int64_t q0 = 0; q0 < ns[p]; q0 += kBlock) h_work_.push_back(BlockWork{p, (int32_t)q0});
+        // (clouds are laid out src 0, tgt 0, src 1, ... as setup_clouds places them)
+        for (int64_t q0 = 0; q0 < ns[p]; q0 += kRedQ)
+            h_work_.push_back(BlockWork{p, (int32_t)q0, (int32_t)std::min<int64_t>(q0 + kRedQ, ns[p]), (int32_t)soff,
+                                        (int32_t)(soff + ns[p]), {0, 0, 0}});
+        soff += ns[p] + nt[p];
         h_wn_[p] = (int32_t)h_work_.size() - h_wb_[p];
     }
     nwork_ = (int)h_work_.size();
@@ -696,33 +695,15 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         // iteration's end marker; profiled steps: every stage)
         const bool t_se3 = detail || (do_se3 && nn_events_);
         if (detail) HIPCHK(hipEventRecord(ev[0], s));
-        launch_nn_prep(v, s);
-        // The single-query grids run on the side stream, beside the group grids (same-box
-        // A/B: loop -0.13 ms/step), in every configuration.  The fork event doubles as the
-        // start of the SE(3) NN bracket when that stage is timed; the bracket ends once both
-        // SE(3) grids are done (main stream after the SE(3) join), so it measures the span
-        // of the two-stream launch pair, first start to last end.
-        const int slot = it % kLoopRing;
-        hipEvent_t fork = t_se3 ? ev[1] : fork_ev_[slot];
-        HIPCHK(hipEventRecord(fork, s));
-        HIPCHK(hipStreamWaitEvent(side_, fork, 0));
-        if (do_se3) {
-            launch_nn_single(v, 12, side_);
-            HIPCHK(hipEventRecord(join_ev_[slot], side_));
-        }
-        if (do_r3) {
-            launch_nn_single(v, 3, side_);
-            HIPCHK(hipEventRecord(join3_ev_[slot], side_));
-        }
-        if (do_se3) {
-            launch_nn_group(v, 12, s);
-            HIPCHK(hipStreamWaitEvent(s, join_ev_[slot], 0));
-        }
+        // the phases of iteration it (opened by it-1's k_reduce_final) reach the host through
+        // this k_nn_prep (ring slot it-1); without look-ahead, k_reduce_final writes them
+        launch_nn_prep(v, (lag == 1 && it >= 2) ? d_phase_ + (size_t)((it - 1) % kLoopRing) * npairs : nullptr, s);
+        // One search grid per phase (single-query waves and groups together, k_nn.hip): no
+        // second stream and no cross-stream events.  ev[1] / ev[2] bracket the SE(3) search.
+        if (t_se3) HIPCHK(hipEventRecord(ev[1], s));
+        if (do_se3) launch_nn(v, 12, s);
         if (t_se3) HIPCHK(hipEventRecord(ev[2], s));
-        if (do_r3) {
-            launch_nn_group(v, 3, s);
-            HIPCHK(hipStreamWaitEvent(s, join3_ev_[slot], 0));
-        }
+        if (do_r3) launch_nn(v, 3, s);
         if (detail) HIPCHK(hipEventRecord(ev[3], s));
         // (no recheck stage: the NN grids re-resolve their uncertified queries inline; the
         // ev[3] -> ev[4] bracket stays empty and time_recheck reads ~0)
@@ -730,7 +711,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         if (any_trim) launch_trim(v, s);
         if (detail) HIPCHK(hipEventRecord(ev[5], s));
         launch_reduce(v, (const int32_t*)d_wb_.p, (const int32_t*)d_wn_.p, (PairState*)d_state_.p, (double*)d_hist_.p,
-                      d_phase_ + (size_t)(it % kLoopRing) * npairs, s);
+                      lag == 0 ? d_phase_ + (size_t)(it % kLoopRing) * npairs : nullptr, s);
         HIPCHK(hipGetLastError());
         if (detail) HIPCHK(hipEventRecord(ev[6], s));
         loop_detail_[it % kLoopRing] = detail;
@@ -738,10 +719,20 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         return 0;
     };
     // wait for iteration `it`, add its kernel times; returns the pairs of iteration it+1
-    auto finish = [&](int it) -> int {
+    // (last: the loop's final, empty, iteration -- no k_nn_prep follows to publish its slot)
+    auto finish = [&](int it, bool last) -> int {
         hipEvent_t* ev = &loop_ev_[(it % kLoopRing) * kLoopEv];
+        // (the phase slot of iteration it is written by the next iteration's k_nn_prep, queued
+        // already, or with lag 0 by this iteration's k_reduce_final -- after its end event)
         if (loop_detail_[it % kLoopRing]) HIPCHK(spin_wait(ev[6]));
-        else HIPCHK(spin_phases(h_phase_ + (size_t)(it % kLoopRing) * npairs, npairs, s));
+        if (last && lag == 1) {
+            if (!loop_detail_[it % kLoopRing]) {
+                HIPCHK(hipEventRecord(ev_[15], s));
+                HIPCHK(spin_wait(ev_[15]));
+            }
+        } else {
+            HIPCHK(spin_phases(h_phase_ + (size_t)(it % kLoopRing) * npairs, npairs, s));
+        }
         float ms[6] = {};
         if (loop_detail_[it % kLoopRing]) {
             for (int k = 0; k < 6; ++k) HIPCHK(hipEventElapsedTime(&ms[k], ev[k], ev[k + 1]));
@@ -796,6 +787,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
             HIPCHK(hipMemset((unsigned long long*)d_stats_.p + 10, 0, sizeof(unsigned long long)));
 #endif
         }
+        if (last && lag == 1) return 0;
         const volatile int32_t* ph = h_phase_ + (size_t)(it % kLoopRing) * npairs;
         n_se3 = n_r3 = 0;
         for (int p = 0; p < npairs; ++p) {
@@ -810,7 +802,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     if (enqueue(it)) return SE3ICP_ERR_HIP;
     for (;;) {
         if (lag == 0) {
-            const int left = finish(it);
+            const int left = finish(it, false);
             if (tr) {
                 rc = record_trace(tr, it, trace_phase, s);
                 if (rc) return rc;
@@ -822,8 +814,8 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         }
         ++it;
         if (enqueue(it)) return SE3ICP_ERR_HIP;  // phase flags as of iteration it-2
-        if (finish(it - 1) == 0) {               // iteration `it` is empty
-            (void)finish(it);
+        if (finish(it - 1, false) == 0) {        // iteration `it` is empty
+            (void)finish(it, true);
             break;
         }
     }
@@ -1094,9 +1086,8 @@ int Engine::nn(const double* query, int64_t nq, const double* data, int64_t nd, 
     HIPCHK(hipMemsetAsync(d_rechecked_.p, 0, sizeof(int32_t), s));
     HIPCHK(hipMemsetAsync(d_corr_idx_.p, 0xff, sizeof(int32_t) * L, s));
     View v = view();
-    launch_nn_prep(v, s);
-    if (dim == 12) launch_nn_se3(v, s);
-    else launch_nn_r3(v, s);
+    launch_nn_prep(v, nullptr, s);
+    launch_nn(v, dim, s);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(idx, d_corr_idx_.p, sizeof(int32_t) * nq, hipMemcpyDeviceToHost, s));
     int32_t rech = 0;

@@ -97,9 +97,6 @@ class Engine {
     bool profile_ = false;
     std::mutex mu_;
     hipStream_t stream_ = nullptr;
-    // the loop's second stream: the one-query-per-wave NN grids run on it beside the group
-    // grids (independent queries), forked after k_nn_prep and joined before the trim
-    hipStream_t side_ = nullptr;
     KernelTimes ktimes_;
 
     // geometry of the current batch
@@ -112,9 +109,9 @@ class Engine {
     // se3icp_set_lrf_exact: 0 k_lrf8 + hand-overs (default), 1 the exact one-query-per-wavefront
     // k_lrf for every point, 2 the global-buffer k_knn_big for every point (all bitwise equal)
     int lrf_exact_only_ = 0;
-    // se3icp_set_nn_events(0): no HIP event bracket around the SE(3) NN launch pair outside
-    // profiled batches (the end marker leaves the GPU idle a few us; the fork event is recorded
-    // either way; time_se3_correspondence_search_ms is then 0)
+    // se3icp_set_nn_events(0): no HIP event bracket around the SE(3) NN search outside
+    // profiled batches (each marker leaves the GPU idle a few us;
+    // time_se3_correspondence_search_ms is then 0)
     bool nn_events_ = true;
     se3icp_trace* trace_ = nullptr;      // armed per-iteration record of one pair (se3icp_set_trace)
     int record_trace(se3icp_trace* tr, int it, int& phase_of_it, hipStream_t s);
@@ -159,9 +156,6 @@ class Engine {
     // loop iterations in flight: kernel-time events and launched NN phases per ring slot
     static constexpr int kLoopRing = 4, kLoopEv = 7;
     hipEvent_t loop_ev_[kLoopRing * kLoopEv];
-    // side-stream fork / SE(3) join / R3 join per ring slot (no timing; a timed SE(3) launch
-    // pair forks on its loop_ev_ bracket start instead)
-    hipEvent_t fork_ev_[kLoopRing] = {}, join_ev_[kLoopRing] = {}, join3_ev_[kLoopRing] = {};
     int loop_flags_[kLoopRing] = {};
     bool loop_detail_[kLoopRing] = {};
 };

@@ -374,153 +374,175 @@ __device__ __forceinline__ T wsum(T x) {
     return x;
 }
 
-__global__ __launch_bounds__(256) void k_reduce(View v) {
-    __shared__ double red[4][kRedVals];
+// One correspondence's terms (ISR.cpp:689-703, 57-110; MSE ISR.cpp:379-400) added to acc:
+// vs the moved source point, vt the target point, ns0 / nt the source (initial frame) and
+// target normals, w2 the cf weight squared (1 otherwise), dist the stored distance.
+__device__ __forceinline__ void corr_terms(int est, bool cf, const double* T, const double* vs, const double* vt,
+                                           const double* ns0, const double* nt, double w2, double dist, double* acc) {
+    if (est == EST_PT2PT) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) { acc[a] += vs[a]; acc[3 + a] += vt[a]; }
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int b = 0; b < 3; ++b) acc[6 + a * 3 + b] += vt[a] * vs[b];
+        acc[15] += 1.0;
+        acc[27] += dist;
+        return;
+    }
+    if (est == EST_PT2PL) {
+        const double r = (vs[0] - vt[0]) * nt[0] + (vs[1] - vt[1]) * nt[1] + (vs[2] - vt[2]) * nt[2];
+        const double J[6] = {vs[1] * nt[2] - vs[2] * nt[1], vs[2] * nt[0] - vs[0] * nt[2], vs[0] * nt[1] - vs[1] * nt[0],
+                             nt[0], nt[1], nt[2]};
+        int k = 0;
+#pragma unroll
+        for (int a = 0; a < 6; ++a)
+#pragma unroll
+            for (int b = a; b < 6; ++b) acc[k++] += J[a] * J[b];
+#pragma unroll
+        for (int a = 0; a < 6; ++a) acc[21 + a] += J[a] * r;
+        acc[27] += dist;
+        return;
+    }
+    // GICP: Cs = R Cs0 R^T (PointCloud::Transform on covariances, ISR.cpp:706); both
+    // covariances from the stored normals (ISR.cpp:33-52: 3 loads instead of 6)
+    double C0[3][3];
+    {
+        double c6[6];
+        gicp_cov_from_normal(d3{ns0[0], ns0[1], ns0[2]}, 1e-3, c6);
+        C0[0][0] = c6[0]; C0[0][1] = C0[1][0] = c6[1]; C0[0][2] = C0[2][0] = c6[2];
+        C0[1][1] = c6[3]; C0[1][2] = C0[2][1] = c6[4]; C0[2][2] = c6[5];
+    }
+    double RC[3][3], M[3][3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) RC[a][b] = T[a * 4] * C0[0][b] + T[a * 4 + 1] * C0[1][b] + T[a * 4 + 2] * C0[2][b];
+    {
+        double Ct[6];
+        gicp_cov_from_normal(d3{nt[0], nt[1], nt[2]}, 1e-3, Ct);
+        const int map[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+#pragma unroll
+            for (int b = 0; b < 3; ++b)
+                M[a][b] = Ct[map[a][b]] + (RC[a][0] * T[b * 4] + RC[a][1] * T[b * 4 + 1] + RC[a][2] * T[b * 4 + 2]);
+    }
+    // M^-1 by cofactors (M is SPD)
+    double Mi[3][3];
+    Mi[0][0] = M[1][1] * M[2][2] - M[1][2] * M[2][1];
+    Mi[0][1] = M[0][2] * M[2][1] - M[0][1] * M[2][2];
+    Mi[0][2] = M[0][1] * M[1][2] - M[0][2] * M[1][1];
+    Mi[1][0] = M[1][2] * M[2][0] - M[1][0] * M[2][2];
+    Mi[1][1] = M[0][0] * M[2][2] - M[0][2] * M[2][0];
+    Mi[1][2] = M[0][2] * M[1][0] - M[0][0] * M[1][2];
+    Mi[2][0] = M[1][0] * M[2][1] - M[1][1] * M[2][0];
+    Mi[2][1] = M[0][1] * M[2][0] - M[0][0] * M[2][1];
+    Mi[2][2] = M[0][0] * M[1][1] - M[0][1] * M[1][0];
+    const double det = M[0][0] * Mi[0][0] + M[0][1] * Mi[1][0] + M[0][2] * Mi[2][0];
+    // J^T J = G^T M^-1 G and J^T r = G^T M^-1 d for every W with W^T W = M^-1 (the
+    // reference's W = M^-1/2, ISR.cpp:78, is one of them), so the sums are formed from
+    // A = w^2 M^-1 and G = [S | I], S = -[vs]x, without a matrix root or factor:
+    // J^T J = [[S^T A S, S^T A], [A S, A]], J^T r = [S^T A d; A d].
+    const double sc = w2 / det;
+    double A[3][3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) A[a][b] = 0.5 * (Mi[a][b] + Mi[b][a]) * sc;
+    const double S[3][3] = {{0, vs[2], -vs[1]}, {-vs[2], 0, vs[0]}, {vs[1], -vs[0], 0}};
+    const double d[3] = {vs[0] - vt[0], vs[1] - vt[1], vs[2] - vt[2]};
+    double B[3][3];  // A S
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) B[a][b] = A[a][0] * S[0][b] + A[a][1] * S[1][b] + A[a][2] * S[2][b];
+    double H[6][6];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+#pragma unroll
+        for (int b = a; b < 3; ++b) H[a][b] = S[0][a] * B[0][b] + S[1][a] * B[1][b] + S[2][a] * B[2][b];
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            H[a][3 + b] = B[b][a];  // (S^T A)[a][b] = (A S)[b][a]
+            H[3 + a][3 + b] = A[a][b];
+        }
+    }
+    double Ad[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) Ad[a] = A[a][0] * d[0] + A[a][1] * d[1] + A[a][2] * d[2];
+    int k = 0;
+#pragma unroll
+    for (int a = 0; a < 6; ++a)
+#pragma unroll
+        for (int b = a; b < 6; ++b) acc[k++] += H[a][b];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        acc[21 + a] += S[0][a] * Ad[0] + S[1][a] * Ad[1] + S[2][a] * Ad[2];
+        acc[24 + a] += Ad[a];
+    }
+    // estimate_current_mse_compute_euclidean for cf (ISR.cpp:390-400), the stored distance else
+    acc[27] += cf ? sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]) : dist;
+}
+
+// Block b sums the terms of its pair's queries q0 + threadIdx.x + kRedThreads u (u < kRedPer,
+// below q1).  Every input of the thread's kRedPer correspondences is loaded before the
+// first is used: a wave's latency is a few dependent round trips (work record -> index and
+// distance -> target gathers), so the loads of several correspondences share them.
+__global__ __launch_bounds__(kRedThreads) void k_reduce(View v) {
+    constexpr int NW = kRedThreads / 64;
+    __shared__ double red[NW][kRedVals];
     const BlockWork w = v.work[blockIdx.x];
     const PairDev* P = v.pairs + w.pair;
     double acc[kRedVals];
 #pragma unroll
     for (int i = 0; i < kRedVals; ++i) acc[i] = 0.0;
     if (P->phase == PHASE_IDLE) return;
-    const CloudDev cs = v.clouds[P->src], ct = v.clouds[P->tgt];
-    const int qi = w.q0 + threadIdx.x;
-    bool kept = qi < cs.n;
-    if (kept && P->trim) {
-        kept = P->nkeep > 0 && trim_key_of(v.corr_dist, cs.off, qi) <= v.trim_key[w.pair];
+    const int est = P->est;
+    const bool cf = P->cf != 0;
+    // trimmed pairs keep the keys (float dist bits << 32 | query) up to the cut (none when nkeep = 0)
+    const unsigned long long cut = P->trim ? (P->nkeep > 0 ? v.trim_key[w.pair] : 0ull) : ~0ull;
+    const bool none = (int)(P->trim != 0) & (int)(P->nkeep <= 0);
+    const size_t ld = v.ld;
+    int g[kRedPer], gt[kRedPer];
+    float dd[kRedPer];
+    bool kept[kRedPer];
+#pragma unroll
+    for (int u = 0; u < kRedPer; ++u) {
+        const int qi = w.q0 + (int)threadIdx.x + kRedThreads * u;
+        kept[u] = qi < w.q1;
+        g[u] = w.s_off + (kept[u] ? qi : w.q0);
+        dd[u] = v.corr_dist[g[u]];
+        gt[u] = w.t_off + v.corr_idx[g[u]];
+        const unsigned long long key = ((unsigned long long)__float_as_uint(dd[u]) << 32) | (unsigned)qi;
+        kept[u] = (bool)((int)kept[u] & (int)!none & (int)(key <= cut));
     }
-    if (kept) {
+    double xs[kRedPer][3], xt[kRedPer][3], n0[kRedPer][3], nt[kRedPer][3], w2[kRedPer];
+#pragma unroll
+    for (int u = 0; u < kRedPer; ++u) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            xs[u][a] = v.xyz64[a * ld + g[u]];
+            xt[u][a] = v.xyz64[a * ld + gt[u]];
+            n0[u][a] = est == EST_GICP ? v.nrm64[a * ld + g[u]] : 0.0;
+            nt[u][a] = est != EST_PT2PT ? v.nrm64[a * ld + gt[u]] : 0.0;
+        }
+        if (cf) {
+            const double wc = (v.conf64[g[u]] + v.conf64[gt[u]]) / 2.0;  // ISR.cpp:913
+            w2[u] = wc * wc;
+        } else {
+            w2[u] = 1.0;
+        }
+    }
+    {
         double T[12];
         load_T(P, T);
-        const int g = cs.off + qi;
-        const int j = v.corr_idx[g];
-        const int gt = ct.off + j;
-        double vs[3];
-        pose_point(T, v.xyz64[g], v.xyz64[v.ld + g], v.xyz64[2 * (size_t)v.ld + g], vs);
-        const double vt[3] = {v.xyz64[gt], v.xyz64[v.ld + gt], v.xyz64[2 * (size_t)v.ld + gt]};
-        const double dist = (double)v.corr_dist[g];
-        const int est = P->est;
-        if (est == EST_PT2PT) {
 #pragma unroll
-            for (int a = 0; a < 3; ++a) { acc[a] = vs[a]; acc[3 + a] = vt[a]; }
-#pragma unroll
-            for (int a = 0; a < 3; ++a)
-#pragma unroll
-                for (int b = 0; b < 3; ++b) acc[6 + a * 3 + b] = vt[a] * vs[b];
-            acc[15] = 1.0;
-            acc[27] = dist;
-        } else {
-            double J[3][6], r[3];
-            int nrows;
-            double wgt = 1.0;
-            if (est == EST_PT2PL) {
-                const double n[3] = {v.nrm64[gt], v.nrm64[v.ld + gt], v.nrm64[2 * (size_t)v.ld + gt]};
-                r[0] = (vs[0] - vt[0]) * n[0] + (vs[1] - vt[1]) * n[1] + (vs[2] - vt[2]) * n[2];
-                J[0][0] = vs[1] * n[2] - vs[2] * n[1];
-                J[0][1] = vs[2] * n[0] - vs[0] * n[2];
-                J[0][2] = vs[0] * n[1] - vs[1] * n[0];
-                J[0][3] = n[0]; J[0][4] = n[1]; J[0][5] = n[2];
-                nrows = 1;
-            } else {
-                // Cs = R Cs0 R^T (PointCloud::Transform on covariances, ISR.cpp:706)
-                // (both covariances from the stored normals, ISR.cpp:33-52: 3 loads instead of 6)
-                double C0[3][3];
-                {
-                    double c6[6];
-                    gicp_cov_from_normal(d3{v.nrm64[g], v.nrm64[v.ld + g], v.nrm64[2 * (size_t)v.ld + g]}, 1e-3, c6);
-                    C0[0][0] = c6[0]; C0[0][1] = C0[1][0] = c6[1]; C0[0][2] = C0[2][0] = c6[2];
-                    C0[1][1] = c6[3]; C0[1][2] = C0[2][1] = c6[4]; C0[2][2] = c6[5];
-                }
-                double RC[3][3], M[3][3];
-#pragma unroll
-                for (int a = 0; a < 3; ++a)
-#pragma unroll
-                    for (int b = 0; b < 3; ++b) RC[a][b] = T[a * 4] * C0[0][b] + T[a * 4 + 1] * C0[1][b] + T[a * 4 + 2] * C0[2][b];
-                {
-                    double Ct[6];
-                    gicp_cov_from_normal(d3{v.nrm64[gt], v.nrm64[v.ld + gt], v.nrm64[2 * (size_t)v.ld + gt]}, 1e-3, Ct);
-                    const int map[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
-#pragma unroll
-                    for (int a = 0; a < 3; ++a)
-#pragma unroll
-                        for (int b = 0; b < 3; ++b)
-                            M[a][b] = Ct[map[a][b]] + (RC[a][0] * T[b * 4] + RC[a][1] * T[b * 4 + 1] + RC[a][2] * T[b * 4 + 2]);
-                }
-                // M^-1 by cofactors (M is SPD)
-                double Mi[3][3];
-                Mi[0][0] = M[1][1] * M[2][2] - M[1][2] * M[2][1];
-                Mi[0][1] = M[0][2] * M[2][1] - M[0][1] * M[2][2];
-                Mi[0][2] = M[0][1] * M[1][2] - M[0][2] * M[1][1];
-                Mi[1][0] = M[1][2] * M[2][0] - M[1][0] * M[2][2];
-                Mi[1][1] = M[0][0] * M[2][2] - M[0][2] * M[2][0];
-                Mi[1][2] = M[0][2] * M[1][0] - M[0][0] * M[1][2];
-                Mi[2][0] = M[1][0] * M[2][1] - M[1][1] * M[2][0];
-                Mi[2][1] = M[0][1] * M[2][0] - M[0][0] * M[2][1];
-                Mi[2][2] = M[0][0] * M[1][1] - M[0][1] * M[1][0];
-                const double det = M[0][0] * Mi[0][0] + M[0][1] * Mi[1][0] + M[0][2] * Mi[2][0];
-                if (P->cf) {
-                    const double wc = (v.conf64[g] + v.conf64[gt]) / 2.0;  // ISR.cpp:913
-                    wgt = wc * wc;
-                }
-                // J^T J = G^T M^-1 G and J^T r = G^T M^-1 d for every W with W^T W = M^-1
-                // (the reference's W = M^-1/2, ISR.cpp:78, is one of them), so the sums are
-                // formed from A = w^2 M^-1 and G = [S | I], S = -[vs]x, without a matrix root
-                // or factor: J^T J = [[S^T A S, S^T A], [A S, A]], J^T r = [S^T A d; A d].
-                const double sc = wgt / det;
-                double A[3][3];
-#pragma unroll
-                for (int a = 0; a < 3; ++a)
-#pragma unroll
-                    for (int b = 0; b < 3; ++b) A[a][b] = 0.5 * (Mi[a][b] + Mi[b][a]) * sc;
-                const double S[3][3] = {{0, vs[2], -vs[1]}, {-vs[2], 0, vs[0]}, {vs[1], -vs[0], 0}};
-                const double d[3] = {vs[0] - vt[0], vs[1] - vt[1], vs[2] - vt[2]};
-                double B[3][3];  // A S
-#pragma unroll
-                for (int a = 0; a < 3; ++a)
-#pragma unroll
-                    for (int b = 0; b < 3; ++b) B[a][b] = A[a][0] * S[0][b] + A[a][1] * S[1][b] + A[a][2] * S[2][b];
-                double H[6][6];
-#pragma unroll
-                for (int a = 0; a < 3; ++a) {
-#pragma unroll
-                    for (int b = a; b < 3; ++b) H[a][b] = S[0][a] * B[0][b] + S[1][a] * B[1][b] + S[2][a] * B[2][b];
-#pragma unroll
-                    for (int b = 0; b < 3; ++b) {
-                        H[a][3 + b] = B[b][a];     // (S^T A)[a][b] = (A S)[b][a]
-                        H[3 + a][3 + b] = A[a][b];
-                    }
-                }
-                double Ad[3];
-#pragma unroll
-                for (int a = 0; a < 3; ++a) Ad[a] = A[a][0] * d[0] + A[a][1] * d[1] + A[a][2] * d[2];
-                int k = 0;
-#pragma unroll
-                for (int a = 0; a < 6; ++a)
-#pragma unroll
-                    for (int b = a; b < 6; ++b) acc[k++] += H[a][b];
-#pragma unroll
-                for (int a = 0; a < 3; ++a) {
-                    acc[21 + a] += S[0][a] * Ad[0] + S[1][a] * Ad[1] + S[2][a] * Ad[2];
-                    acc[24 + a] += Ad[a];
-                }
-                nrows = 0;
-            }
-#pragma unroll
-            for (int rr = 0; rr < 3; ++rr) {
-                if (rr >= nrows) break;
-                int k = 0;
-#pragma unroll
-                for (int a = 0; a < 6; ++a)
-#pragma unroll
-                    for (int b = a; b < 6; ++b) acc[k++] += wgt * J[rr][a] * J[rr][b];
-#pragma unroll
-                for (int a = 0; a < 6; ++a) acc[21 + a] += wgt * J[rr][a] * r[rr];
-            }
-            if (P->cf) {  // estimate_current_mse_compute_euclidean, ISR.cpp:390-400
-                acc[27] = sqrt(((vs[0] - vt[0]) * (vs[0] - vt[0]) + (vs[1] - vt[1]) * (vs[1] - vt[1])) +
-                               (vs[2] - vt[2]) * (vs[2] - vt[2]));
-            } else {
-                acc[27] = dist;
-            }
+        for (int u = 0; u < kRedPer; ++u) {
+            if (!kept[u]) continue;
+            double vs[3];
+            pose_point(T, xs[u][0], xs[u][1], xs[u][2], vs);
+            corr_terms(est, cf, T, vs, xt[u], n0[u], nt[u], w2[u], (double)dd[u], acc);
         }
     }
     const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -534,7 +556,14 @@ __global__ __launch_bounds__(256) void k_reduce(View v) {
     __syncthreads();
     if (threadIdx.x < kRedVals) {
         const int i = threadIdx.x;
-        v.red_partial[(size_t)blockIdx.x * kRedVals + i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+        double s4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            s4[k] = red[k][i];
+#pragma unroll
+            for (int w2 = k + 4; w2 < NW; w2 += 4) s4[k] += red[w2][i];
+        }
+        v.red_partial[(size_t)blockIdx.x * kRedVals + i] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
     }
 }
 
@@ -557,7 +586,7 @@ __global__ __launch_bounds__(kFinThreads) void k_reduce_final(View v, const int3
     if ((int)(p == 0) & (int)(threadIdx.x < 3)) v.flag_count[threadIdx.x] = 0;  // single-query lists
     PairDev* P = v.pairs + p;
     if (P->phase == PHASE_IDLE) {
-        if (threadIdx.x == 0) next_phase[p] = PHASE_IDLE;
+        if ((int)(threadIdx.x == 0) & (int)(next_phase != nullptr)) next_phase[p] = PHASE_IDLE;
         return;
     }
     __shared__ double part[kFinChunks][kRedVals];
@@ -601,7 +630,7 @@ __global__ __launch_bounds__(kFinThreads) void k_reduce_final(View v, const int3
             double* h = hist + ((size_t)(S.iter % kHist) * v.npairs + p) * 12;
             for (int k = 0; k < 12; ++k) h[k] = P->T[k];
         }
-        next_phase[p] = P->phase;
+        if (next_phase) next_phase[p] = P->phase;
     }
 }
 
@@ -613,7 +642,7 @@ void launch_trim(const View& v, hipStream_t s) {
 }
 void launch_reduce(const View& v, const int32_t* pair_wb, const int32_t* pair_wn, PairState* state, double* hist,
                    int32_t* next_phase, hipStream_t s) {
-    hipLaunchKernelGGL(k_reduce, dim3(v.nwork), dim3(256), 0, s, v);
+    hipLaunchKernelGGL(k_reduce, dim3(v.nwork), dim3(kRedThreads), 0, s, v);
     hipLaunchKernelGGL(k_reduce_final, dim3(v.npairs), dim3(kFinThreads), 0, s, v, pair_wb, pair_wn, state, hist, next_phase);
 }
 

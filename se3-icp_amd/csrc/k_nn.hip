@@ -14,7 +14,7 @@
 // (sqrt(d1) + 2m)^2 and the second-best distance d2, m = the query's displacement in
 // this iteration (so the extra work is at most that of an exact 2-NN search).
 //
-// Search (k_nn_group).  The queries k_nn_prep could not settle are compacted per chunk
+// Search (k_nn_search, group part).  The queries k_nn_prep could not settle are compacted per chunk
 // (<= 1024 consecutive source tree positions, i.e. close together in the search space;
 // the pose acts on the vectors as an isometry, so they stay close as the source moves)
 // and swept 64 per wavefront.  The wave walks the TARGET kd-tree depth first; a node is
@@ -42,7 +42,7 @@ using namespace loopdev;
 
 // Tuned constants (A/B on the bench's C4 batch; the rejected alternatives are listed in
 // DESIGN.md's measurement log):
-//   k_nn_group blocks are ONE wave: a block's LDS is released when its last wave ends, so
+//   k_nn_search blocks are ONE wave: a block's LDS is released when its last wave ends, so
 //   4-wave blocks whose waves ended at different times stranded LDS (a CU held at most five
 //   28.7 KB blocks): SE(3) NN -9 %.
 constexpr int kTPL = 4;        // targets per lane in the compacted leaf sweeps (kept in registers across queries)
@@ -184,17 +184,19 @@ __device__ __forceinline__ void compact_sweep(const float4* tile, const float4* 
     }
 }
 
-// chunks with at least kDense searched queries use k_nn_group, sparser ones k_nn_single
+// chunks with at least kDense searched queries are searched 64 per wave, sparser ones one query per wave (k_nn_search)
 // (measured: a 12-D wave-per-query search costs ~5x the lanes' share of a group's, a 3-D
 // one far more, but a group's latency bounds an iteration with few groups; A/B 64 / 128 /
 // 256 within 1 % of each other with one-wave group blocks)
 constexpr int kDense = 256;
-constexpr int kWpe = 4;        // waves per SIMD of k_nn_group (its natural 128 VGPRs; 5 measured +8 %)
+constexpr int kWpe = 4;        // waves per SIMD of k_nn_search (its natural 128 VGPRs; 5 measured +8 %)
 constexpr int kXcdRun = 256;   // group blocks per XCD run (16 chunks; runs dealt round-robin over the XCDs:
                                // neighbouring chunks share target leaves in one L2, SE(3) NN -3 %)
 constexpr int kSmall = 4;      // groups of at most this many queries are searched one query at a time
-constexpr int kSingleBlocks = 4096;  // grid of the one-query-per-wave kernels (4 waves per block, grid-strided)
-static_assert(kSingleBlocks % 8 == 0, "k_nn_single deals the list to the 8 XCDs in whole eighths of its grid");
+// one-query-per-wave blocks at the front of the search grid (grid-strided; 4,096 measured
+// faster than 16,384 at C4: fewer empty waves to dispatch in iterations without sparse chunks)
+constexpr int kSingleWaves = 4096;
+static_assert(kSingleWaves % 8 == 0, "single_list deals the list to the 8 XCDs in whole eighths of its waves");
 constexpr double kExpand = 1.0;      // search widening, in units of the query's displacement this iteration
 
 template <int D>
@@ -270,8 +272,9 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
     pose_point(T, mt[0], mt[1], mt[2], Qt);
     const double rot2 = 3.0 * a2 * (1.0 + 1e-12);  // |rotation columns|^2 (12-D), 0 (3-D)
     const int it = P->iter;
-    const float4 cr = v.cert[g];
-    const int ci = __float_as_int(cr.z);
+    NNCert* cp = v.cert + gx;  // (the phase's tree slot: coalesced)
+    const float4 c0 = reinterpret_cast<const float4*>(cp)[0];
+    const int ci = __float_as_int(c0.z);
     const double qn = sqrt(rot2 + Qt[0] * Qt[0] + Qt[1] * Qt[1] + Qt[2] * Qt[2]);
     if ((int)(ci >= P->phase_start) & (int)(ci < it) & (int)(it - ci < kHist)) {
         double Tr[12], Qr[3];
@@ -282,14 +285,13 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
         // |q_now - q_then|, padded for the frame's orthonormality and the rounding of the
         // two f64 queries the searches used
         const double dl = sqrt(a2 * rot_frob2(T, Tr) * (1.0 + 1e-12) + dt * dt) * (1.0 + 1e-12) + 2e-15 * (qn + qr);
-        const double a = (double)cr.y - dl, b = (double)cr.x + dl;
+        const double a = (double)c0.y - dl, b = (double)c0.x + dl;
         // margin for the f64 rounding of the reference's own squared distances (|q| + |target| <= M)
         const double M = 2.0 * qn + b;
         if ((int)(a > b) & (int)((a - b) * (a + b) > 1e-14 * M * M)) {
-            const int j = v.corr_idx[g];
-            double Q12[12];
-            Q12[D - 3] = Qt[0]; Q12[D - 2] = Qt[1]; Q12[D - 1] = Qt[2];
-            v.corr_dist[g] = stored_dist(v, D == 12 ? PHASE_SE3 : PHASE_R3, ct, Q12, j);
+            // settled: corr_idx[g] (= the record's j) stays; the distance to its anchor
+            const double t[3] = {cp->t[0], cp->t[1], cp->t[2]};
+            v.corr_dist[g] = anchor_dist(Qt, t);
             return true;
         }
     }
@@ -301,7 +303,7 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
         const double dt = dist3_f64(Qt, Qp);
         m = (float)(kExpand * sqrt(a2 * rot_frob2(T, Tp) + dt * dt));
     }
-    v.cert[g].w = m;
+    cp->margin = m;
     // No previous match (a pair's first search): seed one from a greedy descent of the
     // target tree (the child whose f32 box bound is smaller, down to a leaf; a target of
     // that leaf).  The search only uses it for its first pruning threshold, so any target
@@ -347,7 +349,7 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
 
 // One 1024-thread block per chunk (a node of level CL = GL - 4 of the source tree: 16
 // query leaves of level GL).  Settles what the certificates allow and packs the rest
-// for k_nn_group: consecutive leaves' remaining queries share a 64-lane group as long as
+// for k_nn_search: consecutive leaves' remaining queries share a 64-lane group as long as
 // they fit, a leaf is never split (with every query searched, a group is one leaf).
 // qlist[c][j][lane] = local tree position, qcount[c][j] = lanes of group j.
 #ifdef SE3ICP_PROF
@@ -361,13 +363,19 @@ __device__ unsigned long long g_wave_hist[2][41];
 __device__ unsigned long long g_wave_span[2] = {~0ull, 0ull};
 #endif
 // (8 waves per SIMD: two 1024-thread blocks per CU, <= 64 VGPRs)
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_nn_prep(View v) {
+// publish (may be null): the host's ring slot of the previous iteration, which receives
+// every pair's phase in this one (its k_reduce_final opened it).  Written first thing by
+// block 0, so the host-memory write completes inside this launch instead of delaying the
+// end of k_reduce_final (a fine-grained host write held the next launch back ~6 us).
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void k_nn_prep(View v, int32_t* publish) {
 #ifdef SE3ICP_PROF
     const unsigned long long tp0 = __builtin_amdgcn_s_memrealtime();
 #endif
+    if ((int)(blockIdx.x == 0) & (int)(publish != nullptr))
+        for (int p = threadIdx.x; p < v.npairs; p += blockDim.x) publish[p] = v.pairs[p].phase;
     constexpr int NL = kChunkQ / 64;  // leaves (groups) per chunk
     __shared__ int s_cnt[NL], s_slot[NL], s_base[NL], s_wc[NL], s_single;
-    const int c = xcd_block_runs(blockIdx.x, gridDim.x, kXcdRun / 16);  // (k_nn_group's chunk runs)
+    const int c = xcd_block_runs(blockIdx.x, gridDim.x, kXcdRun / 16);  // (k_nn_search's chunk runs)
     const int pair = c >> v.chunk_level;
     const PairDev* P = v.pairs + pair;
     const int phase = P->phase;
@@ -472,27 +480,34 @@ __device__ __forceinline__ void nn_finish(const View& v, const PairDev* P, int p
                                           float thr, float na, float nb) {
     const bool rc = (bool)((int)flag & (int)(ct.n > 1));
     if (rc) atomicAdd(&v.pair_rechecked[pair], 1);
-    // certificate for the next iterations (k_nn_prep): exact match distance <= sqrt(d1 + err),
-    // every other target >= min(d2 - err(d2), thr): visited ones by the top-2, unvisited
-    // ones because every box skipped had a bound >= thr at the time (thr only decreases)
-    // (one 16-B store; the margin slot w is dead once the search has read it)
-    if ((int)flag | (int)(i1 < 0)) {
-        v.cert[g] = make_float4(0.f, 0.f, __int_as_float(-1), 0.f);
-    } else {
-        const float l2 = fminf(d2 - f32_err(d2, na, nb, D), thr * (1.f - 4e-6f));
-        v.cert[g] = make_float4(sqrtf(d1 + f32_err(d1, na, nb, D)) * (1.f + 1e-6f),
-                                sqrtf(fmaxf(l2, 0.f)) * (1.f - 1e-6f), __int_as_float(P->iter), 0.f);
-    }
+    // certificate for the next iterations (k_nn_prep), at the source tree slot gx: exact
+    // match distance <= sqrt(d1 + err), every other target >= min(d2 - err(d2), thr):
+    // visited ones by the top-2, unvisited ones because every box skipped had a bound >= thr
+    // at the time (thr only decreases); the match and its anchor (the margin slot is dead
+    // once the search has read it)
+    float4* cw = reinterpret_cast<float4*>(v.cert + gx);
+    const bool nocert = (bool)((int)flag | (int)(i1 < 0));
+    if (nocert) cw[0] = make_float4(0.f, 0.f, __int_as_float(-1), __int_as_float(0));
     if (rc) return;
     // tree position -> target index; a NaN query keeps the reference's zero-initialised index
-    i1 = (i1 < 0) ? 0 : TR.perm[ct.off + i1];
-    v.corr_idx[g] = i1;
+    const int j = (i1 < 0) ? 0 : TR.perm[ct.off + i1];
+    v.corr_idx[g] = j;
     // the stored distance needs the translation part of the query only (ISR.cpp:465-468)
-    double Tm[12], Q12[12];
+    double Tm[12], Qt[3], t[3];
     load_T(P, Tm);
     const double* m = TR.tvec64 + gx;  // (3 rows: points / translations)
-    pose_point(Tm, m[0], m[v.ld], m[2 * (size_t)v.ld], Q12 + D - 3);
-    v.corr_dist[g] = stored_dist(v, D == 12 ? PHASE_SE3 : PHASE_R3, ct, Q12, i1);
+    pose_point(Tm, m[0], m[v.ld], m[2 * (size_t)v.ld], Qt);
+    match_anchor(v, D == 12 ? PHASE_SE3 : PHASE_R3, ct, j, t);
+    v.corr_dist[g] = anchor_dist(Qt, t);
+    if (!nocert) {
+        const float l2 = fminf(d2 - f32_err(d2, na, nb, D), thr * (1.f - 4e-6f));
+        cw[0] = make_float4(sqrtf(d1 + f32_err(d1, na, nb, D)) * (1.f + 1e-6f), sqrtf(fmaxf(l2, 0.f)) * (1.f - 1e-6f),
+                            __int_as_float(P->iter), __int_as_float(j));
+        double* tw = reinterpret_cast<double*>(cw + 1);
+        tw[0] = t[0];
+        tw[1] = t[1];
+        tw[2] = t[2];
+    }
 }
 
 template <int D>
@@ -501,7 +516,19 @@ __device__ __forceinline__ void single_one(const View& v, const PairDev* P, int 
                                            unsigned* n_box);
 
 template <int D>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kWpe))) void k_nn_group(View v) {
+__device__ __forceinline__ void single_list(const View& v, int bw);
+
+// One launch per phase and iteration: blocks [0, kSingleWaves) are one-query-per-wave
+// searches of the phase's single-query list (single_list, dispatched first: they are the
+// launch's latency tail), the rest one 64-query group each.  (Round 3 ran the two parts as
+// two grids on two streams, joined by events: two extra launches and two cross-stream
+// waits per iteration.)
+template <int D>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kWpe))) void k_nn_search(View v) {
+    if (blockIdx.x < (unsigned)kSingleWaves) {
+        single_list<D>(v, (int)blockIdx.x);
+        return;
+    }
     constexpr int NV = (D + 3) / 4;
     __shared__ float4 s_tile[kLeafMax * NV];
     // compacted leaf sweeps (12-D): the wave's query vectors, the list of lanes that want
@@ -514,7 +541,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kWpe))) void
     // wave-uniform work item: group gi & 15 (64 listed queries) of chunk c; the pair record,
     // node boxes and leaf ranges become scalar loads (blocks of one XCD take runs of
     // consecutive chunks: a pair's target tree stays in that XCD's L2)
-    const int gq = __builtin_amdgcn_readfirstlane(xcd_block_runs(blockIdx.x, gridDim.x, kXcdRun));
+    // (kSingleWaves is a multiple of 8: block b and b - kSingleWaves share an XCD)
+    const int gq = __builtin_amdgcn_readfirstlane(
+        xcd_block_runs((int)blockIdx.x - kSingleWaves, (int)gridDim.x - kSingleWaves, kXcdRun));
     if ((gq >> 4) >= v.nchunks) return;
     const int c = gq >> 4;
     const int gi = gq;
@@ -528,7 +557,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kWpe))) void
     const TreeRef TR = (D == 12) ? v.t12 : v.t3;
     if (cnt_q <= kSmall) {
         // a group of a few queries (a chunk's leftovers): each searched by all 64 lanes in
-        // turn (k_nn_single's lane-parallel search) -- a lone query with a wide ball would
+        // turn (single_one's lane-parallel search) -- a lone query with a wide ball would
         // otherwise walk the tree one node per step and set the launch's time
         unsigned n_eval = 0, n_box = 0;
         for (int q = 0; q < cnt_q; ++q) {
@@ -546,7 +575,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kWpe))) void
     const bool valid = lane < cnt_q;
     const int gx = cs.off + v.qlist[(size_t)gi * 64 + (valid ? lane : 0)];  // source tree slot
     const int g = cs.off + TR.perm[gx];
-    const float mrg = valid ? v.cert[g].w : 0.f;
+    const float mrg = valid ? v.cert[gx].margin : 0.f;
 
     // query: f64 pose applied to the source element, rounded to f32
     float q[D];
@@ -798,7 +827,7 @@ __device__ __forceinline__ void single_one(const View& v, const PairDev* P, int 
     f32x2 q2[(D + 1) / 2];
 #pragma unroll
     for (int r = 0; r < D / 2; ++r) q2[r] = f32x2{q[2 * r], q[2 * r + 1]};
-    const float mrg = v.cert[g].w;
+    const float mrg = v.cert[gx].margin;
     auto widen = [&](float a1, float a2) __attribute__((always_inline)) {
         const float e = sqrtf(a1) + 2.f * mrg;
         const float t = fmaxf(a1, fminf(e * e, a2));
@@ -897,17 +926,20 @@ __device__ __forceinline__ void single_one(const View& v, const PairDev* P, int 
 // R3 entries from the back (counters flag_count[1], [2]).  The list holds each sparse
 // chunk's queries together (nearby points: they read the same target leaves), so every XCD
 // takes one contiguous eighth of it (blocks are dealt to the XCDs round-robin): neighbouring
-// queries' leaf reads meet in one L2 instead of being fetched by all eight.
+// queries' leaf reads meet in one L2 instead of being fetched by all eight.  bw: the wave's
+// block, < kSingleWaves.
 template <int D>
-__global__ __launch_bounds__(256) void k_nn_single(View v) {
+__device__ __forceinline__ void single_list(const View& v, int bw) {
     const int lane = threadIdx.x & 63;
     const int nq = __builtin_amdgcn_readfirstlane(v.flag_count[D == 12 ? 1 : 2]);
-    const int xcd = blockIdx.x & 7, nbx = gridDim.x >> 3;  // (gridDim.x: a multiple of 8)
+    if (nq <= 0) return;
+    constexpr int nbx = kSingleWaves >> 3;  // waves per XCD
+    const int xcd = bw & 7;
     const int seg = (nq + 7) >> 3;
     const int f_end = min(nq, (xcd + 1) * seg);
-    const int w0 = __builtin_amdgcn_readfirstlane(xcd * seg + (int)(blockIdx.x >> 3) * 4 + (int)(threadIdx.x >> 6));
+    const int w0 = __builtin_amdgcn_readfirstlane(xcd * seg + (bw >> 3));
     unsigned n_eval = 0, n_box = 0;
-    for (int f = w0; f < f_end; f += nbx * 4) {
+    for (int f = w0; f < f_end; f += nbx) {
         const int gx = __builtin_amdgcn_readfirstlane(D == 12 ? v.sq_list[f] : v.sq_list[v.ld - 1 - f]);
         const int pair = v.cloud_of[gx] >> 1;
         const PairDev* P = v.pairs + pair;
@@ -964,27 +996,14 @@ double nn_prep_span() {
     return h[1] > h[0] ? (h[1] - h[0]) / 100.0 : 0.0;
 }
 #endif
-void launch_nn_prep(const View& v, hipStream_t s) {
-    hipLaunchKernelGGL(k_nn_prep, dim3(v.nchunks), dim3(kChunkQ), 0, s, v);
+void launch_nn_prep(const View& v, int32_t* publish, hipStream_t s) {
+    hipLaunchKernelGGL(k_nn_prep, dim3(v.nchunks), dim3(kChunkQ), 0, s, v, publish);
 }
-// 16 groups of 64 per chunk, one wave per group
-// and the single-query kernel over a fixed grid (kSingleBlocks x 4 waves)
-void launch_nn_se3(const View& v, hipStream_t s) {
-    hipLaunchKernelGGL(k_nn_group<12>, dim3(v.nchunks * (kChunkQ / 64)), dim3(64), 0,
-                       s, v);
-    hipLaunchKernelGGL(k_nn_single<12>, dim3(kSingleBlocks), dim3(256), 0, s, v);
-}
-void launch_nn_group(const View& v, int D, hipStream_t s) {
-    if (D == 12) hipLaunchKernelGGL(k_nn_group<12>, dim3(v.nchunks * (kChunkQ / 64)), dim3(64), 0, s, v);
-    else hipLaunchKernelGGL(k_nn_group<3>, dim3(v.nchunks * (kChunkQ / 64)), dim3(64), 0, s, v);
-}
-void launch_nn_single(const View& v, int D, hipStream_t s) {
-    if (D == 12) hipLaunchKernelGGL(k_nn_single<12>, dim3(kSingleBlocks), dim3(256), 0, s, v);
-    else hipLaunchKernelGGL(k_nn_single<3>, dim3(kSingleBlocks), dim3(256), 0, s, v);
-}
-void launch_nn_r3(const View& v, hipStream_t s) {
-    hipLaunchKernelGGL(k_nn_group<3>, dim3(v.nchunks * (kChunkQ / 64)), dim3(64), 0, s, v);
-    hipLaunchKernelGGL(k_nn_single<3>, dim3(kSingleBlocks), dim3(256), 0, s, v);
+// kSingleWaves single-query waves, then 16 groups of 64 per chunk, one wave each
+void launch_nn(const View& v, int D, hipStream_t s) {
+    const dim3 grid(kSingleWaves + v.nchunks * (kChunkQ / 64));
+    if (D == 12) hipLaunchKernelGGL(k_nn_search<12>, grid, dim3(64), 0, s, v);
+    else hipLaunchKernelGGL(k_nn_search<3>, grid, dim3(64), 0, s, v);
 }
 
 }  // namespace se3icp

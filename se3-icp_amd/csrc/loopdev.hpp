@@ -90,17 +90,32 @@ __device__ __forceinline__ void target12(const View& v, const CloudDev& ct, bool
 
 // distance stored with the correspondence: the R3 distance between translation parts
 // in the SE(3) phase (ISR.cpp:465-468, beta-weighted target_se3_cloud_ translation even
-// in the cf variant) and the 3-D NN distance in the R3 phase (ISR.cpp:411-413), f64 -> float
-__device__ __forceinline__ float stored_dist(const View& v, int phase, const CloudDev& ct, const double* Q, int j) {
+// in the cf variant) and the 3-D NN distance in the R3 phase (ISR.cpp:411-413), f64 -> float.
+// The match's anchor: its translation row (SE(3) phase) or its point (R3 phase).
+__device__ __forceinline__ void match_anchor(const View& v, int phase, const CloudDev& ct, int j, double* t) {
     const int gt = ct.off + j;
     if (phase == PHASE_SE3) {
-        const double dx = Q[9] - v.fr64[(size_t)gt * 12 + 9];
-        const double dy = Q[10] - v.fr64[(size_t)gt * 12 + 10];
-        const double dz = Q[11] - v.fr64[(size_t)gt * 12 + 11];
-        return (float)sqrt((dx * dx + dy * dy) + dz * dz);
+        t[0] = v.fr64[(size_t)gt * 12 + 9];
+        t[1] = v.fr64[(size_t)gt * 12 + 10];
+        t[2] = v.fr64[(size_t)gt * 12 + 11];
+    } else {
+        t[0] = v.xyz64[gt];
+        t[1] = v.xyz64[v.ld + gt];
+        t[2] = v.xyz64[2 * (size_t)v.ld + gt];
     }
-    const double b[3] = {v.xyz64[gt], v.xyz64[v.ld + gt], v.xyz64[2 * (size_t)v.ld + gt]};
-    return (float)sqrt(l2_nanoflann3(Q, b));
+}
+// q: the query's translation part (SE(3)) or point (R3); no FMA contraction (the
+// reference's x86 arithmetic)
+__device__ __forceinline__ float anchor_dist(const double* q, const double* t) {
+#pragma clang fp contract(off)
+    const double d0 = q[0] - t[0], d1 = q[1] - t[1], d2 = q[2] - t[2];
+    return (float)sqrt((d0 * d0 + d1 * d1) + d2 * d2);
+}
+// Q: the query vector of the phase (12-D: translation part in Q[9..11]; 3-D: Q[0..2])
+__device__ __forceinline__ float stored_dist(const View& v, int phase, const CloudDev& ct, const double* Q, int j) {
+    double t[3];
+    match_anchor(v, phase, ct, j, t);
+    return anchor_dist(phase == PHASE_SE3 ? Q + 9 : Q, t);
 }
 
 __device__ __forceinline__ bool key_less(double da, int ia, double db, int ib) {

@@ -38,6 +38,21 @@ struct TreeRef {
     const float* hi;
 };
 
+// k_nn.hip certificate record of a query (View::cert), written by its last search:
+//   d1: the match is at most d1 away (exact distance, conservatively rounded), l2: every
+//   other target at least l2, iter: the iteration of that search (-1: none), j: the match
+//   (target index), t: the match's anchor for the stored distance (ISR.cpp:465-468 / 411-413:
+//   the target's translation row in the SE(3) phase, its point in the R3 phase), margin: the
+//   search-radius expansion of a query searched in the current iteration (k_nn_prep)
+struct alignas(16) NNCert {
+    float d1, l2;
+    int32_t iter, j;
+    double t[3];
+    float margin;
+    int32_t _pad;
+};
+static_assert(sizeof(NNCert) == 48, "three 16-B words");
+
 struct View {
     int32_t ld;        // SoA row stride (total points of the batch, padded to 64)
     int32_t npts;      // real points of the batch (per-point kernels stop here)
@@ -75,21 +90,18 @@ struct View {
     TreeRef t3, t12;
     // loop NN work (k_nn.hip): chunk c = node (c mod 2^CL) of level CL of pair (c >> CL)'s
     // source tree (<= kChunkQ positions); k_nn_prep compacts the chunk's queries that its
-    // certificate cannot settle into qlist, k_nn_group sweeps them 64 per wavefront
+    // certificate cannot settle into qlist, k_nn_search sweeps them 64 per wavefront
     int32_t chunk_level;  // CL
     int32_t nchunks;      // npairs << CL
     int32_t* qlist;       // [nchunks * kChunkQ] global slots of the searched queries, tree order
     int32_t* qcount;      // [nchunks][16] lanes of each group (0: none)
-    int32_t* sq_list;     // [ld] queries of sparse chunks (global source tree slots) for k_nn_single:
+    int32_t* sq_list;     // [ld] queries of sparse chunks (global source tree slots), one per wave:
                           // SE(3) phase from the front (count flag_count[1]), R3 from the back ([2])
     const double* hist;   // [kHist][npairs][12] pose T used at iteration k, row k % kHist
-    // NN certificate of each source point from its last search, one 16-B record per point
-    // (k_nn_prep gathers it through the tree permutation: one cache line, not four):
-    //   x = d1: the match is at most d1 away (exact distance, conservatively rounded),
-    //   y = l2: every other target at least l2,
-    //   z = the iteration of that search (int bits; -1: none),
-    //   w = the search-radius expansion of a query searched in this iteration
-    float4* cert;
+    // NN certificate of each source point from its last search, one 48-B record per slot of
+    // the PHASE's source tree (12-D in the SE(3) phase, 3-D in the R3 phase: a certificate of
+    // the other phase is void anyway), so k_nn_prep reads them in tree order, coalesced
+    NNCert* cert;
 };
 
 // ---- k_setup.hip
@@ -133,19 +145,18 @@ void launch_knn_big(const View& v, int write_knn, int k_min, const int32_t* qlis
 
 // ---- k_loop.hip
 // exact 1-NN of every active pair's source points: k_nn_prep settles the queries whose
-// certificate still holds and lists the rest, k_nn_group sweeps those 64 per wavefront
+// certificate still holds and lists the rest, k_nn_search sweeps those 64 per wavefront
+// (and the queries of sparse chunks one per wavefront, in the same grid)
 // through the target kd-tree (12-D in the SE(3) phase, 3-D in the R3 phase)
-void launch_nn_prep(const View& v, hipStream_t s);
+// publish: host slot that receives every pair's phase at the start of the launch (or null)
+void launch_nn_prep(const View& v, int32_t* publish, hipStream_t s);
 void nn_prof_report();  // (SE3ICP_PROF builds: k_nn_prep block phases, then reset)
 #ifdef SE3ICP_PROF
 double nn_prep_span();        // span of the last k_nn_prep launch (us)
 void nn_wave_report(int it);  // SE(3) group-wave durations since the last call
 #endif
-void launch_nn_se3(const View& v, hipStream_t s);
-void launch_nn_r3(const View& v, hipStream_t s);
-// the two grids of a phase (D = 12 or 3) separately: the group grid, the one-query-per-wave grid
-void launch_nn_group(const View& v, int D, hipStream_t s);
-void launch_nn_single(const View& v, int D, hipStream_t s);
+// the search of a phase (D = 12 or 3): one grid, single-query waves first, then the groups
+void launch_nn(const View& v, int D, hipStream_t s);
 void launch_trim(const View& v, hipStream_t s);
 // reduce + (k_reduce_final) per-pair solve and loop state machine; next_phase[p] receives
 // pair p's phase in the next iteration (PHASE_IDLE: finished)

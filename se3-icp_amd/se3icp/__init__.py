@@ -8,7 +8,8 @@ from ._lib import (METHODS, Params, Result, Se3IcpError, default_params, device_
 from .io import read_ply_xyz, write_ply_xyz  # noqa: F401
 from .registration import (DeviceBatchRunner, IterativeSE3Registration, PairResult, cli_params,  # noqa: F401
                            estimate_normals,
-                           kitti_params, knn_self, last_kernel_times, set_profiling, lounge_params, nearest_neighbors,
+                           kitti_params, knn_self, last_kernel_times, set_nn_events, set_profiling, lounge_params,
+                           nearest_neighbors,
                            register_batch, register_batch_device, register_batch_traced, toldi_frames)
 
 __all__ = [

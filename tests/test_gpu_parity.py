@@ -442,6 +442,30 @@ def test_batch_independence_16_vs_two_8(se3icp_mod):
         assert (f.num_iterations, f.num_pure_se3_iterations) == (h.num_iterations, h.num_pure_se3_iterations)
 
 
+def test_profiled_and_event_modes_equal_the_plain_loop(se3icp_mod):
+    """Per-stage HIP events (se3icp_set_profiling) and the SE(3) NN bracket
+    (se3icp_set_nn_events) change only how the host follows the loop, never its results:
+    bitwise the poses and iteration counts of the plain loop (C4 params, pairs that switch
+    to the R3 phase and finish at different iterations)."""
+    from se3icp import datasets
+    pairs, _ = datasets.kitti_like_pairs(4, seed=4)
+    p = se3icp_mod.kitti_params()
+    runs = {}
+    try:
+        for name, prof, ev in (("plain", False, False), ("events", False, True), ("profiled", True, True)):
+            se3icp_mod.set_profiling(prof)
+            se3icp_mod.set_nn_events(ev)
+            runs[name] = se3icp_mod.register_batch(pairs, "se3_gicp", p)
+    finally:
+        se3icp_mod.set_profiling(False)
+        se3icp_mod.set_nn_events(True)
+    for name in ("events", "profiled"):
+        for i, (a, b) in enumerate(zip(runs[name], runs["plain"])):
+            assert np.array_equal(a.T, b.T), (name, i, a.T - b.T)
+            assert (a.num_iterations, a.num_pure_se3_iterations) == (b.num_iterations, b.num_pure_se3_iterations), name
+    assert min(r.num_iterations for r in runs["plain"]) > 10
+
+
 def test_device_batch_runner_equals_register_batch(se3icp_mod):
     """The benchmark's timed call (clouds resident in HBM, prebuilt arguments, results read
     after the calls) returns bitwise the poses of the host-buffer batch entry, every call."""

@@ -7,10 +7,9 @@ Usage:
   tools/pmc_summary.py --workload C4 --command "<cmd>" --stats-md profiles/r04_C4_kernel_stats.md \
       --trace-dir gpurun_out/prof
 
-The stats summary also lists, per loop NN launch pair (k_nn_group<D> on the main stream and
-k_nn_single<D> on the side stream, the n-th dispatch of each), the SPAN from the first start
-to the last end -- what bench.py's roofline_other times with HIP events -- since the two
-kernels overlap and their averages do not add up to it.
+Round-3 builds ran each loop NN search as two grids on two streams (k_nn_group<D>,
+k_nn_single<D>); for such traces the stats summary also lists the SPAN of each launch pair,
+first start to last end.  Since round 4 the search is one grid (k_nn_search<D>).
 
 Each --pmc-dir holds one separate `rocprofv3 --pmc <counters> --output-format csv` pass
 (FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950).  HBM bytes per launch follow
