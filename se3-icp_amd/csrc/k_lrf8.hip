@@ -806,6 +806,10 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(6))) vo
     __builtin_amdgcn_wave_barrier();
 
     PROF8_NOW(t_a1);
+#if defined(SE3ICP_LRF8_CUT) && SE3ICP_LRF8_CUT == 1
+    if (lane == 0 && n_leaves == 12345u) v.stats[0] = nlist;  // (measurement build: stop after the traversal)
+    return;
+#endif
     PROF8_ADD(c_scan, t_a0, t_a1);
     // ---------------------------------------------------------------- final sets
     // Each list in rank order by exact key (ties by point index); every set boundary must
@@ -850,6 +854,10 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(6))) vo
     }
     const bool mine = (bool)((int)(mode == 1) & (int)!fb_q);
 
+#if defined(SE3ICP_LRF8_CUT) && SE3ICP_LRF8_CUT == 2
+    if (lane == 0 && n_cand == 12345u) v.stats[0] = n_cand;  // (measurement build: stop after the final order)
+    return;
+#endif
     // ---------------------------------------------------------------- per-query sums
     // (group g, list entries l, l+8, ...; see k_knn.hip for the 21 sums and the TOLDI
     // covariance about the quirk centroid, ISR.cpp:259-272).  The same loops, lane
@@ -944,6 +952,9 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(6))) vo
         atomicAdd(ctr + 4, (unsigned long long)n_cand);
     }
 
+#if defined(SE3ICP_LRF8_CUT) && SE3ICP_LRF8_CUT == 3
+    return;  // (measurement build: stop after the neighbour sums)
+#endif
     // ---------------------------------------------------------------- eigen-solves
     // TOLDI: C about the quirk centroid cl = (S' - q) / rz (ISR.cpp:259-272, see k_knn.hip),
     // its smallest eigenvector by cyclic Jacobi; normals: FastEigen3x3 of the kn-point
