@@ -135,7 +135,8 @@ Engine::~Engine() {
                      &d_qlist_, &d_qcount_, &d_hist_, &d_cert_, &d_sqlist_, &d_state_, &d_trim_cand_, &d_trim_ctr_, &d_scales_, &d_trim_hist_,
                      &d_lrf_fb_, &d_lrf_fbn_, &d_big_d_, &d_big_i_,
                      &t3_.perm, &t3_.pos, &t3_.vec, &t3_.vec64, &t3_.vec64a, &t3_.blo, &t3_.bhi, &t3_.lo, &t3_.hi, &t3_.scr,
-                     &t12_.perm, &t12_.pos, &t12_.vec, &t12_.vec64, &t12_.blo, &t12_.bhi, &t12_.lo, &t12_.hi, &t12_.scr};
+                     &t12_.perm, &t12_.pos, &t12_.vec, &t12_.vec64, &t12_.blo, &t12_.bhi, &t12_.lo, &t12_.hi, &t12_.scr,
+                     &t12_.vecT};
     for (DevBuf* b : all)
         if (b->p) (void)hipFree(b->p);
     if (h_pairs_) (void)hipHostFree(h_pairs_);
@@ -258,6 +259,7 @@ int Engine::build_tree(int D, const float* vec, hipStream_t s, const double* vec
     const size_t nb = (size_t)nclouds_ * nnodes * D;
     if (!ensure<uint32_t>(tb.blo, nb) || !ensure<uint32_t>(tb.bhi, nb) || !ensure<float>(tb.lo, nb) ||
         !ensure<float>(tb.hi, nb) || !ensure<float>(tb.scr, (size_t)D * ld_) ||
+        (D == 12 && !ensure<float>(tb.vecT, (size_t)12 * ld_)) ||
         (vec64 && !ensure<double>(tb.vec64, (size_t)3 * ld_)) ||
         (vec64 && D == 3 && !ensure<double4>(tb.vec64a, (size_t)ld_)))
         return SE3ICP_ERR_OUT_OF_MEMORY;
@@ -277,6 +279,7 @@ int Engine::build_tree(int D, const float* vec, hipStream_t s, const double* vec
     t.clouds = (const CloudDev*)d_clouds_.p;
     t.cloud_of = (const int32_t*)d_cloud_of_.p;
     t.vec = vec;
+    t.vecT = (D == 12) ? (float*)tb.vecT.p : const_cast<float*>(vec);  // (3-D: the input is columns)
     t.perm = (int32_t*)tb.perm.p;
     t.pos = (int32_t*)tb.pos.p;
     t.tvec = (float*)tb.vec.p;

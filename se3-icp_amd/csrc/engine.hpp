@@ -73,7 +73,7 @@ class Engine {
         CloudSetup st{};
     };
     struct TreeBufs {
-        DevBuf perm, pos, vec, vec64, vec64a, blo, bhi, lo, hi, scr;
+        DevBuf perm, pos, vec, vec64, vec64a, blo, bhi, lo, hi, scr, vecT;  // (vecT: 12-D input columns)
         int L = 0;  // depth of the trees in these buffers
     };
     int init();

@@ -45,14 +45,26 @@ __device__ __forceinline__ float ord_float(uint32_t u) {
     return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
 }
 
-// identity permutations; the sampled-box scratch of the first `box_nodes` heap nodes of
-// every cloud (the levels k_tree_bbox serves) cleared
+// identity permutations; the 12-D input rows copied into columns (t.vecT); the sampled-box
+// scratch of the first `box_nodes` heap nodes of every cloud (the levels k_tree_bbox serves)
+// cleared
 __global__ __launch_bounds__(256) void k_tree_init(TreeView t, int32_t* perm2, int box_nodes) {
     const int g = blockIdx.x * blockDim.x + threadIdx.x;
     if (g < t.npts) {
         const CloudDev cl = t.clouds[t.cloud_of[g]];
         t.perm[g] = g - cl.off;
         perm2[g] = g - cl.off;  // (both buffers hold valid point indices at all times)
+        if (t.D == 12) {
+            const float4* r = reinterpret_cast<const float4*>(t.vec + (size_t)g * 12);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const float4 x = r[k];
+                t.vecT[(size_t)(4 * k) * t.ld + g] = x.x;
+                t.vecT[(size_t)(4 * k + 1) * t.ld + g] = x.y;
+                t.vecT[(size_t)(4 * k + 2) * t.ld + g] = x.z;
+                t.vecT[(size_t)(4 * k + 3) * t.ld + g] = x.w;
+            }
+        }
     }
     const int per = box_nodes * t.D;
     const size_t nb = (size_t)t.nclouds * per;
@@ -252,7 +264,7 @@ __global__ __launch_bounds__(kPartThreads) void k_part_hist(TreeView t, int leve
             const int node = tree_node_of(g - cl.off, cl.n, level);
             const int id = part_node_id(c, level, node), slot = id - id0;
             const PartDim pd = dims[id];
-            const float x = t.vec[tree_in_ix(t, pd.best, cl.off + t.perm[g])];
+            const float x = tree_in_col(t, pd.best, cl.off + t.perm[g]);
             float qf = (x - pd.lo) * pd.scale;
             qf = fminf(fmaxf(qf, 0.f), kKeyMax);  // NaN -> 0
             const uint32_t key = (uint32_t)qf;
@@ -649,7 +661,7 @@ __global__ __launch_bounds__(kLevThreads) void k_tree_level(TreeView t, int leve
             pp[u] = e < m ? perm_in[base + e] : 0;
         }
 #pragma unroll
-        for (int u = 0; u < kLevU; ++u) x[u] = t.vec[tree_in_ix(t, pd.best, cl.off + pp[u])];
+        for (int u = 0; u < kLevU; ++u) x[u] = tree_in_col(t, pd.best, cl.off + pp[u]);
 #pragma unroll
         for (int u = 0; u < kLevU; ++u) {
             const int e = e0 + u * kLevThreads;
@@ -747,8 +759,8 @@ __global__ __launch_bounds__(kLevThreads) void k_tree_level(TreeView t, int leve
 // permutation stays in LDS and every level splits its sub-nodes at the median of the
 // coordinate of largest sample variance (a register sort by one wave for sub-nodes of
 // <= 512 points, a stable LDS partition above).  The node's vectors are first copied into
-// t.tvec at their level-G positions (column-major), so the levels read a few L2-resident
-// columns instead of gathering rows of the input.  The workgroup then finishes its subtree
+// t.scr at their level-G positions, one column per dimension, so the levels read a few
+// L2-resident columns instead of gathering rows of the input.  The workgroup then finishes its subtree
 // in place of k_tree_finish / k_tree_leafbox / k_tree_up: the final permutation and its
 // inverse, the tree-ordered f32 (and f64) vectors, and the boxes of every leaf and inner
 // node below level G.  s_val holds level-G positions e (s_p[e]: the point); ties in the
@@ -773,7 +785,10 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
     const int A = tree_first(n, G, i), m = tree_first(n, G, i + 1) - A;
     const int tid = threadIdx.x;
     const size_t ld = t.ld;
-    float* row0 = t.scr + (size_t)(cl.off + A) * D;  // the node's vectors at the level-G positions: row0[e * D + d]
+    // the node's vectors at the level-G positions, one column per dimension (col0[d * m + e]):
+    // a level gathers one coordinate of every point, 4 B from a 16-KB column instead of a
+    // 64-B sector of a 48-B row (round 3: 1.7 GB of HBM traffic per 12-D launch)
+    float* col0 = t.scr + (size_t)(cl.off + A) * D;
 #ifdef SE3ICP_PROF
     unsigned long long tq[5];
     tq[0] = __builtin_amdgcn_s_memrealtime();
@@ -786,12 +801,17 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
         if (p >= 0) {
             if constexpr (D == 12) {
                 const float4* r = reinterpret_cast<const float4*>(t.vec + (size_t)(cl.off + p) * 12);
-                float4* w = reinterpret_cast<float4*>(row0 + (size_t)e * 12);
 #pragma unroll
-                for (int k = 0; k < 3; ++k) w[k] = r[k];
+                for (int k = 0; k < 3; ++k) {
+                    const float4 x = r[k];
+                    col0[(4 * k) * m + e] = x.x;
+                    col0[(4 * k + 1) * m + e] = x.y;
+                    col0[(4 * k + 2) * m + e] = x.z;
+                    col0[(4 * k + 3) * m + e] = x.w;
+                }
             } else {
 #pragma unroll
-                for (int d = 0; d < D; ++d) row0[e * D + d] = t.vec[(size_t)d * ld + cl.off + p];
+                for (int d = 0; d < D; ++d) col0[d * m + e] = t.vec[(size_t)d * ld + cl.off + p];
             }
         }
     }
@@ -823,7 +843,7 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
                     ++cnt;
 #pragma unroll
                     for (int d = 0; d < D; ++d) {
-                        const float x = row0[p * D + d];
+                        const float x = col0[d * m + p];
                         s1[d] += x;
                         s2[d] = fmaf(x, x, s2[d]);
                     }
@@ -866,7 +886,7 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
                         if (e < a1) {
                             const int p = s_val[e];
                             const unsigned lo = pk ? ((unsigned)s_p[p] << 12) | (unsigned)p : (unsigned)p;
-                            key[u] = ((unsigned long long)ord_bits(row0[p * D + bd]) << 32) | lo;
+                            key[u] = ((unsigned long long)ord_bits(col0[bd * m + p]) << 32) | lo;
                         }
                     }
                     wave_sort_keys<PER>(key);
@@ -909,7 +929,7 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
                     const int sub = tree_node_of(A + e, n, l) - (i << r);
                     const int p = s_val[e];
                     const float sd = s_sd[sub];
-                    const float x = row0[p * D + s_best[sub]];
+                    const float x = col0[s_best[sub] * m + p];
                     float qf = sd > 0.f ? (x - (s_mu[sub] - 8.f * sd)) * (4194303.f / (16.f * sd)) : 0.f;
                     qf = fminf(fmaxf(qf, 0.f), 4194303.f);  // NaN -> 0
                     q[u] = (uint32_t)qf;
@@ -1040,9 +1060,9 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
         const int e = s_val[x];
         const int p = s_p[e];
         const int g = cl.off + A + x, src = cl.off + p;
-        float v[D];
+        float v[D];  // (the input vectors of the point: a 48-B row / three columns)
         if constexpr (D == 12) {
-            const float4* r = reinterpret_cast<const float4*>(row0 + (size_t)e * 12);
+            const float4* r = reinterpret_cast<const float4*>(t.vec + (size_t)src * 12);
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 const float4 q = r[k];
@@ -1050,7 +1070,7 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
             }
         } else {
 #pragma unroll
-            for (int d = 0; d < D; ++d) v[d] = row0[e * D + d];
+            for (int d = 0; d < D; ++d) v[d] = t.vec[(size_t)d * ld + src];
         }
         if (in) {
             t.perm[g] = p;

@@ -24,6 +24,9 @@ struct TreeView {
     const CloudDev* clouds;
     const int32_t* cloud_of;
     const float* vec;  // input vectors, original order: 12-D [ld][12] rows, 3-D [3][ld] columns
+    // the input as [D][ld] columns (3-D: vec itself; 12-D: a copy k_tree_init writes), for the
+    // passes that gather ONE coordinate per point (a 4-B column entry, not a 48-B row's sector)
+    float* vecT;
     int32_t* perm;     // [ld] tree position (global slot) -> local point index
     int32_t* pos;      // [ld] point (global slot) -> local tree position
     float* tvec;       // vectors in tree order: 3-D [3][ld] columns, 12-D [ld][12] rows (tree_tv_ix)
@@ -55,6 +58,8 @@ __host__ __device__ __forceinline__ int tree_heap(int level, int i) { return (1 
 __device__ __forceinline__ size_t tree_in_ix(const TreeView& t, int d, int p) {
     return t.D == 12 ? (size_t)p * 12 + d : (size_t)d * t.ld + p;
 }
+// coordinate d of the input vector at global slot p, from the column copy
+__device__ __forceinline__ float tree_in_col(const TreeView& t, int d, int p) { return t.vecT[(size_t)d * t.ld + p]; }
 
 // element d of the tree-ordered vector at global tree slot x: the 12-D vectors are 48-B
 // rows (a leaf's 64 targets are one contiguous 3-KB run: three 16-B loads per lane instead
