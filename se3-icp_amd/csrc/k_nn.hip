@@ -977,8 +977,8 @@ void nn_wave_report(int it) {
     if (hipMemcpyFromSymbol(sp, HIP_SYMBOL(g_wave_span), sizeof(sp)) != hipSuccess) return;
     double tot = 0, n = 0;
     for (int b = 0; b < 41; ++b) { tot += (double)h[1][b]; n += (double)h[0][b]; }
-    std::fprintf(stderr, "[nn] iter %d: wave span %.1f us; summed wave time / 4096 slots %.1f us; durations (25 us bins):",
-                 it, sp[1] > sp[0] ? (sp[1] - sp[0]) / 100.0 : 0.0, tot / 100.0 / 4096.0);
+    std::fprintf(stderr, "[nn] iter %d: %.0f group waves, span %.1f us; summed wave time / 4096 slots %.1f us; "
+                 "durations (25 us bins):", it, n, sp[1] > sp[0] ? (sp[1] - sp[0]) / 100.0 : 0.0, tot / 100.0 / 4096.0);
     for (int b = 0; b < 41; ++b)
         if (h[0][b]) std::fprintf(stderr, " %d:%llu/%.1f%%", 25 * b, h[0][b], 100.0 * (double)h[1][b] / std::max(tot, 1.0));
     std::fprintf(stderr, "\n");
