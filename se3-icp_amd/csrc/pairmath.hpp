@@ -85,15 +85,30 @@ SE3ICP_HD void svd3(const double A[3][3], double U[3][3], double s[3], double V[
             for (int q = p + 1; q < 3; ++q) {
                 if (fabs(B[p][q]) <= thr && fabs(B[q][p]) <= thr) continue;
                 done = false;
-                // 1) left rotation making the block symmetric
+                // 1) left rotation making the block symmetric: the angle atan2(c - b, a + d),
+                //    its cosine and sine from the hypotenuse (no trigonometric calls: the
+                //    serial solve of k_reduce_final spent most of its time in them)
                 const double a = B[p][p], b = B[p][q], c = B[q][p], d = B[q][q];
-                const double th1 = atan2(c - b, a + d);
-                svd3_rot_left(B, U, p, q, cos(th1), sin(th1));
-                // 2) symmetric Jacobi on [[x, y], [y, z]]
+                {
+                    const double h = sqrt((a + d) * (a + d) + (c - b) * (c - b));
+                    const double c1 = h > 0.0 ? (a + d) / h : 1.0, s1 = h > 0.0 ? (c - b) / h : 0.0;
+                    svd3_rot_left(B, U, p, q, c1, s1);
+                }
+                // 2) symmetric Jacobi on [[x, y], [y, z]]: the angle 0.5 atan2(2y, z - x) in
+                //    (-pi/2, pi/2], its cosine and sine by the half-angle formulas (the
+                //    well-conditioned one of the two for the sign of cos 2t)
                 const double x = B[p][p], y = 0.5 * (B[p][q] + B[q][p]), z = B[q][q];
                 if (y != 0.0) {
-                    const double th2 = 0.5 * atan2(2.0 * y, z - x);
-                    const double c2 = cos(th2), s2 = sin(th2);
+                    const double h = sqrt(4.0 * y * y + (z - x) * (z - x));
+                    const double c2t = (z - x) / h, s2t = 2.0 * y / h;
+                    double c2, s2;
+                    if (c2t >= 0.0) {
+                        c2 = sqrt(0.5 * (1.0 + c2t));
+                        s2 = s2t / (2.0 * c2);
+                    } else {
+                        s2 = copysign(sqrt(0.5 * (1.0 - c2t)), s2t);
+                        c2 = s2t / (2.0 * s2);
+                    }
                     svd3_rot_left(B, U, p, q, c2, -s2);  // J^T from the left (J = [[c,s],[-s,c]] on the right)
                     svd3_rot_right(B, V, p, q, c2, s2);
                 }

@@ -88,6 +88,31 @@ def test_umeyama_matches_numpy_and_recovers_exact_motion(pairmath):
     assert np.array_equal(got[1].reshape(4, 4), np.eye(4))
 
 
+def test_umeyama_rotation_extremes(pairmath):
+    """The Jacobi rotations of the 3x3 SVD come from half-angle formulas, not trigonometric
+    calls: half turns (cos 2t = -1 blocks), quarter turns, near-identity motions and a planar
+    source (rank-2 cross-covariance) must still give numpy's umeyama."""
+    rng = np.random.default_rng(11)
+    cases, want = [], []
+    rots = [np.diag([-1.0, -1.0, 1.0]), np.diag([1.0, -1.0, -1.0]), np.diag([-1.0, 1.0, -1.0]),
+            _rot(0, 0, np.pi / 2), _rot(np.pi / 2, 0, 0), _rot(0, np.pi - 1e-9, 0), _rot(1e-9, -2e-9, 3e-9),
+            _rot(np.pi, np.pi / 2, -np.pi / 3)]
+    for i, R in enumerate(rots):
+        src = rng.normal(size=(100, 3)) * np.array([2.0, 1.0, 0.5])
+        if i == len(rots) - 1:
+            src[:, 2] = 0.0  # planar source
+        t = rng.uniform(-1, 1, 3)
+        dst = src @ R.T + t
+        s, n = _moments(src, dst)
+        cases.append("U " + _fmt(s) + " " + _fmt([n]))
+        want.append(_umeyama(src, dst))
+        assert np.allclose(want[-1][:3, :3], R, atol=1e-7)
+    for got, T in zip(pairmath(cases), want):
+        G = got.reshape(4, 4)
+        assert np.abs(G - T).max() < 1e-9, (G, T)
+        assert np.isclose(np.linalg.det(G[:3, :3]), 1.0)
+
+
 def _pack(A, b):
     return np.concatenate([A[np.triu_indices(6)], b])
 
