@@ -308,7 +308,9 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
     // target tree (the child whose f32 box bound is smaller, down to a leaf; a target of
     // that leaf).  The search only uses it for its first pruning threshold, so any target
     // is valid; a near one spares the group walk the nodes an infinite threshold opens.
-    if ((int)(v.corr_idx[g] < 0) & (int)(ct.n > 0)) {
+    // (only a run's first iteration can lack one: corr_idx is reset to -1 when the run
+    // starts and every search writes it, so later iterations skip this dependent gather)
+    if ((int)(it == 1) & (int)(ct.n > 0) && v.corr_idx[g] < 0) {
         double m0[D], Q[D];
         load_m0<D>(v, TR, gx, g, m0);
         pose_m0<D>(T, m0, Q);
