@@ -7,7 +7,7 @@
 //   split by a stable median partition (ties keep tree order) of a coordinate quantised to
 //   a 22-bit key -- no device-wide sort.
 //   * global levels while the nodes hold more than kLocalMax (4096) points: the first ones,
-//     while there are fewer than kTreeWgMin nodes, by the multi-pass k_part_* sequence
+//     while there are fewer than kTreeWgMin nodes (12-D: 2 kTreeWgMin), by the multi-pass k_part_* sequence
 //     (sampled box -> split dimension, block histograms of the top 11 key bits, the median
 //     bin, its low 11 bits, segmented counts, one carry scan, scatter); the rest by one
 //     k_tree_level launch per level (a workgroup per node);
@@ -15,7 +15,8 @@
 //     every sub-node at the median of its largest-sample-variance coordinate, and writes
 //     the final permutation, its inverse, the tree-ordered vectors and the boxes of its
 //     leaves and inner nodes; k_tree_up unions the boxes above.
-//   At C4 (16 clouds of ~120k points): 17 launches per tree.  Leaves hold <= 64 points.
+//   At C4 (16 clouds of ~120k points): 17 launches for the 3-D tree, 25 for the 12-D one.
+//   Leaves hold <= 64 points.
 // Outputs per cloud: perm (tree position -> point), pos (inverse), the vectors in tree
 // order (coalesced leaf loads) and f32 AABBs of all 2^(L+1)-1 nodes (heap order),
 // inflated by a few ulps so the f32 boxes bound the f64 points they stand for.
@@ -763,8 +764,7 @@ __global__ __launch_bounds__(kLevThreads) void k_tree_level(TreeView t, int leve
 // L2-resident columns instead of gathering rows of the input.  The workgroup then finishes its subtree
 // in place of k_tree_finish / k_tree_leafbox / k_tree_up: the final permutation and its
 // inverse, the tree-ordered f32 (and f64) vectors, and the boxes of every leaf and inner
-// node below level G.  s_val holds level-G positions e (s_p[e]: the point); ties in the
-// wave sorts are broken by the point index, as when s_val held the points.
+// node below level G.  s_val holds level-G positions e (s_p[e]: the point).
 constexpr int kLocalMax = 4096;  // power of two
 constexpr int kWaveSortPer = 8;  // sub-nodes of <= 512 points: register sort by one wave
 constexpr int kLocalThreads = 512;
@@ -793,30 +793,55 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
     unsigned long long tq[5];
     tq[0] = __builtin_amdgcn_s_memrealtime();
 #endif
-    // the node's points and their vectors at the level-G positions
-    for (int e = tid; e < kLocalMax; e += kLocalThreads) {
-        const int p = e < m ? t.perm[cl.off + A + e] : -1;
-        s_val[e] = e;
-        s_p[e] = p;
-        if (p >= 0) {
-            if constexpr (D == 12) {
-                const float4* r = reinterpret_cast<const float4*>(t.vec + (size_t)(cl.off + p) * 12);
+    // the node's points and their vectors at the level-G positions: every permutation entry
+    // of the thread first, then the rows in batches of LB with all their loads issued before
+    // the column stores (a load after a store to another global array is not hoisted above
+    // it, so one point at a time was two dependent round trips per point)
+    {
+        constexpr int LP = kLocalMax / kLocalThreads;
+        constexpr int LB = D == 12 ? 4 : LP;
+        static_assert(LP % LB == 0, "whole batches");
+        int pl[LP];
 #pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    const float4 x = r[k];
-                    col0[(4 * k) * m + e] = x.x;
-                    col0[(4 * k + 1) * m + e] = x.y;
-                    col0[(4 * k + 2) * m + e] = x.z;
-                    col0[(4 * k + 3) * m + e] = x.w;
+        for (int u = 0; u < LP; ++u) {
+            const int e = tid + u * kLocalThreads;
+            pl[u] = e < m ? t.perm[cl.off + A + e] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < LP; ++u) {
+            const int e = tid + u * kLocalThreads;
+            s_val[e] = e;
+            s_p[e] = pl[u];
+        }
+#pragma unroll
+        for (int u0 = 0; u0 < LP; u0 += LB) {
+            float x[LB][D];
+#pragma unroll
+            for (int u = 0; u < LB; ++u) {
+                const int p = pl[u0 + u] >= 0 ? pl[u0 + u] : 0;
+                if constexpr (D == 12) {
+                    const float4* r = reinterpret_cast<const float4*>(t.vec + (size_t)(cl.off + p) * 12);
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        const float4 q = r[k];
+                        x[u][4 * k] = q.x; x[u][4 * k + 1] = q.y; x[u][4 * k + 2] = q.z; x[u][4 * k + 3] = q.w;
+                    }
+                } else {
+#pragma unroll
+                    for (int d = 0; d < D; ++d) x[u][d] = t.vec[(size_t)d * ld + cl.off + p];
                 }
-            } else {
+            }
 #pragma unroll
-                for (int d = 0; d < D; ++d) col0[d * m + e] = t.vec[(size_t)d * ld + cl.off + p];
+            for (int u = 0; u < LB; ++u) {
+                const int e = tid + (u0 + u) * kLocalThreads;
+                if (pl[u0 + u] >= 0) {
+#pragma unroll
+                    for (int d = 0; d < D; ++d) col0[d * m + e] = x[u][d];
+                }
             }
         }
     }
     __syncthreads();  // (global writes of the workgroup, read back by other threads of it)
-    const bool pk = n <= (1 << 20);  // tie order of the wave sorts: (point, position) in 32 bits
 #ifdef SE3ICP_PROF
     tq[1] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -870,30 +895,35 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
         __syncthreads();
         const int max_sub = (m + nsub - 1) / nsub + 1;  // sub-node sizes differ by <= 1
         if (max_sub <= 64 * kWaveSortPer) {
-            // small sub-nodes: one wave sorts each in registers, (coordinate, point) keys, in a
-            // network of the sub-node's size (128, 256 or 512 keys)
+            // small sub-nodes: one wave sorts each in registers, in a network of the sub-node's
+            // size (128, 256 or 512 keys) over 32-bit keys: the split coordinate quantised to
+            // 20 bits over the sub-node's sample mean +- 8 sd | the level-G position (12 bits,
+            // which also orders ties).  Any order gives a valid balanced tree (the searches
+            // are exact over the node boxes); this one keeps the split at the median.
             const int lane = tid & 63, wv = tid >> 6;
             auto wave_level = [&](auto per_tag) {
                 constexpr int PER = decltype(per_tag)::value;
                 for (int k = wv; k < nsub; k += kLocalThreads / 64) {
                     const int a0 = tree_first(n, l, (i << r) + k) - A, a1 = tree_first(n, l, (i << r) + k + 1) - A;
                     const int bd = s_best[k];
-                    unsigned long long key[PER];
+                    const float sd = s_sd[k], qlo = s_mu[k] - 8.f * sd;
+                    const float qs = sd > 0.f ? 1048575.f / (16.f * sd) : 0.f;
+                    unsigned key[PER];
 #pragma unroll
                     for (int u = 0; u < PER; ++u) {
                         const int e = a0 + lane * PER + u;
-                        key[u] = ~0ull;
+                        key[u] = ~0u;
                         if (e < a1) {
                             const int p = s_val[e];
-                            const unsigned lo = pk ? ((unsigned)s_p[p] << 12) | (unsigned)p : (unsigned)p;
-                            key[u] = ((unsigned long long)ord_bits(col0[bd * m + p]) << 32) | lo;
+                            const float qf = fminf(fmaxf((col0[bd * m + p] - qlo) * qs, 0.f), 1048575.f);  // NaN -> 0
+                            key[u] = ((unsigned)qf << 12) | (unsigned)p;
                         }
                     }
-                    wave_sort_keys<PER>(key);
+                    wave_sort_u32<PER>(key);
 #pragma unroll
                     for (int u = 0; u < PER; ++u) {
                         const int e = a0 + lane * PER + u;
-                        if (e < a1) s_val[e] = (int32_t)((unsigned)key[u] & (pk ? 0xfffu : 0xffffffffu));
+                        if (e < a1) s_val[e] = (int32_t)(key[u] & 0xfffu);
                     }
                 }
             };
@@ -1052,69 +1082,93 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
     const int R = t.L - G;  // levels of the subtree below its root
     const int lane = tid & 63, wv = tid >> 6;
     const size_t bbase = (size_t)c * t.nnodes * D;
-    for (int j = wv; j < (1 << R); j += kLocalThreads / 64) {
-        const int leaf = (i << R) + j;
-        const int a0 = tree_first(n, t.L, leaf), a1 = tree_first(n, t.L, leaf + 1);
-        const bool in = lane < a1 - a0;
-        const int x = a0 - A + (in ? lane : 0);
-        const int e = s_val[x];
-        const int p = s_p[e];
-        const int g = cl.off + A + x, src = cl.off + p;
-        float v[D];  // (the input vectors of the point: a 48-B row / three columns)
-        if constexpr (D == 12) {
-            const float4* r = reinterpret_cast<const float4*>(t.vec + (size_t)src * 12);
+    // FB leaves per wave at a time: their row loads are issued together, then each leaf's
+    // stores and box (one leaf at a time was two dependent round trips per leaf)
+    constexpr int FB = D == 12 ? 2 : 4;
+    constexpr int NWV = kLocalThreads / 64;
+    for (int j0 = wv; j0 < (1 << R); j0 += FB * NWV) {
+        float v[FB][D];  // (the input vectors of the point: a 48-B row / three columns)
+        double w64[FB][3];
+        int xq[FB], pq[FB];
+        bool inq[FB];
 #pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                const float4 q = r[k];
-                v[4 * k] = q.x; v[4 * k + 1] = q.y; v[4 * k + 2] = q.z; v[4 * k + 3] = q.w;
-            }
-        } else {
-#pragma unroll
-            for (int d = 0; d < D; ++d) v[d] = t.vec[(size_t)d * ld + src];
-        }
-        if (in) {
-            t.perm[g] = p;
-            t.pos[src] = A + x;
+        for (int b = 0; b < FB; ++b) {
+            const int j = j0 + b * NWV;
+            const int leaf = (i << R) + j;
+            const bool live = j < (1 << R);
+            const int a0 = live ? tree_first(n, t.L, leaf) : A, a1 = live ? tree_first(n, t.L, leaf + 1) : A;
+            inq[b] = lane < a1 - a0;
+            xq[b] = a0 - A + (inq[b] ? lane : 0);
+            const int e = s_val[xq[b]];
+            pq[b] = s_p[e];
+            const int src = cl.off + pq[b];
             if constexpr (D == 12) {
-                float4* o = reinterpret_cast<float4*>(t.tvec + (size_t)g * 12);
+                const float4* r = reinterpret_cast<const float4*>(t.vec + (size_t)src * 12);
 #pragma unroll
-                for (int k = 0; k < 3; ++k) o[k] = make_float4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+                for (int k = 0; k < 3; ++k) {
+                    const float4 q = r[k];
+                    v[b][4 * k] = q.x; v[b][4 * k + 1] = q.y; v[b][4 * k + 2] = q.z; v[b][4 * k + 3] = q.w;
+                }
             } else {
 #pragma unroll
-                for (int d = 0; d < D; ++d) t.tvec[(size_t)d * ld + g] = v[d];
+                for (int d = 0; d < D; ++d) v[b][d] = t.vec[(size_t)d * ld + src];
             }
-            if (want64) {
+            w64[b][0] = w64[b][1] = w64[b][2] = 0.0;
+            if ((int)want64 & (int)inq[b]) {
                 if constexpr (D == 12) {  // the translation rows only (the loop reads the frames by point)
                     // (byte offset 96*src + 72 is 8 mod 16: three 8-B loads, no double2)
                     const double* r64 = t.vec64 + (size_t)src * 12 + 9;
-                    const double w0 = r64[0], w1 = r64[1], w2 = r64[2];
-                    t.tvec64[g] = w0;
-                    t.tvec64[ld + g] = w1;
-                    t.tvec64[2 * ld + g] = w2;
+                    w64[b][0] = r64[0]; w64[b][1] = r64[1]; w64[b][2] = r64[2];
                 } else {
-                    double w[3] = {0.0, 0.0, 0.0};
 #pragma unroll
-                    for (int d = 0; d < D; ++d) t.tvec64[(size_t)d * ld + g] = w[d] = t.vec64[(size_t)d * ld + src];
-                    if (t.tpt64) t.tpt64[g] = make_double4(w[0], w[1], w[2], 0.0);
+                    for (int d = 0; d < D; ++d) w64[b][d] = t.vec64[(size_t)d * ld + src];
                 }
             }
         }
-        const size_t hb = bbase + (size_t)tree_heap(t.L, leaf) * D;
 #pragma unroll
-        for (int d = 0; d < D; ++d) {
-            float lo = in ? v[d] : INFINITY, hi = in ? v[d] : -INFINITY;
+        for (int b = 0; b < FB; ++b) {
+            const int j = j0 + b * NWV;
+            if (j >= (1 << R)) break;  // (wave-uniform)
+            const int leaf = (i << R) + j;
+            const bool in = inq[b];
+            const int x = xq[b], p = pq[b];
+            const int g = cl.off + A + x, src = cl.off + p;
+            if (in) {
+                t.perm[g] = p;
+                t.pos[src] = A + x;
+                if constexpr (D == 12) {
+                    float4* o = reinterpret_cast<float4*>(t.tvec + (size_t)g * 12);
 #pragma unroll
-            for (int o = 32; o >= 1; o >>= 1) {  // (DPP / swizzle / permlane exchanges)
-                lo = fminf(lo, xor_lane(lo, o));
-                hi = fmaxf(hi, xor_lane(hi, o));
+                    for (int k = 0; k < 3; ++k) o[k] = make_float4(v[b][4 * k], v[b][4 * k + 1], v[b][4 * k + 2], v[b][4 * k + 3]);
+                } else {
+#pragma unroll
+                    for (int d = 0; d < D; ++d) t.tvec[(size_t)d * ld + g] = v[b][d];
+                }
+                if (want64) {
+#pragma unroll
+                    for (int d = 0; d < 3; ++d) t.tvec64[(size_t)d * ld + g] = w64[b][d];
+                    if constexpr (D == 3) {
+                        if (t.tpt64) t.tpt64[g] = make_double4(w64[b][0], w64[b][1], w64[b][2], 0.0);
+                    }
+                }
             }
-            if (lo <= hi) {
-                lo = lo - (fabsf(lo) * 4.8e-7f + 1e-30f);
-                hi = hi + (fabsf(hi) * 4.8e-7f + 1e-30f);
-            }
-            if (lane == d) {  // empty leaf: [inf, -inf], a box no query reaches
-                t.lo[hb + d] = lo;
-                t.hi[hb + d] = hi;
+            const size_t hb = bbase + (size_t)tree_heap(t.L, leaf) * D;
+#pragma unroll
+            for (int d = 0; d < D; ++d) {
+                float lo = in ? v[b][d] : INFINITY, hi = in ? v[b][d] : -INFINITY;
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) {  // (DPP / swizzle / permlane exchanges)
+                    lo = fminf(lo, xor_lane(lo, o));
+                    hi = fmaxf(hi, xor_lane(hi, o));
+                }
+                if (lo <= hi) {
+                    lo = lo - (fabsf(lo) * 4.8e-7f + 1e-30f);
+                    hi = hi + (fabsf(hi) * 4.8e-7f + 1e-30f);
+                }
+                if (lane == d) {  // empty leaf: [inf, -inf], a box no query reaches
+                    t.lo[hb + d] = lo;
+                    t.hi[hb + d] = hi;
+                }
             }
         }
     }
@@ -1285,7 +1339,10 @@ int build_trees(TreeView t, void* tmp, size_t tmp_bytes, uint32_t* qbuf, int32_t
     tc.perm = (G % 2 == 0) ? final_perm : perm_alt;
     int32_t* other = (G % 2 == 0) ? perm_alt : final_perm;
     int H = 0;  // levels of the multi-pass path (k_tree_bbox / k_part_*)
-    while (H < G && (t.nclouds << H) < kTreeWgMin) ++H;
+    // (12-D: a level of 32 nodes through the multi-pass sequence too -- one 1024-thread
+    // workgroup per 60k-point node left 7/8 of the CUs idle for 120 us; 3-D breaks even)
+    const int wg_min = t.D == 12 ? 2 * kTreeWgMin : kTreeWgMin;
+    while (H < G && (t.nclouds << H) < wg_min) ++H;
     hipLaunchKernelGGL(k_tree_init, dim3(gfill), dim3(256), 0, s, tc, other, (1 << H) - 1);
     if (ps.overflow_words) hipLaunchKernelGGL(k_clear_words, dim3(256), dim3(256), 0, s, ps.overflow, ps.overflow_words);
     const int nblk = (t.npts + kPartElems - 1) / kPartElems;

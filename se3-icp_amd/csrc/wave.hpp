@@ -188,6 +188,43 @@ __device__ __forceinline__ void wave_sort_keys(unsigned long long (&k)[PER]) {
     bitonic_net<PER, 64 * PER, 64 * PER>(k, threadIdx.x & 63, nullptr);
 }
 
+// The same network over 32-bit keys, registers and lane exchanges only (64*PER keys of one
+// wave): an in-register compare-exchange is a min and a max, a cross-lane one the
+// partner's key and a min or max -- about half the instructions of the 64-bit network.
+template <int PER, int KK, int JD>
+__device__ __forceinline__ void bitonic_stage_u32(unsigned (&k)[PER], int lane) {
+    if constexpr (JD < PER) {
+#pragma unroll
+        for (int s = 0; s < PER; ++s) {
+            if ((s & JD) == 0) {
+                const int t = s | JD;
+                const bool up = ((lane * PER + s) & KK) == 0;
+                const unsigned lo = min(k[s], k[t]), hi = max(k[s], k[t]);
+                k[s] = up ? lo : hi;
+                k[t] = up ? hi : lo;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int s = 0; s < PER; ++s) {
+            const int e = lane * PER + s;
+            const unsigned pk = xor_lane(k[s], JD / PER);
+            k[s] = (((e & JD) == 0) == ((e & KK) == 0)) ? min(pk, k[s]) : max(pk, k[s]);
+        }
+    }
+}
+template <int PER, int N, int KK = 2, int JD = 1>
+__device__ __forceinline__ void bitonic_net_u32(unsigned (&k)[PER], int lane) {
+    bitonic_stage_u32<PER, KK, JD>(k, lane);
+    if constexpr (JD > 1) bitonic_net_u32<PER, N, KK, JD / 2>(k, lane);
+    else if constexpr (KK < N) bitonic_net_u32<PER, N, KK * 2, KK>(k, lane);
+}
+// ascending register sort of the 64*PER 32-bit keys of one wave
+template <int PER>
+__device__ __forceinline__ void wave_sort_u32(unsigned (&k)[PER]) {
+    bitonic_net_u32<PER, 64 * PER>(k, threadIdx.x & 63);
+}
+
 // Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, Workgroup
 // dispatch): relabel them so that each XCD runs one contiguous range of the grid and its
 // L2 keeps the data neighbouring blocks share (bijective for any grid size).
