@@ -677,8 +677,12 @@ void launch_lrf(const View& v, int write_knn, hipStream_t s) {
                        v.setup, v.clouds, v.t3.lo, v.t3.hi, nullptr, nullptr, kQ);
 }
 
-constexpr int kListQpw = 4;        // queries per wave of the hand-over pass (measured: 1, 2, 4, 8)
-constexpr int kListBlocks = 1024;  // its grid (strided)
+// The hand-over pass: queries per wave and its grid (strided).  1,280 4-wave blocks are one
+// resident round at 5 waves per SIMD; two queries per wave then cover C4's ~9.9k hand-overs
+// in that round (same-box A/B at C4, k_lrf8 + k_lrf: 4.01 ms at 4 per wave / 1,024 blocks,
+// 3.92 at 2 / 1,280, 3.95 at 3 / 1,024, 4.02 at 2 / 2,048; round 3: 1 and 8 per wave slower)
+constexpr int kListQpw = 2;
+constexpr int kListBlocks = 1280;
 void launch_lrf_list(const View& v, const int32_t* qlist, const int32_t* qcount, hipStream_t s, int qpw) {
     const size_t lds = sizeof(int) * (size_t)kWaves * kQ * std::min(v.kmax, kSmallK);
     const int nblk = std::max(1, std::min(kListBlocks, (v.npts + kWaves * kQ - 1) / (kWaves * kQ)));
