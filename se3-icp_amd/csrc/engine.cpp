@@ -129,7 +129,7 @@ Engine::~Engine() {
     (void)hipSetDevice(dev_);
     DevBuf* all[] = {&d_clouds_, &d_setup_, &d_pairs_, &d_cloud_of_, &d_inptr_, &d_in_, &d_xyz64_, &d_xyz32_,
                      &d_fr64_, &d_fr32_, &d_nrm64_, &d_conf64_, &d_knn_,
-                     &d_corr_idx_, &d_corr_dist_, &d_flag_count_, &d_trim_key_, &d_red_partial_,
+                     &d_corr_idx_, &d_corr_dist_, &d_flag_count_, &d_gcost_, &d_cls_, &d_trim_key_, &d_red_partial_,
                      &d_red_out_, &d_work_, &d_wb_, &d_wn_, &d_chunks_, &d_partial_, &d_centers_,
                      &d_rechecked_, &d_keys0_, &d_vals1_, &d_sort_tmp_, &d_stats_,
                      &d_qlist_, &d_qcount_, &d_hist_, &d_cert_, &d_sqlist_, &d_state_, &d_trim_cand_, &d_trim_ctr_, &d_scales_, &d_trim_hist_,
@@ -216,6 +216,8 @@ View Engine::view() const {
     v.corr_dist = (float*)d_corr_dist_.p;
     v.stats = (unsigned long long*)d_stats_.p;
     v.flag_count = (int32_t*)d_flag_count_.p;
+    v.gcost = (uint32_t*)d_gcost_.p;
+    v.cls = (int32_t*)d_cls_.p;
     v.trim_key = (uint64_t*)d_trim_key_.p;
     v.trim_cand = (unsigned long long*)d_trim_cand_.p;
     v.trim_ctr = (unsigned*)d_trim_ctr_.p;
@@ -506,10 +508,13 @@ int Engine::setup_chunks(int npairs, hipStream_t s) {
     chunk_level_ = std::max(0, tree_L_ - 4);
     nchunks_ = npairs << chunk_level_;
     if (!ensure<int32_t>(d_qlist_, (size_t)nchunks_ * kChunkQ) || !ensure<int32_t>(d_qcount_, (size_t)nchunks_ * (kChunkQ / 64)) ||
-        !ensure<double>(d_hist_, (size_t)kHist * npairs * 12))
+        !ensure<double>(d_hist_, (size_t)kHist * npairs * 12) || !ensure<uint32_t>(d_gcost_, (size_t)nchunks_ * 16) ||
+        !ensure<int32_t>(d_cls_, nn_cls_words(nchunks_)))
         return SE3ICP_ERR_OUT_OF_MEMORY;
     if (pinned(h_hist_, h_hist_cap_, (size_t)npairs * 12)) return SE3ICP_ERR_OUT_OF_MEMORY;
     HIPCHK(hipMemsetAsync(d_cert_.p, 0xff, sizeof(NNCert) * ld_, s));  // iteration -1: no certificate
+    HIPCHK(hipMemsetAsync(d_gcost_.p, 0, sizeof(uint32_t) * nchunks_ * 16, s));
+    HIPCHK(hipMemsetAsync(d_cls_.p, 0, sizeof(int32_t) * 2 * 8 * 16, s));
     return 0;
 }
 

@@ -584,6 +584,7 @@ __global__ __launch_bounds__(kFinThreads) void k_reduce_final(View v, const int3
                                                       PairState* state, double* hist, int32_t* next_phase) {
     const int p = blockIdx.x;
     if ((int)(p == 0) & (int)(threadIdx.x < 3)) v.flag_count[threadIdx.x] = 0;  // single-query lists
+    if ((int)(p == 0) & (int)(threadIdx.x < 2 * 8 * 16)) v.cls[threadIdx.x] = 0;  // search cost-class counts
     PairDev* P = v.pairs + p;
     if (P->phase == PHASE_IDLE) {
         if ((int)(threadIdx.x == 0) & (int)(next_phase != nullptr)) next_phase[p] = PHASE_IDLE;

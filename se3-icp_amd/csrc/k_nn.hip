@@ -192,12 +192,32 @@ constexpr int kDense = 256;
 constexpr int kWpe = 4;        // waves per SIMD of k_nn_search (its natural 128 VGPRs; 5 measured +8 %)
 constexpr int kXcdRun = 256;   // group blocks per XCD run (16 chunks; runs dealt round-robin over the XCDs:
                                // neighbouring chunks share target leaves in one L2, SE(3) NN -3 %)
+__device__ __forceinline__ int group_xcd(int g, int nb) {
+    const int whole = nb / (8 * kXcdRun) * (8 * kXcdRun);
+    return g < whole ? (g / kXcdRun) & 7 : g & 7;
+}
 constexpr int kSmall = 4;      // groups of at most this many queries are searched one query at a time
 // one-query-per-wave blocks at the front of the search grid (grid-strided; 4,096 measured
 // faster than 16,384 at C4: fewer empty waves to dispatch in iterations without sparse chunks)
 constexpr int kSingleWaves = 4096;
 static_assert(kSingleWaves % 8 == 0, "single_list deals the list to the 8 XCDs in whole eighths of its waves");
 constexpr double kExpand = 1.0;      // search widening, in units of the query's displacement this iteration
+
+// Cost-ordered dispatch of the SE(3) group waves: k_nn_prep files each group under its XCD
+// (the block -> XCD map of the run-dealt order) and a cost class (its wave's duration in the
+// previous search, half-octaves, longest first, unknown first); a group block then takes the
+// i-th item of its XCD's lists in class order, so the long waves start first and the
+// launch's tail is short waves (C2, two group waves per slot: SE(3) NN 8.4 -> 7.6 ms per
+// step; C4 within noise; the R3 searches keep the run order -- ordered, C4's R3 NN was 10 %
+// slower: their short waves gain less than the L2 locality of the run order).
+constexpr int kClsHead = 2 * 8 * 16;  // counts [phase][XCD][class]
+__host__ __device__ inline int cls_cap(int nchunks) { return nchunks * 16 / 8 + 1; }
+__device__ __forceinline__ int cost_class(unsigned t) {
+    if (t == 0u) return 0;
+    const int b = 31 - __clz((int)t);
+    const int b2 = 2 * b + (b >= 1 ? (int)((t >> (b - 1)) & 1u) : 0);
+    return min(15, max(1, 33 - b2));
+}
 
 template <int D>
 __device__ __forceinline__ double dist_f64(const double* a, const double* b) {
@@ -431,6 +451,13 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
             s_base[lane] = base_l;
             v.qcount[c * NL + lane] = dense ? gcnt_l : 0;
         }
+        if ((int)dense & (int)(total > 0) & (int)(lane <= grp) & (int)(phase == PHASE_SE3)) {
+            const int g = c * NL + lane;
+            const int ph = 0;
+            const int row = (ph * 8 + group_xcd(g, v.nchunks * NL)) * 16 + cost_class(v.gcost[g]);
+            const int at = atomicAdd(&v.cls[row], 1);
+            v.cls[kClsHead + (size_t)row * cls_cap(v.nchunks) + at] = g;
+        }
         if (lane == 0) {
             s_single = ((int)!dense & (int)(total > 0)) ? atomicAdd(&v.flag_count[phase == PHASE_SE3 ? 1 : 2], total) : -1;
             if (phase != PHASE_IDLE) {  // work counters: queries / searched queries per phase
@@ -544,259 +571,290 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kWpe))) void
     // node boxes and leaf ranges become scalar loads (blocks of one XCD take runs of
     // consecutive chunks: a pair's target tree stays in that XCD's L2)
     // (kSingleWaves is a multiple of 8: block b and b - kSingleWaves share an XCD)
-    const int gq = __builtin_amdgcn_readfirstlane(
-        xcd_block_runs((int)blockIdx.x - kSingleWaves, (int)gridDim.x - kSingleWaves, kXcdRun));
-    if ((gq >> 4) >= v.nchunks) return;
-    const int c = gq >> 4;
-    const int gi = gq;
-    const int pair = c >> v.chunk_level;
-    const PairDev* P = v.pairs + pair;
-    const int phase = P->phase;
-    if (phase != (D == 12 ? PHASE_SE3 : PHASE_R3)) return;
-    const int cnt_q = __builtin_amdgcn_readfirstlane(v.qcount[gi]);
-    if (cnt_q <= 0) return;
-    const CloudDev cs = v.clouds[P->src], ct = v.clouds[P->tgt];
-    const TreeRef TR = (D == 12) ? v.t12 : v.t3;
-    if (cnt_q <= kSmall) {
-        // a group of a few queries (a chunk's leftovers): each searched by all 64 lanes in
-        // turn (single_one's lane-parallel search) -- a lone query with a wide ball would
-        // otherwise walk the tree one node per step and set the launch's time
-        unsigned n_eval = 0, n_box = 0;
-        for (int q = 0; q < cnt_q; ++q) {
-            const int gxq = __builtin_amdgcn_readfirstlane(cs.off + v.qlist[(size_t)gi * 64 + q]);
-            const int gq = __builtin_amdgcn_readfirstlane(cs.off + TR.perm[gxq]);
-            single_one<D>(v, P, pair, TR, ct, gxq, gq, lane, &n_eval, &n_box);
+    auto group = [&](const int gq) __attribute__((always_inline)) {
+        if ((gq >> 4) >= v.nchunks) return;
+        const int c = gq >> 4;
+        const int gi = gq;
+        const int pair = c >> v.chunk_level;
+        const PairDev* P = v.pairs + pair;
+        const int phase = P->phase;
+        if (phase != (D == 12 ? PHASE_SE3 : PHASE_R3)) return;
+        const int cnt_q = __builtin_amdgcn_readfirstlane(v.qcount[gi]);
+        if (cnt_q <= 0) return;
+        const CloudDev cs = v.clouds[P->src], ct = v.clouds[P->tgt];
+        const TreeRef TR = (D == 12) ? v.t12 : v.t3;
+        if (cnt_q <= kSmall) {
+            // a group of a few queries (a chunk's leftovers): each searched by all 64 lanes in
+            // turn (single_one's lane-parallel search) -- a lone query with a wide ball would
+            // otherwise walk the tree one node per step and set the launch's time
+            unsigned n_eval = 0, n_box = 0;
+            for (int q = 0; q < cnt_q; ++q) {
+                const int gxq = __builtin_amdgcn_readfirstlane(cs.off + v.qlist[(size_t)gi * 64 + q]);
+                const int gq = __builtin_amdgcn_readfirstlane(cs.off + TR.perm[gxq]);
+                single_one<D>(v, P, pair, TR, ct, gxq, gq, lane, &n_eval, &n_box);
+            }
+            if (lane == 0) {
+                unsigned long long* st = v.stats + kStatCols * (gi & 63) + (D == 12 ? 0 : 2);
+                atomicAdd(st, 64ull * n_eval);
+                atomicAdd(st + 1, 64ull * n_box);
+            }
+            return;
         }
-        if (lane == 0) {
+        const bool valid = lane < cnt_q;
+        const int gx = cs.off + v.qlist[(size_t)gi * 64 + (valid ? lane : 0)];  // source tree slot
+        const int g = cs.off + TR.perm[gx];
+        const float mrg = valid ? v.cert[gx].margin : 0.f;
+
+        // query: f64 pose applied to the source element, rounded to f32
+        float q[D];
+        float na;
+        {  // (the f64 query is recomputed at the end rather than held through the traversal)
+            double Tm[12], Q[D];
+            load_T(P, Tm);
+            double m0[D];
+            load_m0<D>(v, TR, gx, g, m0);
+            pose_m0<D>(Tm, m0, Q);
+            double n2 = 0;
+    #pragma unroll
+            for (int r = 0; r < D; ++r) {
+                const double c = (D == 3) ? Q[r] - P->f32_center[r] : Q[r];
+                q[r] = (float)c;
+                n2 += c * c;
+            }
+            na = (float)sqrt(n2) * 1.000001f;
+        }
+        const float nb = (D == 12) ? P->tgt_norm12 : P->tgt_norm3;
+        f32x2 q2[(D + 1) / 2];
+    #pragma unroll
+        for (int r = 0; r < D / 2; ++r) q2[r] = f32x2{q[2 * r], q[2 * r + 1]};
+        const float* tv = TR.tvec + tree_tv_ix<D>(0, ct.off, 0);  // (the cloud's first slot)
+        const size_t ld = v.ld;
+        if constexpr (D == 12) {
+            s_q[lane * 3 + 0] = make_float4(q[0], q[1], q[2], q[3]);
+            s_q[lane * 3 + 1] = make_float4(q[4], q[5], q[6], q[7]);
+            s_q[lane * 3 + 2] = make_float4(q[8], q[9], q[10], q[11]);
+        } else {
+            s_q[lane] = make_float4(q[0], q[1], q[2], 0.f);
+        }
+
+        // pruning threshold for the best / second-best f32 distances a1 <= a2: the certified
+        // radius a1 + 3 err, widened by the margin up to (sqrt(a1) + 2 mrg)^2 but never past a2
+        auto widen = [&](float a1, float a2) __attribute__((always_inline)) {
+            const float e = sqrtf(a1) + 2.f * mrg;
+            const float t = fmaxf(a1, fminf(e * e, a2));
+            return t + 3.f * f32_err(t, na, nb, D);
+        };
+        float d1 = INFINITY, d2 = INFINITY;
+        int i1 = -1;  // target tree position of the best candidate
+        float thr = valid ? INFINITY : -1.f;
+        if (valid) {  // seed the pruning threshold with the previous match
+            const int prev = v.corr_idx[g];
+            if (prev >= 0 && prev < ct.n) {
+                const int tp = TR.pos[ct.off + prev];
+                float s = 0.f;
+    #pragma unroll
+                for (int r = 0; r < D; ++r) {
+                    const float e = q[r] - tv[tree_tv_ix<D>(ld, tp, r)];
+                    s = fmaf(e, e, s);
+                }
+                thr = widen(s, INFINITY);
+            }
+        }
+
+        const float* box_lo = TR.lo + (size_t)P->tgt * TR.nnodes * D;
+        const float* box_hi = TR.hi + (size_t)P->tgt * TR.nnodes * D;
+        const int first_leaf = (1 << TR.L) - 1;
+        float4* tile = s_tile;
+        int stk = 0;  // DFS stack in a VGPR: lane i holds entry i (depth <= 2L+1 < 64)
+        int sp = 1;
+        unsigned n_eval = 0, n_box = 0;  // wave-uniform work counters (roofline accounting)
+    #ifdef SE3ICP_PROF
+        unsigned n_want = 0, n_leafv = 0;
+        unsigned long long c_leaf = 0, c_lload = 0;  // shader-clock cycles in leaf visits / their target loads
+        const unsigned long long c_w0 = __builtin_amdgcn_s_memtime();
+        const unsigned n_valid = (unsigned)__popcll(__ballot(valid));
+        const unsigned long long t_w0 = __builtin_amdgcn_s_memrealtime();
+    #endif
+        while (sp > 0) {
+            const int h = __builtin_amdgcn_readlane(stk, sp - 1);
+            --sp;
+            if (h >= first_leaf) {
+                const int li = h - first_leaf;
+                const int ta = tree_first(ct.n, TR.L, li), tb = tree_first(ct.n, TR.L, li + 1);
+                const int cnt = tb - ta;
+                if (cnt <= 0) continue;
+                // lanes whose own bound admits this leaf (box re-tested: the bounds shrank since the push)
+                unsigned long long W = ~0ull;
+                int w = 64;
+                {
+                    float lbh;
+                    if constexpr (D == 12) lbh = box_lb12_u(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q2);
+                    else lbh = box_lb_u<D>(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q);
+                    W = __ballot(lbh * (1.f - 2e-6f) < thr);
+                    if (W == 0ull) continue;
+                    w = __popcll(W);
+                }
+    #ifdef SE3ICP_PROF
+                n_want += __popcll(W & __ballot(valid));
+                ++n_leafv;
+                const unsigned long long c_l0 = __builtin_amdgcn_s_memtime();
+    #endif
+                __builtin_amdgcn_wave_barrier();
+                if (lane < cnt) {
+                    if constexpr (D == 12) {  // the leaf's rows: one contiguous run, three 16-B loads per lane
+                        const float4* r = reinterpret_cast<const float4*>(tv + (size_t)(ta + lane) * 12);
+                        const float4 a = r[0], b = r[1], c = r[2];
+                        tile[lane * 3] = a;
+                        tile[lane * 3 + 1] = b;
+                        tile[lane * 3 + 2] = c;
+                    } else {
+                        tile[lane] = make_float4(tv[ta + lane], tv[ld + ta + lane], tv[2 * ld + ta + lane], 0.f);
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+    #ifdef SE3ICP_PROF
+                __builtin_amdgcn_s_waitcnt(0);
+                const unsigned long long c_l1 = __builtin_amdgcn_s_memtime();
+                c_lload += c_l1 - c_l0;
+    #endif
+                if (w > kCompact) {
+                    // every lane sweeps every target (broadcast LDS reads)
+                    for (int j = 0; j < cnt; ++j) {
+                        float acc;
+                        if constexpr (D == 12) {
+                            acc = dist12(q2, tile + j * 3);
+                        } else {
+                            const float4 A = tile[j];
+                            float e;
+                            e = q[0] - A.x; acc = e * e;
+                            e = q[1] - A.y; acc = fmaf(e, e, acc);
+                            e = q[2] - A.z; acc = fmaf(e, e, acc);
+                        }
+                        const bool lt = acc < d1;
+                        d2 = __builtin_amdgcn_fmed3f(d1, d2, acc);
+                        d1 = lt ? acc : d1;
+                        i1 = lt ? (ta + j) : i1;  // target tree position
+                    }
+                    n_eval += cnt;
+                } else {
+                    // compacted: LPQ lanes per wanting query (8 for leaves of <= 32 targets, 16
+                    // up to 64), 4 targets per lane, then a top-2 merge over the LPQ lanes and
+                    // into the query's own lane
+                    if ((W >> lane) & 1ull)
+                        s_wl[__builtin_amdgcn_mbcnt_hi((unsigned)(W >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)W, 0u))] = lane;
+                    __builtin_amdgcn_wave_barrier();
+                    constexpr int kL32 = 32 / kTPL, kL64 = 64 / kTPL;  // lanes per query
+                    if (cnt <= 32) compact_sweep<D, kL32>(tile, s_q, s_wl, s_r1, s_r2, s_rb, w, cnt, ta, lane);
+                    else compact_sweep<D, kL64>(tile, s_q, s_wl, s_r1, s_r2, s_rb, w, cnt, ta, lane);
+                    __builtin_amdgcn_wave_barrier();
+                    if ((W >> lane) & 1ull) {
+                        const float r1 = s_r1[lane], r2 = s_r2[lane];
+                        const int rb = s_rb[lane];
+                        d2 = fminf(fmaxf(d1, r1), fminf(d2, r2));
+                        i1 = r1 < d1 ? rb : i1;
+                        d1 = fminf(d1, r1);
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                    {  // 64-lane evaluation slots issued
+                        const int qpi = 64 / (cnt <= 32 ? 32 / kTPL : 64 / kTPL);
+                        n_eval += kTPL * ((w + qpi - 1) / qpi);
+                    }
+                }
+                if ((int)valid & (int)(d1 < INFINITY)) thr = fminf(thr, widen(d1, d2));
+    #ifdef SE3ICP_PROF
+                c_leaf += __builtin_amdgcn_s_memtime() - c_l0;
+    #endif
+                continue;
+            }
+            n_box += 2;
+            const int hl = 2 * h + 1, hr = 2 * h + 2;
+            float ll, lr;
+            if constexpr (D == 12) {
+                ll = box_lb12_u(box_lo + (size_t)hl * D, box_hi + (size_t)hl * D, q2);
+                lr = box_lb12_u(box_lo + (size_t)hr * D, box_hi + (size_t)hr * D, q2);
+            } else {
+                ll = box_lb_u<D>(box_lo + (size_t)hl * D, box_hi + (size_t)hl * D, q);
+                lr = box_lb_u<D>(box_lo + (size_t)hr * D, box_hi + (size_t)hr * D, q);
+            }
+            // the f32 bound is within (D+2) ulps of the exact distance to the (inflated) box
+            const bool vl = __ballot(ll * (1.f - 2e-6f) < thr) != 0ull;
+            const bool vr = __ballot(lr * (1.f - 2e-6f) < thr) != 0ull;
+            const bool left_first = __builtin_amdgcn_readfirstlane(ll <= lr ? 1 : 0) != 0;
+            const int nearh = left_first ? hl : hr, farh = left_first ? hr : hl;
+            const bool vnear = left_first ? vl : vr, vfar = left_first ? vr : vl;
+            if (vfar) { stk = (lane == sp) ? farh : stk; ++sp; }
+            if (vnear) { stk = (lane == sp) ? nearh : stk; ++sp; }
+        }
+
+        if (lane == 0) {  // 64 lanes per evaluation; 64 counter slots against contention
             unsigned long long* st = v.stats + kStatCols * (gi & 63) + (D == 12 ? 0 : 2);
             atomicAdd(st, 64ull * n_eval);
             atomicAdd(st + 1, 64ull * n_box);
+            // the wave's work (box-test steps + leaf sweeps): the chunk's cost for k_nn_order
+    #ifdef SE3ICP_PROF
+            if (D == 12) {
+                atomicAdd(v.stats + kStatCols * (gi & 63) + 8, (unsigned long long)n_want);
+                atomicAdd(v.stats + kStatCols * (gi & 63) + 9, (unsigned long long)n_leafv);
+                const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t_w0;
+                // longest wave, with its leaf visits, box-test steps and valid queries
+                atomicMax(v.stats + 10, (dt << 40) | ((unsigned long long)min(n_box, 0xfffffu) << 20) |
+                                            ((unsigned long long)min(n_leafv, 0x3fffu) << 6) | (n_valid % 64u));
+                atomicAdd(v.stats + kStatCols + 10, dt * dt);                      // (spread)
+                atomicAdd(v.stats + kStatCols * (gi & 63) + 11, (1ull << 44) + dt);  // waves, wave time
+                const int hb = min((int)(dt / 2500ull), 40);
+                atomicAdd(&g_wave_hist[0][hb], 1ull);
+                atomicAdd(&g_wave_hist[1][hb], dt);
+                atomicMin(&g_wave_span[0], t_w0);
+                atomicMax(&g_wave_span[1], t_w0 + dt);
+                atomicAdd(v.stats + kStatCols * (gi & 63) + 12, c_leaf);   // shader cycles in leaf visits,
+                atomicAdd(v.stats + kStatCols * (gi & 63) + 14, c_lload);  // in their target loads,
+                atomicAdd(v.stats + kStatCols * (gi & 63) + 13, __builtin_amdgcn_s_memtime() - c_w0);  // in the wave
+            }
+    #endif
         }
+        // certification (see the header) and the stored distance; the uncertified queries are
+        // re-resolved in f64 by the whole wave, one after the other (few: ~0.4 % of queries)
+        const bool flag = (bool)((int)valid & ((int)(i1 < 0) | (int)!(d2 - d1 > 2.f * f32_err(d2, na, nb, D))));
+        if (valid) nn_finish<D>(v, P, pair, TR, ct, gx, g, flag, d1, d2, i1, thr, na, nb);
+        unsigned long long fm = __ballot((int)flag & (int)(ct.n > 1));
+        const int seed = i1 < 0 ? 0 : TR.perm[ct.off + i1];
+        while (fm) {
+            const int j = __builtin_ctzll(fm);
+            fm &= fm - 1ull;
+            recheck_one<D>(v, P, ct, __shfl(g, j, 64), __shfl(seed, j, 64), lane);
+        }
+    };
+    if (D == 12) {
+        const int bb = (int)blockIdx.x - kSingleWaves, x = bb & 7, i = bb >> 3;
+        const int row0 = x * 16;
+        int acc = 0, k = -1, lo = 0;
+        for (int j = 0; j < 16; ++j) {
+            const int cj = __builtin_amdgcn_readfirstlane(v.cls[row0 + j]);
+            if ((int)(k < 0) & (int)(i < acc + cj)) { k = j; lo = acc; }
+            acc += cj;
+        }
+        // (no group of this XCD timed yet -- a phase's first search: the run order, whose
+        // neighbouring chunks share target leaves in the XCD's L2)
+        const int known = acc - __builtin_amdgcn_readfirstlane(v.cls[row0]);
+        if (known == 0) {
+            const int gs = __builtin_amdgcn_readfirstlane(xcd_block_runs(bb, (int)gridDim.x - kSingleWaves, kXcdRun));
+            const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+            group(gs);
+            const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+            if ((int)(lane == 0) & (int)((gs >> 4) < v.nchunks)) v.gcost[gs] = (unsigned)min(t1 - t0, 0xffffffffull) | 1u;
+            return;
+        }
+        if (k < 0) return;
+        const int gq = __builtin_amdgcn_readfirstlane(v.cls[kClsHead + (size_t)(row0 + k) * cls_cap(v.nchunks) + (i - lo)]);
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        group(gq);
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) v.gcost[gq] = (unsigned)min(t1 - t0, 0xffffffffull) | 1u;
         return;
     }
-    const bool valid = lane < cnt_q;
-    const int gx = cs.off + v.qlist[(size_t)gi * 64 + (valid ? lane : 0)];  // source tree slot
-    const int g = cs.off + TR.perm[gx];
-    const float mrg = valid ? v.cert[gx].margin : 0.f;
-
-    // query: f64 pose applied to the source element, rounded to f32
-    float q[D];
-    float na;
-    {  // (the f64 query is recomputed at the end rather than held through the traversal)
-        double Tm[12], Q[D];
-        load_T(P, Tm);
-        double m0[D];
-        load_m0<D>(v, TR, gx, g, m0);
-        pose_m0<D>(Tm, m0, Q);
-        double n2 = 0;
-#pragma unroll
-        for (int r = 0; r < D; ++r) {
-            const double c = (D == 3) ? Q[r] - P->f32_center[r] : Q[r];
-            q[r] = (float)c;
-            n2 += c * c;
-        }
-        na = (float)sqrt(n2) * 1.000001f;
-    }
-    const float nb = (D == 12) ? P->tgt_norm12 : P->tgt_norm3;
-    f32x2 q2[(D + 1) / 2];
-#pragma unroll
-    for (int r = 0; r < D / 2; ++r) q2[r] = f32x2{q[2 * r], q[2 * r + 1]};
-    const float* tv = TR.tvec + tree_tv_ix<D>(0, ct.off, 0);  // (the cloud's first slot)
-    const size_t ld = v.ld;
-    if constexpr (D == 12) {
-        s_q[lane * 3 + 0] = make_float4(q[0], q[1], q[2], q[3]);
-        s_q[lane * 3 + 1] = make_float4(q[4], q[5], q[6], q[7]);
-        s_q[lane * 3 + 2] = make_float4(q[8], q[9], q[10], q[11]);
-    } else {
-        s_q[lane] = make_float4(q[0], q[1], q[2], 0.f);
-    }
-
-    // pruning threshold for the best / second-best f32 distances a1 <= a2: the certified
-    // radius a1 + 3 err, widened by the margin up to (sqrt(a1) + 2 mrg)^2 but never past a2
-    auto widen = [&](float a1, float a2) __attribute__((always_inline)) {
-        const float e = sqrtf(a1) + 2.f * mrg;
-        const float t = fmaxf(a1, fminf(e * e, a2));
-        return t + 3.f * f32_err(t, na, nb, D);
-    };
-    float d1 = INFINITY, d2 = INFINITY;
-    int i1 = -1;  // target tree position of the best candidate
-    float thr = valid ? INFINITY : -1.f;
-    if (valid) {  // seed the pruning threshold with the previous match
-        const int prev = v.corr_idx[g];
-        if (prev >= 0 && prev < ct.n) {
-            const int tp = TR.pos[ct.off + prev];
-            float s = 0.f;
-#pragma unroll
-            for (int r = 0; r < D; ++r) {
-                const float e = q[r] - tv[tree_tv_ix<D>(ld, tp, r)];
-                s = fmaf(e, e, s);
-            }
-            thr = widen(s, INFINITY);
-        }
-    }
-
-    const float* box_lo = TR.lo + (size_t)P->tgt * TR.nnodes * D;
-    const float* box_hi = TR.hi + (size_t)P->tgt * TR.nnodes * D;
-    const int first_leaf = (1 << TR.L) - 1;
-    float4* tile = s_tile;
-    int stk = 0;  // DFS stack in a VGPR: lane i holds entry i (depth <= 2L+1 < 64)
-    int sp = 1;
-    unsigned n_eval = 0, n_box = 0;  // wave-uniform work counters (roofline accounting)
-#ifdef SE3ICP_PROF
-    unsigned n_want = 0, n_leafv = 0;
-    unsigned long long c_leaf = 0, c_lload = 0;  // shader-clock cycles in leaf visits / their target loads
-    const unsigned long long c_w0 = __builtin_amdgcn_s_memtime();
-    const unsigned n_valid = (unsigned)__popcll(__ballot(valid));
-    const unsigned long long t_w0 = __builtin_amdgcn_s_memrealtime();
-#endif
-    while (sp > 0) {
-        const int h = __builtin_amdgcn_readlane(stk, sp - 1);
-        --sp;
-        if (h >= first_leaf) {
-            const int li = h - first_leaf;
-            const int ta = tree_first(ct.n, TR.L, li), tb = tree_first(ct.n, TR.L, li + 1);
-            const int cnt = tb - ta;
-            if (cnt <= 0) continue;
-            // lanes whose own bound admits this leaf (box re-tested: the bounds shrank since the push)
-            unsigned long long W = ~0ull;
-            int w = 64;
-            {
-                float lbh;
-                if constexpr (D == 12) lbh = box_lb12_u(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q2);
-                else lbh = box_lb_u<D>(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q);
-                W = __ballot(lbh * (1.f - 2e-6f) < thr);
-                if (W == 0ull) continue;
-                w = __popcll(W);
-            }
-#ifdef SE3ICP_PROF
-            n_want += __popcll(W & __ballot(valid));
-            ++n_leafv;
-            const unsigned long long c_l0 = __builtin_amdgcn_s_memtime();
-#endif
-            __builtin_amdgcn_wave_barrier();
-            if (lane < cnt) {
-                if constexpr (D == 12) {  // the leaf's rows: one contiguous run, three 16-B loads per lane
-                    const float4* r = reinterpret_cast<const float4*>(tv + (size_t)(ta + lane) * 12);
-                    const float4 a = r[0], b = r[1], c = r[2];
-                    tile[lane * 3] = a;
-                    tile[lane * 3 + 1] = b;
-                    tile[lane * 3 + 2] = c;
-                } else {
-                    tile[lane] = make_float4(tv[ta + lane], tv[ld + ta + lane], tv[2 * ld + ta + lane], 0.f);
-                }
-            }
-            __builtin_amdgcn_wave_barrier();
-#ifdef SE3ICP_PROF
-            __builtin_amdgcn_s_waitcnt(0);
-            const unsigned long long c_l1 = __builtin_amdgcn_s_memtime();
-            c_lload += c_l1 - c_l0;
-#endif
-            if (w > kCompact) {
-                // every lane sweeps every target (broadcast LDS reads)
-                for (int j = 0; j < cnt; ++j) {
-                    float acc;
-                    if constexpr (D == 12) {
-                        acc = dist12(q2, tile + j * 3);
-                    } else {
-                        const float4 A = tile[j];
-                        float e;
-                        e = q[0] - A.x; acc = e * e;
-                        e = q[1] - A.y; acc = fmaf(e, e, acc);
-                        e = q[2] - A.z; acc = fmaf(e, e, acc);
-                    }
-                    const bool lt = acc < d1;
-                    d2 = __builtin_amdgcn_fmed3f(d1, d2, acc);
-                    d1 = lt ? acc : d1;
-                    i1 = lt ? (ta + j) : i1;  // target tree position
-                }
-                n_eval += cnt;
-            } else {
-                // compacted: LPQ lanes per wanting query (8 for leaves of <= 32 targets, 16
-                // up to 64), 4 targets per lane, then a top-2 merge over the LPQ lanes and
-                // into the query's own lane
-                if ((W >> lane) & 1ull)
-                    s_wl[__builtin_amdgcn_mbcnt_hi((unsigned)(W >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)W, 0u))] = lane;
-                __builtin_amdgcn_wave_barrier();
-                constexpr int kL32 = 32 / kTPL, kL64 = 64 / kTPL;  // lanes per query
-                if (cnt <= 32) compact_sweep<D, kL32>(tile, s_q, s_wl, s_r1, s_r2, s_rb, w, cnt, ta, lane);
-                else compact_sweep<D, kL64>(tile, s_q, s_wl, s_r1, s_r2, s_rb, w, cnt, ta, lane);
-                __builtin_amdgcn_wave_barrier();
-                if ((W >> lane) & 1ull) {
-                    const float r1 = s_r1[lane], r2 = s_r2[lane];
-                    const int rb = s_rb[lane];
-                    d2 = fminf(fmaxf(d1, r1), fminf(d2, r2));
-                    i1 = r1 < d1 ? rb : i1;
-                    d1 = fminf(d1, r1);
-                }
-                __builtin_amdgcn_wave_barrier();
-                {  // 64-lane evaluation slots issued
-                    const int qpi = 64 / (cnt <= 32 ? 32 / kTPL : 64 / kTPL);
-                    n_eval += kTPL * ((w + qpi - 1) / qpi);
-                }
-            }
-            if ((int)valid & (int)(d1 < INFINITY)) thr = fminf(thr, widen(d1, d2));
-#ifdef SE3ICP_PROF
-            c_leaf += __builtin_amdgcn_s_memtime() - c_l0;
-#endif
-            continue;
-        }
-        n_box += 2;
-        const int hl = 2 * h + 1, hr = 2 * h + 2;
-        float ll, lr;
-        if constexpr (D == 12) {
-            ll = box_lb12_u(box_lo + (size_t)hl * D, box_hi + (size_t)hl * D, q2);
-            lr = box_lb12_u(box_lo + (size_t)hr * D, box_hi + (size_t)hr * D, q2);
-        } else {
-            ll = box_lb_u<D>(box_lo + (size_t)hl * D, box_hi + (size_t)hl * D, q);
-            lr = box_lb_u<D>(box_lo + (size_t)hr * D, box_hi + (size_t)hr * D, q);
-        }
-        // the f32 bound is within (D+2) ulps of the exact distance to the (inflated) box
-        const bool vl = __ballot(ll * (1.f - 2e-6f) < thr) != 0ull;
-        const bool vr = __ballot(lr * (1.f - 2e-6f) < thr) != 0ull;
-        const bool left_first = __builtin_amdgcn_readfirstlane(ll <= lr ? 1 : 0) != 0;
-        const int nearh = left_first ? hl : hr, farh = left_first ? hr : hl;
-        const bool vnear = left_first ? vl : vr, vfar = left_first ? vr : vl;
-        if (vfar) { stk = (lane == sp) ? farh : stk; ++sp; }
-        if (vnear) { stk = (lane == sp) ? nearh : stk; ++sp; }
-    }
-
-    if (lane == 0) {  // 64 lanes per evaluation; 64 counter slots against contention
-        unsigned long long* st = v.stats + kStatCols * (gi & 63) + (D == 12 ? 0 : 2);
-        atomicAdd(st, 64ull * n_eval);
-        atomicAdd(st + 1, 64ull * n_box);
-        // the wave's work (box-test steps + leaf sweeps): the chunk's cost for k_nn_order
-#ifdef SE3ICP_PROF
-        if (D == 12) {
-            atomicAdd(v.stats + kStatCols * (gi & 63) + 8, (unsigned long long)n_want);
-            atomicAdd(v.stats + kStatCols * (gi & 63) + 9, (unsigned long long)n_leafv);
-            const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t_w0;
-            // longest wave, with its leaf visits, box-test steps and valid queries
-            atomicMax(v.stats + 10, (dt << 40) | ((unsigned long long)min(n_box, 0xfffffu) << 20) |
-                                        ((unsigned long long)min(n_leafv, 0x3fffu) << 6) | (n_valid % 64u));
-            atomicAdd(v.stats + kStatCols + 10, dt * dt);                      // (spread)
-            atomicAdd(v.stats + kStatCols * (gi & 63) + 11, (1ull << 44) + dt);  // waves, wave time
-            const int hb = min((int)(dt / 2500ull), 40);
-            atomicAdd(&g_wave_hist[0][hb], 1ull);
-            atomicAdd(&g_wave_hist[1][hb], dt);
-            atomicMin(&g_wave_span[0], t_w0);
-            atomicMax(&g_wave_span[1], t_w0 + dt);
-            atomicAdd(v.stats + kStatCols * (gi & 63) + 12, c_leaf);   // shader cycles in leaf visits,
-            atomicAdd(v.stats + kStatCols * (gi & 63) + 14, c_lload);  // in their target loads,
-            atomicAdd(v.stats + kStatCols * (gi & 63) + 13, __builtin_amdgcn_s_memtime() - c_w0);  // in the wave
-        }
-#endif
-    }
-    // certification (see the header) and the stored distance; the uncertified queries are
-    // re-resolved in f64 by the whole wave, one after the other (few: ~0.4 % of queries)
-    const bool flag = (bool)((int)valid & ((int)(i1 < 0) | (int)!(d2 - d1 > 2.f * f32_err(d2, na, nb, D))));
-    if (valid) nn_finish<D>(v, P, pair, TR, ct, gx, g, flag, d1, d2, i1, thr, na, nb);
-    unsigned long long fm = __ballot((int)flag & (int)(ct.n > 1));
-    const int seed = i1 < 0 ? 0 : TR.perm[ct.off + i1];
-    while (fm) {
-        const int j = __builtin_ctzll(fm);
-        fm &= fm - 1ull;
-        recheck_one<D>(v, P, ct, __shfl(g, j, 64), __shfl(seed, j, 64), lane);
-    }
+    const int gq = __builtin_amdgcn_readfirstlane(
+        xcd_block_runs((int)blockIdx.x - kSingleWaves, (int)gridDim.x - kSingleWaves, kXcdRun));
+    group(gq);
 }
 
 // ------------------------------------------------------------------ one wavefront per query
@@ -998,6 +1056,7 @@ double nn_prep_span() {
     return h[1] > h[0] ? (h[1] - h[0]) / 100.0 : 0.0;
 }
 #endif
+size_t nn_cls_words(int nchunks) { return (size_t)kClsHead + (size_t)kClsHead * cls_cap(nchunks); }
 void launch_nn_prep(const View& v, int32_t* publish, hipStream_t s) {
     hipLaunchKernelGGL(k_nn_prep, dim3(v.nchunks), dim3(kChunkQ), 0, s, v, publish);
 }

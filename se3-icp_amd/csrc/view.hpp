@@ -102,6 +102,8 @@ struct View {
     // the PHASE's source tree (12-D in the SE(3) phase, 3-D in the R3 phase: a certificate of
     // the other phase is void anyway), so k_nn_prep reads them in tree order, coalesced
     NNCert* cert;
+    uint32_t* gcost;      // [nchunks * 16] duration of each group's last search wave (100 MHz ticks; 0: none)
+    int32_t* cls;         // cost-ordered dispatch: [2 phases][8 XCDs][16 classes] counts, then the lists
 };
 
 // ---- k_setup.hip
@@ -157,6 +159,8 @@ void nn_wave_report(int it);  // SE(3) group-wave durations since the last call
 #endif
 // the search of a phase (D = 12 or 3): one grid, single-query waves first, then the groups
 void launch_nn(const View& v, int D, hipStream_t s);
+// words of View::cls for nchunks chunks (counts + per-XCD class lists)
+size_t nn_cls_words(int nchunks);
 void launch_trim(const View& v, hipStream_t s);
 // reduce + (k_reduce_final) per-pair solve and loop state machine; next_phase[p] receives
 // pair p's phase in the next iteration (PHASE_IDLE: finished)
