@@ -36,6 +36,8 @@ namespace {
 // k_tree_local phase ends over all workgroups (100 MHz clock): [D == 12][0] start (min),
 // [1..4] the latest end of load / levels / final / boxes
 __device__ unsigned long long g_tree_prof[2][5] = {{~0ull, 0, 0, 0, 0}, {~0ull, 0, 0, 0, 0}};
+// k_tree_local per level below G: summed workgroup time of levels 0..7, [8] workgroups
+__device__ unsigned long long g_tree_lev[2][9];
 #endif
 
 __device__ __forceinline__ uint32_t ord_bits(float f) {
@@ -845,8 +847,18 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
 #ifdef SE3ICP_PROF
     tq[1] = __builtin_amdgcn_s_memrealtime();
 #endif
+#ifdef SE3ICP_PROF
+    unsigned long long t_lev = tq[1];
+#endif
     for (int l = G; l < t.L; ++l) {
         const int r = l - G;
+#ifdef SE3ICP_PROF
+        if ((int)(r > 0) & (int)(tid == 0) & (int)(r <= 8)) {
+            const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+            atomicAdd(&g_tree_lev[D == 12][r - 1], now - t_lev);
+            t_lev = now;
+        }
+#endif
         const int nsub = 1 << r;  // sub-nodes of this level under the WG's node (<= 128: see the host)
         // split dimension of each sub-node: widest extent of the box of every
         // kSplitSample-th point (the sample of the global levels), a wave per sub-node
@@ -1074,6 +1086,11 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
     }
 #ifdef SE3ICP_PROF
     tq[2] = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) {
+        const int last = t.L - G - 1;
+        if (last >= 0 && last < 8) atomicAdd(&g_tree_lev[D == 12][last], tq[2] - t_lev);
+        atomicAdd(&g_tree_lev[D == 12][8], 1ull);
+    }
 #endif
     // the final order, a wave per leaf (<= 64 consecutive tree positions): permutation,
     // inverse, f32 and f64 vectors (the layouts k_tree_finish writes) and the leaf's box
@@ -1399,6 +1416,18 @@ void tree_prof_report() {
     unsigned long long z[2][5];
     for (int k = 0; k < 2; ++k) { z[k][0] = ~0ull; for (int j = 1; j < 5; ++j) z[k][j] = 0; }
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tree_prof), z, sizeof(z));
+    unsigned long long lv[2][9];
+    if (hipMemcpyFromSymbol(lv, HIP_SYMBOL(g_tree_lev), sizeof(lv)) == hipSuccess) {
+        for (int k = 0; k < 2; ++k) {
+            if (!lv[k][8]) continue;
+            std::fprintf(stderr, "[prof] k_tree_local<%d> per workgroup and level below G (us):", k ? 12 : 3);
+            for (int j = 0; j < 8; ++j)
+                if (lv[k][j]) std::fprintf(stderr, " %.1f", lv[k][j] / 100.0 / lv[k][8]);
+            std::fprintf(stderr, "\n");
+        }
+        const unsigned long long zl[2][9] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tree_lev), zl, sizeof(zl));
+    }
 #endif
 }
 
