@@ -855,6 +855,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
             const double mean = std::fmod(sum[11], 17592186044416.0) / nw;  // 100 MHz ticks
             const double sq = (double)stats[kStatCols + 10] / nw;
             nn_prof_report();
+            trim_prof_report();
             std::fprintf(stderr, "[prof] nn12: leaf visits %.0f; %.0f group waves, %.1f us each on average (sd %.1f, "
                          "longest %.1f us; 100 MHz clock)\n",
                          sum[9], nw, mean / 100.0, std::sqrt(std::max(0.0, sq - mean * mean)) / 100.0,

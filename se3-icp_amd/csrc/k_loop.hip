@@ -17,6 +17,7 @@
 #include <cfloat>
 #include <climits>
 #include <cmath>
+#include <cstdio>
 
 #include "devmath.hpp"
 #include "loopdev.hpp"
@@ -178,6 +179,15 @@ __global__ __launch_bounds__(256) void k_trim_window(View v) {
             if (base + e < (unsigned)kTrimList) cand[base + e] = s_loc[e];
 }
 
+#ifdef SE3ICP_PROF
+// k_trim phases summed over launches and pairs (100 MHz ticks): [0] whole block, [1] the
+// window rank / first digit, [2] compaction passes, [3] global digit-count passes, [4] the
+// LDS digit passes, [5] blocks, [6] blocks on the radix path
+__device__ unsigned long long g_trim_prof[8];
+#define TRIM_T(x) const unsigned long long x = __builtin_amdgcn_s_memrealtime()
+#else
+#define TRIM_T(x) do {} while (0)
+#endif
 // One 1024-thread block per trimming pair (see above).
 __global__ __launch_bounds__(1024) void k_trim(View v) {
     __shared__ unsigned hist[4096];
@@ -196,6 +206,10 @@ __global__ __launch_bounds__(1024) void k_trim(View v) {
         return;
     }
     const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    TRIM_T(tp0);
+#ifdef SE3ICP_PROF
+    unsigned long long c_comp = 0, c_gcount = 0, c_lds = 0;
+#endif
     const unsigned* dist = reinterpret_cast<const unsigned*>(v.corr_dist) + cs.off;
     constexpr int U = 8;  // independent loads in flight per thread
     uint64_t* win = v.trim_key + v.npairs + pair;
@@ -250,6 +264,14 @@ __global__ __launch_bounds__(1024) void k_trim(View v) {
             __syncthreads();
             if (threadIdx.x < 2) ctr[threadIdx.x] = 0u;
             for (int i = threadIdx.x; i < 4096; i += blockDim.x) gh[i] = 0u;
+#ifdef SE3ICP_PROF
+            if (threadIdx.x == 0) {
+                TRIM_T(tpe);
+                atomicAdd(&g_trim_prof[0], tpe - tp0);
+                atomicAdd(&g_trim_prof[1], tpe - tp0);
+                atomicAdd(&g_trim_prof[5], 1ull);
+            }
+#endif
             return;
         }
         __syncthreads();
@@ -283,8 +305,10 @@ __global__ __launch_bounds__(1024) void k_trim(View v) {
         pos = 12;
         __syncthreads();
     }
+    TRIM_T(tp1);
     while (pos < 64) {
         const int w = pos == 0 ? 12 : min(8, 64 - pos);
+        TRIM_T(tl0);
         const int sh = 64 - pos - w;
         const unsigned dmask = (1u << w) - 1u;
         if (!in_lds && sel_count <= (unsigned)kTrimList) {
@@ -314,7 +338,14 @@ __global__ __launch_bounds__(1024) void k_trim(View v) {
             __syncthreads();
             cnt = s_cnt;
             in_lds = true;
+#ifdef SE3ICP_PROF
+            c_comp += __builtin_amdgcn_s_memrealtime() - tl0;
+#endif
         }
+        TRIM_T(tl1);
+#ifdef SE3ICP_PROF
+        const bool lds_pass = in_lds;
+#endif
         for (int i = threadIdx.x; i <= (int)dmask; i += blockDim.x) hist[i] = 0;
         __syncthreads();
         if (in_lds) {
@@ -351,6 +382,10 @@ __global__ __launch_bounds__(1024) void k_trim(View v) {
         mask |= (unsigned long long)dmask << sh;
         pos += w;
         __syncthreads();
+#ifdef SE3ICP_PROF
+        if (lds_pass) c_lds += __builtin_amdgcn_s_memrealtime() - tl1;
+        else c_gcount += __builtin_amdgcn_s_memrealtime() - tl1;
+#endif
         if ((int)in_lds & (int)(sel_count == 1u) & (int)(pos < 64)) {
             // one key left with this prefix (the distance bits usually settle it): it is the cut
             for (unsigned e = threadIdx.x; e < cnt; e += blockDim.x)
@@ -363,6 +398,16 @@ __global__ __launch_bounds__(1024) void k_trim(View v) {
     if (threadIdx.x == 0) {
         v.trim_key[pair] = prefix;
         *win = (prefix & 0xffffffff00000000ull) | __float_as_uint(wv);
+#ifdef SE3ICP_PROF
+        TRIM_T(tpe);
+        atomicAdd(&g_trim_prof[0], tpe - tp0);
+        atomicAdd(&g_trim_prof[1], tp1 - tp0);
+        atomicAdd(&g_trim_prof[2], c_comp);
+        atomicAdd(&g_trim_prof[3], c_gcount);
+        atomicAdd(&g_trim_prof[4], c_lds);
+        atomicAdd(&g_trim_prof[5], 1ull);
+        atomicAdd(&g_trim_prof[6], 1ull);
+#endif
     }
 }
 
@@ -637,6 +682,18 @@ __global__ __launch_bounds__(kFinThreads) void k_reduce_final(View v, const int3
 
 }  // namespace
 
+void trim_prof_report() {
+#ifdef SE3ICP_PROF
+    unsigned long long h[8];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_trim_prof), sizeof(h)) != hipSuccess || !h[5]) return;
+    std::fprintf(stderr, "[prof] k_trim per block (us): whole %.2f, window rank / first digit %.2f; radix-path blocks "
+                 "%llu of %llu: compaction %.2f, global counts %.2f, LDS digits %.2f (per radix block)\n",
+                 h[0] / 100.0 / h[5], h[1] / 100.0 / h[5], h[6], h[5], h[6] ? h[2] / 100.0 / h[6] : 0.0,
+                 h[6] ? h[3] / 100.0 / h[6] : 0.0, h[6] ? h[4] / 100.0 / h[6] : 0.0);
+    const unsigned long long z[8] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_trim_prof), z, sizeof(z));
+#endif
+}
 void launch_trim(const View& v, hipStream_t s) {
     hipLaunchKernelGGL(k_trim_window, dim3(v.npairs * kTrimBlocks), dim3(256), 0, s, v);
     hipLaunchKernelGGL(k_trim, dim3(v.npairs), dim3(1024), 0, s, v);

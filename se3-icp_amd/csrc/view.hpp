@@ -153,6 +153,7 @@ void launch_knn_big(const View& v, int write_knn, int k_min, const int32_t* qlis
 // publish: host slot that receives every pair's phase at the start of the launch (or null)
 void launch_nn_prep(const View& v, int32_t* publish, hipStream_t s);
 void nn_prof_report();  // (SE3ICP_PROF builds: k_nn_prep block phases, then reset)
+void trim_prof_report();  // (SE3ICP_PROF builds: k_trim phases, then reset)
 #ifdef SE3ICP_PROF
 double nn_prep_span();        // span of the last k_nn_prep launch (us)
 void nn_wave_report(int it);  // SE(3) group-wave durations since the last call
