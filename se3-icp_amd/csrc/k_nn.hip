@@ -190,6 +190,9 @@ __device__ __forceinline__ void compact_sweep(const float4* tile, const float4* 
 // 256 within 1 % of each other with one-wave group blocks)
 constexpr int kDense = 256;
 constexpr int kWpe = 4;        // waves per SIMD of k_nn_search (its natural 128 VGPRs; 5 measured +8 %)
+// the 3-D search at 6 waves per SIMD (79 VGPRs, no scratch): same-box A/B x2, C2 (72 R3
+// iterations) 25,957 -> 26,257 iter/s, C4 within noise; 8 (64 VGPRs, 52 B of scratch) +0.8 %
+constexpr int kWpe3 = 6;
 constexpr int kXcdRun = 256;   // group blocks per XCD run (16 chunks; runs dealt round-robin over the XCDs:
                                // neighbouring chunks share target leaves in one L2, SE(3) NN -3 %)
 __device__ __forceinline__ int group_xcd(int g, int nb) {
@@ -553,7 +556,7 @@ __device__ __forceinline__ void single_list(const View& v, int bw);
 // two grids on two streams, joined by events: two extra launches and two cross-stream
 // waits per iteration.)
 template <int D>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kWpe))) void k_nn_search(View v) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kWpe : kWpe3))) void k_nn_search(View v) {
     if (blockIdx.x < (unsigned)kSingleWaves) {
         single_list<D>(v, (int)blockIdx.x);
         return;
