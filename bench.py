@@ -4,11 +4,13 @@
 Default workload (BASELINE.json configs[3]): se3_gicp with the KITTI
 driver's parameters (examples/benchmark_kitti.cpp:133-148: overlap 0.7, mse 1e-7,
 mse_switch 5e-7, max_se3 10, k = 90) on synthetic 64-beam LiDAR scans of ~120k points
-(the KITTI data are not available offline).  64 consecutive-scan pairs are sharded over
-the GPUs: 8 pairs per GPU (weak scaling), each rank registering its own 8 pairs in
-lockstep with no data-path collective; RCCL (torch.distributed "nccl") only gathers the
-per-pair results.  --workload C2 / C3 / C5 runs the other BASELINE configs (secondary
-lines; the headline is C4).
+(the KITTI data are not available offline).  The batch is BASELINE's: 64 consecutive-scan
+pairs (examples/benchmark_kitti.cpp:120-197), a fixed global batch sharded over the GPUs
+(strong scaling: N=1 registers all 64 on one GPU, N=8 eight per GPU), each rank
+registering its block in lockstep with no data-path collective; RCCL (torch.distributed
+"nccl") only gathers the per-pair results.  --workload C2 / C3 / C5 runs the other
+BASELINE configs (C3 32 pairs, C5 256 pairs, C2 8 cases; secondary lines, the headline is
+C4).  --pairs-per-gpu P switches to weak scaling (P pairs per rank).
 
 A step = registering the rank's batch end to end (TOLDI/kNN/normals setup + the ICP loop),
 clouds already resident in HBM.  value = ICP iterations (all ranks) / step wall time.
@@ -39,12 +41,12 @@ METRIC = "ICP iterations/sec + pairs/sec, ~120k-pt KITTI clouds, 1/2/4/8 GPU"
 
 # BASELINE.json configs: method, pairs per GPU, reference parameters
 WORKLOADS = {
-    "C4": dict(method="se3_gicp", ppg=8, run="se3", variant="gicp",
+    "C4": dict(method="se3_gicp", ppg=8, batch=64, run="se3", variant="gicp",
                params=dict(estimated_overlap=0.7, max_num_se3_iterations=10, mse=1e-7, mse_switch_error=5e-7,
                            number_of_nn_for_LRF=90),
                desc="C4: se3_gicp, KITTI driver params (overlap 0.7, mse 1e-7, switch 5e-7, max_se3 10, k=90)",
                data="synthetic (64-beam LiDAR ray-cast street scenes, seed 4; KITTI not available offline)"),
-    "C2": dict(method="se3_pt2pt", ppg=8, run="se3", variant="pt2pt",
+    "C2": dict(method="se3_pt2pt", ppg=8, batch=8, run="se3", variant="pt2pt",
                params=dict(estimated_overlap=1.0, max_num_se3_iterations=10, mse=1e-5, mse_switch_error=5e-5,
                            number_of_nn_for_LRF=90),
                desc="C2: se3_pt2pt on the reference's synthetic bunny problems (benchmark_synthetic.cpp:91-160 with "
@@ -53,16 +55,16 @@ WORKLOADS = {
                     "'synthetic easy_data, ~40k pts'; the driver itself samples 0.02 and has the 'moderate' ranges "
                     "active, B_SYN:111-112), 'easy' ranges (B_SYN:107-108), B_SYN:356-363 params, 8 cases per GPU",
                data="stanford_bunny.ply (tests/golden) -> se3icp_synthetic_reference_device, generated on the GPU"),
-    "C3": dict(method="se3_pt2pl", ppg=32, run="se3", variant="pt2pl",
+    "C3": dict(method="se3_pt2pl", ppg=32, batch=32, run="se3", variant="pt2pl",
                params=dict(estimated_overlap=0.75, max_num_se3_iterations=10, mse_switch_error=5e-5,
                            number_of_nn_for_LRF=90),
                desc="C3: se3_pt2pl, lounge driver params (overlap 0.75, switch 5e-5, max_se3 10, k=90), "
-                    "32 consecutive RGB-D pairs per GPU",
+                    "a batch of 32 consecutive RGB-D pairs",
                data="synthetic RGB-D room sequence (depth 0.4-4 m, stride 4, ~16k pts, seed 3; lounge not offline)"),
-    "C5": dict(method="se3_gicp_with_cf", ppg=32, run="cf", variant="gicp",
+    "C5": dict(method="se3_gicp_with_cf", ppg=32, batch=256, run="cf", variant="gicp",
                params=dict(estimated_overlap=0.75, max_num_se3_iterations=10, mse_switch_error=5e-5,
                            number_of_nn_for_LRF=90),
-               desc="C5: se3_gicp_with_cf, lounge driver params, 256 pairs over 8 GPUs (32 per GPU)",
+               desc="C5: se3_gicp_with_cf, lounge driver params, a batch of 256 pairs (32 per GPU at N=8)",
                data="synthetic RGB-D room sequence (depth 0.4-4 m, stride 4, ~16k pts, seed 5; lounge not offline)"),
 }
 
@@ -151,11 +153,16 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="C4")
-    ap.add_argument("--pairs-per-gpu", type=int, default=0, help="0: the workload's default (C4: 8)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="pairs of the whole job, sharded over the ranks (strong scaling); 0: the workload's "
+                         "BASELINE batch (C4 64, C5 256, C3 32, C2 8)")
+    ap.add_argument("--pairs-per-gpu", type=int, default=0,
+                    help="weak scaling instead: this many pairs per rank (the global batch grows with N)")
     ap.add_argument("--n-az", type=int, default=1975, help="C4 azimuth steps per revolution (~120k pts at 1975)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="collective backend for N > 1 (gloo: ranks may share one GPU, as in the tests)")
+    ap.add_argument("--pair-cache", default="", help="directory for the generated pairs (reused by later runs)")
     ap.add_argument("--dump-poses", default="", help="rank 0 writes the gathered per-pair poses (.npy)")
     ap.add_argument("--c2-setup", choices=sorted(C2_SETUPS), default="easy",
                     help="C2 transform ranges: BASELINE's easy_data (B_SYN:106-108) or the driver's active moderate ones")
@@ -163,7 +170,7 @@ def main():
                     help="C2 cloud: RandomDownSample(0.2) of the 208,353-vertex bunny (41,670 pts, round 3 on) or "
                          "BASELINE.md's 34,834 unique vertices (rounds 1-2); the bench line's workload is then 'C2u'")
     ap.add_argument("--secondary", choices=["auto", "off"], default="auto",
-                    help="C4 at N=1: also time the whole 64-pair batch on this GPU (strong-scaling anchor)")
+                    help="C4 at N=1: also time one 8-pair shard on this GPU (the per-GPU work of the 8-GPU job)")
     args = ap.parse_args()
     W = dict(WORKLOADS[args.workload])
     if args.workload == "C2" and args.c2_setup != "easy":
@@ -202,10 +209,23 @@ def main():
             dist.init_process_group("gloo")
             xdev = torch.device("cpu")
 
-    P = args.pairs_per_gpu or W["ppg"]
+    # strong scaling over the workload's fixed batch (weak with --pairs-per-gpu)
+    scaling, global_batch, first, count = sharding.plan(world, rank, W["batch"], args.global_batch,
+                                                        args.pairs_per_gpu)
     t0 = time.time()
-    first, count = sharding.shard(world * P, world, rank)  # weak scaling: P pairs per rank
-    pairs, gts = make_pairs(args.workload, world * P, first, count, args.n_az, args.c2_setup, devi, args.c2_cloud)
+    cache = (os.path.join(args.pair_cache, f"{args.workload}_{args.c2_cloud}_{args.c2_setup}_{args.n_az}_"
+                          f"{global_batch}_{first}_{count}.npz") if args.pair_cache else "")
+    if cache and os.path.exists(cache):  # (A/B runs on one box: the same synthetic pairs, generated once)
+        z = np.load(cache)
+        pairs = [(z[f"s{i}"], z[f"t{i}"]) for i in range(count)]
+        gts = [z["gts"][i] for i in range(count)]
+    else:
+        pairs, gts = make_pairs(args.workload, global_batch, first, count, args.n_az, args.c2_setup, devi,
+                                args.c2_cloud)
+        if cache:
+            os.makedirs(args.pair_cache, exist_ok=True)
+            np.savez(cache, gts=np.stack(gts), **{f"s{i}": p[0] for i, p in enumerate(pairs)},
+                     **{f"t{i}": p[1] for i, p in enumerate(pairs)})
     npts = [p[0].shape[0] for p in pairs] + [p[1].shape[0] for p in pairs]
     log(f"rank {rank}: {args.workload} generated {count} pairs in {time.time() - t0:.1f}s, points/cloud "
         f"min {min(npts)} mean {np.mean(npts):.0f} max {max(npts)}")
@@ -274,7 +294,7 @@ def main():
     if rank == 0:
         if args.dump_poses:
             np.save(args.dump_poses, gathered.T)
-        total_pairs = world * P * args.steps
+        total_pairs = global_batch * args.steps
         value = iters_all / elapsed
         ms_per_step = 1000.0 * elapsed / args.steps
         rot_errs = [rot_err_deg(r.T, g) for r, g in zip(last, gts)]
@@ -306,15 +326,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,   # BASELINE.md publishes no number for this metric
             "dtype": "f32 sweep + f64 certify/solve",
             "data": W["data"],
             "config": {
                 "workload": W["desc"],
                 "method": W["method"],
-                "pairs_per_gpu": P,
-                "global_batch_pairs": world * P,
+                "pairs_per_gpu": (global_batch // world if global_batch % world == 0
+                                  else [sharding.shard(global_batch, world, r)[1] for r in range(world)]),
+                "global_batch_pairs": global_batch,
                 "points_per_cloud_mean": int(np.mean(npts)),
                 "parallelism": f"pair-sharded dp{world} ({'RCCL' if args.backend == 'nccl' else 'gloo'} "
                                f"result gather only)",
@@ -335,8 +356,8 @@ def main():
             "roofline_reduce": roof_red,
             "cpu_baseline": None,
         }
-        if args.workload == "C4" and world == 1 and args.secondary == "auto":
-            out["secondary_64_pairs_one_gpu"] = bench_batch64(args, W, params, dev, devi)
+        if args.workload == "C4" and world == 1 and args.secondary == "auto" and len(pairs) > 8:
+            out["secondary_8_pair_shard_one_gpu"] = bench_shard8(pairs, W, params, dev, devi)
         if world == 1 and args.cpu_baseline == "auto":
             out["cpu_baseline"], out["parity_vs_cpu"] = cpu_baseline(pairs, last, W, value, params, devi)
         print(json.dumps(out), flush=True)
@@ -465,20 +486,17 @@ def reduce_roofline(res, pairs, W, red_ms, wl):
                     "(k_reduce_final); traffic = both kernels' PMC bytes per launch from this workload's pass"}
 
 
-def bench_batch64(args, W, params, dev, devi, steps=3):
-    """The whole 64-pair KITTI batch of BASELINE configs[3] on this one GPU (the batch the
-    8-GPU job shards), timed like the main steps: a strong-scaling anchor beside the weak-
-    scaling value."""
+def bench_shard8(pairs, W, params, dev, devi, steps=3):
+    """One 8-pair shard of the C4 batch (its first 8 pairs) on this GPU, timed like the
+    main steps: the per-GPU work of the 8-GPU strong-scaling job, so the 1-GPU line shows
+    what the per-iteration chain costs at that batch size (a weak-scaling anchor)."""
     import torch
     import se3icp
-    from se3icp import datasets
-    t0 = time.time()
-    pairs, _ = datasets.kitti_like_pairs(64, seed=4, first=0, total_pairs=64, n_az=args.n_az)
-    log(f"secondary: 64 pairs generated in {time.time() - t0:.1f}s")
-    src = np.concatenate([p[0] for p in pairs])
-    tgt = np.concatenate([p[1] for p in pairs])
-    so = np.concatenate([[0], np.cumsum([p[0].shape[0] for p in pairs])])
-    to = np.concatenate([[0], np.cumsum([p[1].shape[0] for p in pairs])])
+    sub = pairs[:8]
+    src = np.concatenate([p[0] for p in sub])
+    tgt = np.concatenate([p[1] for p in sub])
+    so = np.concatenate([[0], np.cumsum([p[0].shape[0] for p in sub])])
+    to = np.concatenate([[0], np.cumsum([p[1].shape[0] for p in sub])])
     d_src = torch.from_numpy(src).to(dev)
     d_tgt = torch.from_numpy(tgt).to(dev)
     torch.cuda.synchronize()
@@ -492,9 +510,9 @@ def bench_batch64(args, W, params, dev, devi, steps=3):
     torch.cuda.synchronize()
     el = time.perf_counter() - t
     its = sum(sum(r.num_iterations for r in runner.results(k)) for k in range(steps))
-    return {"pairs": 64, "steps": steps, "ms_per_step": round(1000.0 * el / steps, 3), "value": round(its / el, 3),
-            "unit": "ICP iterations/s", "pairs_per_sec": round(64 * steps / el, 4),
-            "note": "examples/benchmark_kitti.cpp:120-197 as one batch on one GPU (synthetic scans, seed 4)"}
+    return {"pairs": len(sub), "steps": steps, "ms_per_step": round(1000.0 * el / steps, 3),
+            "value": round(its / el, 3), "unit": "ICP iterations/s", "pairs_per_sec": round(len(sub) * steps / el, 4),
+            "note": "pairs 0-7 of the batch as one call on one GPU: what each GPU registers in the 8-GPU job"}
 
 
 def host_info():
@@ -609,7 +627,12 @@ def cpu_baseline(pairs, gpu_res, W, gpu_value, gpu_params=None, devi=0, budget_s
             "runs": runs, "host": info,
             "speedup_gpu_vs_cpu": round(gpu_value / best["iter_per_s"], 2),
             # the ideal-scaling ceiling of the host: 1-thread rate x every physical core
-            "speedup_vs_1thread_x_physical_cores": round(gpu_value / (one["iter_per_s"] * phys), 2)}
+            "speedup_vs_1thread_x_physical_cores": round(gpu_value / (one["iter_per_s"] * phys), 2),
+            # north_star: the reference timed on the node's host cores -- the cgroup lets this
+            # process use only part of them, so the full host is the 1-thread rate x every
+            # physical core (ideal scaling; the measured multi-thread rate is `value`)
+            "speedup_vs_full_host": round(gpu_value / (one["iter_per_s"] * phys), 2),
+            "full_host_iter_per_s_ideal": round(one["iter_per_s"] * phys, 3)}
     # per sampled pair: pose and iteration counts; for the first pair also the correspondence
     # set of every iteration (traced on both sides): the share of equal target indices
     per_pair = []

@@ -1116,19 +1116,25 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
             const int a0 = live ? tree_first(n, t.L, leaf) : A, a1 = live ? tree_first(n, t.L, leaf + 1) : A;
             inq[b] = lane < a1 - a0;
             xq[b] = a0 - A + (inq[b] ? lane : 0);
-            const int e = s_val[xq[b]];
-            pq[b] = s_p[e];
+            // lanes outside the leaf load nothing: for an empty node (m == 0) or a trailing
+            // empty leaf s_val / s_p hold no point of this cloud, and cl.off + s_p[..] could
+            // lie before the buffer
+            pq[b] = inq[b] ? s_p[s_val[xq[b]]] : 0;
             const int src = cl.off + pq[b];
-            if constexpr (D == 12) {
-                const float4* r = reinterpret_cast<const float4*>(t.vec + (size_t)src * 12);
 #pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    const float4 q = r[k];
-                    v[b][4 * k] = q.x; v[b][4 * k + 1] = q.y; v[b][4 * k + 2] = q.z; v[b][4 * k + 3] = q.w;
+            for (int d = 0; d < D; ++d) v[b][d] = 0.0f;
+            if (inq[b]) {
+                if constexpr (D == 12) {
+                    const float4* r = reinterpret_cast<const float4*>(t.vec + (size_t)src * 12);
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        const float4 q = r[k];
+                        v[b][4 * k] = q.x; v[b][4 * k + 1] = q.y; v[b][4 * k + 2] = q.z; v[b][4 * k + 3] = q.w;
+                    }
+                } else {
+#pragma unroll
+                    for (int d = 0; d < D; ++d) v[b][d] = t.vec[(size_t)d * ld + src];
                 }
-            } else {
-#pragma unroll
-                for (int d = 0; d < D; ++d) v[b][d] = t.vec[(size_t)d * ld + src];
             }
             w64[b][0] = w64[b][1] = w64[b][2] = 0.0;
             if ((int)want64 & (int)inq[b]) {

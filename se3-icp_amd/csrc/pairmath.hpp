@@ -90,7 +90,7 @@ SE3ICP_HD void svd3(const double A[3][3], double U[3][3], double s[3], double V[
                 //    serial solve of k_reduce_final spent most of its time in them)
                 const double a = B[p][p], b = B[p][q], c = B[q][p], d = B[q][q];
                 {
-                    const double h = sqrt((a + d) * (a + d) + (c - b) * (c - b));
+                    const double h = hypot(a + d, c - b);  // (no overflow at ~1e154, no underflow at ~1e-160)
                     const double c1 = h > 0.0 ? (a + d) / h : 1.0, s1 = h > 0.0 ? (c - b) / h : 0.0;
                     svd3_rot_left(B, U, p, q, c1, s1);
                 }
@@ -99,7 +99,7 @@ SE3ICP_HD void svd3(const double A[3][3], double U[3][3], double s[3], double V[
                 //    well-conditioned one of the two for the sign of cos 2t)
                 const double x = B[p][p], y = 0.5 * (B[p][q] + B[q][p]), z = B[q][q];
                 if (y != 0.0) {
-                    const double h = sqrt(4.0 * y * y + (z - x) * (z - x));
+                    const double h = hypot(2.0 * y, z - x);
                     const double c2t = (z - x) / h, s2t = 2.0 * y / h;
                     double c2, s2;
                     if (c2t >= 0.0) {

@@ -19,6 +19,8 @@ Everything is numpy with an explicit ``numpy.random.Generator(PCG64(seed))``.
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 
@@ -127,7 +129,7 @@ def _street_scene(rng, length: float) -> _Scene:
 
 def kitti_like_sequence(n_scans: int, seed: int = 4, n_az: int = 1975, n_beams: int = 64, step: float = 1.0,
                         max_yaw_deg: float = 2.0, range_noise: float = 0.02, max_range: float = 80.0,
-                        scan_indices=None):
+                        scan_indices=None, workers: int = 0):
     """Return (scans, poses): scans[k] is an (N_k, 3) float64 cloud in the sensor frame of
     scan k, poses[k] its 4x4 world pose.  ~120k points per scan at the defaults.
     ``scan_indices`` ray-casts only those scans (others are None); every scan has its
@@ -145,11 +147,8 @@ def kitti_like_sequence(n_scans: int, seed: int = 4, n_az: int = 1975, n_beams: 
             pos[1] = np.clip(pos[1], -2.5, 2.5)
         poses.append(make_T(rot_3d(0, 0, yaw), pos))
     want = set(range(n_scans)) if scan_indices is None else set(scan_indices)
-    scans = []
-    for k in range(n_scans):
-        if k not in want:
-            scans.append(None)
-            continue
+
+    def cast(k):
         srng = np.random.Generator(np.random.PCG64([seed, k]))
         Rw, pk = poses[k][:3, :3], poses[k][:3, 3]
         az = np.linspace(0, 2 * np.pi, n_az, endpoint=False) + srng.uniform(0, 2 * np.pi / n_az)
@@ -162,7 +161,19 @@ def kitti_like_sequence(n_scans: int, seed: int = 4, n_az: int = 1975, n_beams: 
         t = np.concatenate(ts)
         ok = np.isfinite(t) & (t > 1.0)
         t = t[ok] + srng.normal(0, range_noise, ok.sum())
-        scans.append(np.ascontiguousarray(d[ok] * t[:, None]))
+        return np.ascontiguousarray(d[ok] * t[:, None])
+
+    # every scan has its own stream, so the scans are cast by a thread pool (numpy releases
+    # the GIL in the ray-box arithmetic); the result does not depend on the thread count
+    ks = [k for k in range(n_scans) if k in want]
+    nw = max(1, min(len(ks), workers if workers else min(8, os.cpu_count() or 1)))
+    if nw > 1:
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(nw) as ex:
+            got = dict(zip(ks, ex.map(cast, ks)))
+    else:
+        got = {k: cast(k) for k in ks}
+    scans = [got.get(k) for k in range(n_scans)]
     return scans, poses
 
 

@@ -55,6 +55,24 @@ def shard(n_pairs_total: int, world: int, rank: int) -> tuple[int, int]:
     return first, count
 
 
+def plan(world: int, rank: int, default_batch: int, global_batch: int = 0, pairs_per_gpu: int = 0):
+    """The rank's share of a benchmark job: (scaling, global_batch, first, count).
+
+    Strong scaling (the default): the job registers a fixed batch -- `global_batch`, or the
+    workload's BASELINE batch `default_batch` (C4: the 64 pairs of
+    examples/benchmark_kitti.cpp:120-197) -- split into contiguous blocks over the ranks, so
+    one GPU registers all of it and eight GPUs an eighth each.  Weak scaling when
+    `pairs_per_gpu` is set: every rank registers that many pairs of a world x P batch."""
+    if pairs_per_gpu:
+        scaling, total = "weak", world * pairs_per_gpu
+    else:
+        scaling, total = "strong", global_batch or default_batch
+    first, count = shard(total, world, rank)
+    if count == 0:
+        raise ValueError(f"a batch of {total} pairs leaves rank {rank} of {world} without a pair")
+    return scaling, total, first, count
+
+
 def exchange_results(dist, device, elapsed_s: float, loop_s: float, iterations: int, records: np.ndarray):
     """Cross-rank reduction of one timed region.
 

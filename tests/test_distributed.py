@@ -123,3 +123,54 @@ def test_exchange_results_uneven_shards_gloo_world2(tmp_path):
         np.testing.assert_array_equal(d["num_iterations"], it)
         np.testing.assert_array_equal(d["pure"], pure)
         np.testing.assert_array_equal(d["status"], st)
+
+
+def test_strong_plan_fixes_the_global_batch():
+    """bench.py's default: BASELINE's batch (C4: 64 pairs) split over the ranks, so N=1 holds
+    all 64 and N=8 eight each; uneven splits (64 over 3) keep every pair exactly once."""
+    for world in (1, 2, 3, 4, 8):
+        got = [sharding.plan(world, r, 64) for r in range(world)]
+        assert all(g[0] == "strong" and g[1] == 64 for g in got)
+        assert sum(g[3] for g in got) == 64
+        assert [g[2] for g in got] == [sum(h[3] for h in got[:r]) for r in range(world)]
+    assert [sharding.plan(3, r, 64)[3] for r in range(3)] == [22, 21, 21]
+    assert sharding.plan(1, 0, 64) == ("strong", 64, 0, 64)
+    assert sharding.plan(8, 7, 64) == ("strong", 64, 56, 8)
+    assert sharding.plan(2, 1, 64, global_batch=7) == ("strong", 7, 4, 3)
+    assert sharding.plan(4, 3, 64, pairs_per_gpu=8) == ("weak", 32, 24, 8)
+    with pytest.raises(ValueError):
+        sharding.plan(8, 7, 64, global_batch=5)
+
+
+def _strong_rank_main(rank, world, port, out_dir, total):
+    """One rank of a strong-scaling job: its plan() block of a `total`-pair batch, each pair
+    identified by its global index in the record, through the result exchange."""
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    scaling, tot, first, count = sharding.plan(world, rank, total)
+    res = [_Res(np.eye(4) * (first + k), first + k, k, 0) for k in range(count)]
+    out = sharding.exchange_results(dist, torch.device("cpu"), elapsed_s=float(count), loop_s=0.0,
+                                    iterations=sum(r.num_iterations for r in res), records=sharding.pair_records(res))
+    dist.barrier()
+    dist.destroy_process_group()
+    g = out[3]
+    np.savez(os.path.join(out_dir, f"s{rank}.npz"), elapsed=out[0], iters=out[2], poses=g.T, it=g.num_iterations)
+
+
+def test_strong_shard_64_over_3_gloo(tmp_path):
+    """BASELINE's 64-pair batch over 3 ranks (22 + 21 + 21): every pair is registered by
+    exactly one rank and the gather returns all 64 in batch order."""
+    import torch.multiprocessing as mp
+
+    world, total = 3, 64
+    mp.start_processes(_strong_rank_main, args=(world, _free_port(), str(tmp_path), total), nprocs=world, join=True,
+                       start_method="spawn")
+    for r in range(world):
+        d = np.load(tmp_path / f"s{r}.npz")
+        assert float(d["elapsed"]) == 22.0                 # max over ranks: the largest block
+        assert int(d["iters"]) == sum(range(total))        # every pair counted once
+        np.testing.assert_array_equal(d["it"], np.arange(total))
+        np.testing.assert_array_equal(d["poses"], np.stack([np.eye(4) * k for k in range(total)]))

@@ -1,6 +1,7 @@
 """bench.py's multi-rank path on one GPU: two ranks (gloo, both on cuda:0) register the
-two halves of an 8-pair C3 batch; the gathered poses must be bitwise those of a one-rank
-run over the same 8 pairs.  The 8-GPU RCCL run is the driver's."""
+two blocks (4 + 3) of a fixed 7-pair C3 batch -- bench.py's strong-scaling shard; the
+gathered poses must be bitwise those of a one-rank run over the same 7 pairs (SURVEY.md
+§4 (v), §8e).  The 8-GPU RCCL run is the driver's."""
 import os
 import socket
 import subprocess
@@ -23,22 +24,23 @@ def _port():
 
 @pytest.mark.timeout(900)  # (a fresh box's first `import torch` alone can take minutes)
 def test_two_rank_bench_equals_one_rank(tmp_path):
-    common = ["--steps", "1", "--warmup", "0", "--workload", "C3", "--cpu-baseline", "off"]
+    common = ["--steps", "1", "--warmup", "0", "--workload", "C3", "--cpu-baseline", "off", "--global-batch", "7"]
     one = tmp_path / "one.npy"
     two = tmp_path / "two.npy"
     env = dict(os.environ)
-    r1 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--pairs-per-gpu", "8", "--dump-poses",
+    r1 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dump-poses",
                          str(one)] + common, capture_output=True, text=True, timeout=300, env=env)
     assert r1.returncode == 0, r1.stderr[-3000:]
     r2 = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                          "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
-                         "--gpus", "2", "--backend", "gloo", "--pairs-per-gpu", "4", "--dump-poses", str(two)] + common,
+                         "--gpus", "2", "--backend", "gloo", "--dump-poses", str(two)] + common,
                         capture_output=True, text=True, timeout=300, env=env)
     assert r2.returncode == 0, r2.stderr[-3000:]
     import json
     line = [l for l in r2.stdout.splitlines() if l.startswith("{")][-1]
     d = json.loads(line)
-    assert d["n_gpus"] == 2 and d["config"]["global_batch_pairs"] == 8
+    assert d["n_gpus"] == 2 and d["config"]["global_batch_pairs"] == 7 and d["scaling"] == "strong"
+    assert d["config"]["pairs_per_gpu"] == [4, 3]
     a, b = np.load(one), np.load(two)
-    assert a.shape == b.shape == (8, 4, 4)
+    assert a.shape == b.shape == (7, 4, 4)
     assert np.array_equal(a, b)

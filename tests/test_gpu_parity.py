@@ -215,6 +215,43 @@ def test_nn_exact_ties_pick_lowest_index(se3icp_mod):
     assert gi[0] == 0 and nrech >= 1
 
 
+@pytest.mark.parametrize("dim", [3, 12])
+@pytest.mark.parametrize("nq", [1, 3, 10])
+def test_nn_few_queries_against_large_data(se3icp_mod, refcpu, dim, nq):
+    """A query cloud far smaller than the data cloud shares the batch's tree depth, so its
+    local subtrees hold empty nodes and empty trailing leaves: the tree build must not read
+    outside the clouds there (k_tree_local's final phase)."""
+    rng = np.random.default_rng(100 + dim + nq)
+    data = rng.normal(0, 1, (9000, dim))
+    q = rng.normal(0, 1, (nq, dim))
+    gi, gd2, _ = se3icp_mod.nearest_neighbors(q, data)
+    ri, rd2 = refcpu.nn(q, data)
+    assert np.array_equal(gi, ri)
+    np.testing.assert_allclose(gd2, rd2, rtol=0, atol=1e-12)
+
+
+def test_batch_with_tiny_first_source_cloud(se3icp_mod, refcpu):
+    """First source cloud under 1/64 of the largest cloud of the batch: its
+    subtrees below the shared global levels are mostly empty.  The tiny pair equals its
+    oracle run, the big pair equals its own one-pair run bitwise."""
+    from se3icp import datasets
+    pairs, _ = datasets.kitti_like_pairs(2, seed=4, first=1, total_pairs=8)
+    s0, t0 = pairs[0]
+    rng = np.random.default_rng(7)
+    small = s0[np.sort(rng.choice(s0.shape[0], 1200, replace=False))]
+    assert small.shape[0] * 64 < max(t0.shape[0], pairs[1][0].shape[0])
+    p = se3icp_mod.kitti_params()
+    got = se3icp_mod.register_batch([(small, t0), pairs[1]], "se3_gicp", p)
+    alone = se3icp_mod.register_batch([pairs[1]], "se3_gicp", p)[0]
+    assert np.array_equal(got[1].T, alone.T)
+    assert got[1].num_iterations == alone.num_iterations
+    rp = refcpu.default_params(estimated_overlap=0.7, max_num_se3_iterations=10, mse=1e-7, mse_switch_error=5e-7,
+                               number_of_nn_for_LRF=90)
+    ref = refcpu.register(small, t0, refcpu.RUN_SE3_ICP, "gicp", rp)
+    assert np.linalg.norm(got[0].T - ref["T"]) <= 1e-5, (got[0].T, ref["T"])
+    assert got[0].num_iterations == ref["num_iterations"]
+
+
 # --------------------------------------------------------------------------- synthetic workloads
 def test_bunny_pair_se3_pt2pt(se3icp_mod, refcpu, bunny_unique):
     from se3icp import datasets

@@ -113,6 +113,27 @@ def test_umeyama_rotation_extremes(pairmath):
         assert np.isclose(np.linalg.det(G[:3, :3]), 1.0)
 
 
+@pytest.mark.parametrize("scale", [1e-85, 1e85])
+def test_umeyama_tiny_and_huge_cross_covariance(pairmath, scale):
+    """Cross-covariance entries around 1e-170 and 1e170: the Jacobi
+    hypotenuses must neither underflow to a 0/0 rotation nor overflow to a zeroed block."""
+    rng = np.random.default_rng(13)
+    cases, want, rots = [], [], []
+    for _ in range(6):
+        R = _rot(*rng.uniform(-np.pi, np.pi, 3))
+        src = rng.normal(size=(100, 3)) * np.array([2.0, 1.0, 0.5]) * scale
+        dst = src @ R.T + rng.uniform(-1, 1, 3) * scale
+        s, n = _moments(src, dst)
+        cases.append("U " + _fmt(s) + " " + _fmt([n]))
+        want.append(_umeyama(src, dst))
+        rots.append(R)
+    for got, T, R in zip(pairmath(cases), want, rots):
+        G = got.reshape(4, 4)
+        assert np.all(np.isfinite(G)), G
+        assert np.abs(G[:3, :3] - R).max() < 1e-9, (G, R)
+        assert np.abs(G[:3, 3] - T[:3, 3]).max() < 1e-9 * scale, (G, T)
+
+
 def _pack(A, b):
     return np.concatenate([A[np.triu_indices(6)], b])
 
