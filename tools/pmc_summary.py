@@ -12,9 +12,15 @@ k_nn_single<D>); for such traces the stats summary also lists the SPAN of each l
 first start to last end.  Since round 4 the search is one grid (k_nn_search<D>).
 
 Each --pmc-dir holds one separate `rocprofv3 --pmc <counters> --output-format csv` pass
-(FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950).  HBM bytes per launch follow
-MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) under-reports wide coalesced reads by 2x on
-gfx950, so  hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
+(FETCH_SIZE and WRITE_SIZE cannot share a pass on gfx950).  HBM bytes per launch:
+hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024, with the raw (1 x FETCH_SIZE) figure
+beside it.  The factor 2 is calibrated for every access pattern the kernels use
+(tools/fetch_calib.hip, profiles/r05_fetch_calib.json): on gfx950 every fabric read is a
+128-B request (TCC_EA0_RDREQ_128B = TCC_EA0_RDREQ; the 32-B / 64-B counts and TCC_BUBBLE
+read 0), and FETCH_SIZE = (RDREQ - BUBBLE - RDREQ_32B) x 64 B counts each at 64 B -- so
+FETCH_SIZE is exactly half the request bytes for a coalesced 16-B stream and for scattered
+4-, 8-, 16- and 48-B gathers alike (TCC_EA0_RDREQ_DRAM_32B x 32 B agrees).  A scattered
+gather costs 128 B of fabric traffic per line it touches, whatever its width.
 """
 import argparse
 import collections
@@ -45,14 +51,80 @@ def pmc(dirs):
         nd = max(len(v) for v in cs.values())
         e = {"dispatches": nd, "counters_per_dispatch": means}
         if "FETCH_SIZE" in means and "WRITE_SIZE" in means:
+            e["fetch_bytes_raw"] = means["FETCH_SIZE"] * 1024.0
             e["fetch_bytes_corrected"] = 2.0 * means["FETCH_SIZE"] * 1024.0
             e["write_bytes"] = means["WRITE_SIZE"] * 1024.0
+            e["hbm_bytes_per_launch_raw"] = e["fetch_bytes_raw"] + e["write_bytes"]
             e["hbm_bytes_per_launch"] = e["fetch_bytes_corrected"] + e["write_bytes"]
+        rb = read_bytes_by_size(means)
+        if rb:
+            # the request-size counters (calibrated on tools/fetch_calib.hip, profiles/r05_fetch_calib.json)
+            for name, b in rb.items():
+                e[f"fetch_bytes_{name}"] = b
+            if "WRITE_SIZE" in means and "dram_32b_units" in rb:
+                e["hbm_bytes_per_launch_dram32"] = rb["dram_32b_units"] + means["WRITE_SIZE"] * 1024.0
         if "SQ_WAVE_CYCLES" in means and means["SQ_WAVE_CYCLES"] > 0:
             wc = means["SQ_WAVE_CYCLES"]
             e["frac_wait_any"] = means.get("SQ_WAIT_ANY", 0.0) / wc
             e["frac_wait_inst_any"] = means.get("SQ_WAIT_INST_ANY", 0.0) / wc
             e["frac_active_inst_any"] = means.get("SQ_ACTIVE_INST_ANY", 0.0) / wc
+        out[k] = e
+    return out
+
+
+# request-size TCC counters (rocprofv3 counter_defs.yaml, gfx950 events 42-45, 62, 108, 112)
+TCC_REQ = ["TCC_EA0_RDREQ_sum", "TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum",
+           "TCC_BUBBLE_sum", "TCC_EA0_RDREQ_DRAM_32B_sum", "TCC_EA0_RDREQ_DRAM_sum"]
+
+
+def read_bytes_by_size(c):
+    """Fabric read bytes from the request-size counters of one dispatch (None if absent):
+    32 x 32-B + 64 x 64-B + 128 x 128-B requests, and 32 x the DRAM 32-B units."""
+    out = {}
+    if all(k in c for k in ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum", "TCC_EA0_RDREQ_128B_sum")):
+        out["by_request_size"] = (32.0 * c["TCC_EA0_RDREQ_32B_sum"] + 64.0 * c["TCC_EA0_RDREQ_64B_sum"]
+                                  + 128.0 * c["TCC_EA0_RDREQ_128B_sum"])
+    if "TCC_EA0_RDREQ_DRAM_32B_sum" in c:
+        out["dram_32b_units"] = 32.0 * c["TCC_EA0_RDREQ_DRAM_32B_sum"]
+    return out
+
+
+def calib(plain_jsonl, dirs):
+    """tools/fetch_calib.hip: per access pattern, the counters' bytes against the known
+    requested bytes and access count (the timed, second dispatch of each kernel)."""
+    known = {}
+    for line in open(plain_jsonl):
+        line = line.strip()
+        if line.startswith("{"):
+            d = json.loads(line)
+            known[d["kernel"]] = d
+    per = collections.defaultdict(lambda: collections.defaultdict(dict))  # kernel -> counter -> dispatch -> value
+    for d in dirs:
+        for r in _rows(d, "*counter_collection.csv"):
+            k = r.get("Kernel_Name", "?").split("(")[0].replace("void ", "").strip()
+            per[k][r.get("Counter_Name")][(d, int(r.get("Dispatch_Id", 0)))] = float(r.get("Counter_Value", 0) or 0)
+    out = {}
+    for k, kn in known.items():
+        cs = per.get(k, {})
+        c = {}
+        for name, disp in cs.items():
+            vals = [v for _, v in sorted(disp.items(), key=lambda kv: kv[0][1])]
+            c[name] = vals[-1]  # the timed launch (the first one warms page tables)
+        req = kn["requested_bytes"]
+        e = {"accesses": kn["accesses"], "requested_bytes": req, "ms": kn["ms"], "requested_GBps": kn["requested_GBps"],
+             "counters": c}
+        if "FETCH_SIZE" in c:
+            fb = c["FETCH_SIZE"] * 1024.0
+            e["fetch_size_bytes"] = fb
+            e["fetch_size_over_requested"] = round(fb / req, 4)
+            e["fetch_size_bytes_per_access"] = round(fb / kn["accesses"], 2)
+        for name, b in read_bytes_by_size(c).items():
+            e[f"bytes_{name}"] = b
+            e[f"bytes_{name}_over_requested"] = round(b / req, 4)
+            e[f"bytes_{name}_per_access"] = round(b / kn["accesses"], 2)
+            e[f"GBps_{name}"] = round(b / (kn["ms"] * 1e-3) / 1e9, 1)
+            if "fetch_size_bytes" in e and e["fetch_size_bytes"] > 0:
+                e[f"correction_{name}_over_fetch_size"] = round(b / e["fetch_size_bytes"], 4)
         out[k] = e
     return out
 
@@ -96,9 +168,20 @@ def main():
     ap.add_argument("--trace-dir", nargs="*", default=[])
     ap.add_argument("--stats-md")
     ap.add_argument("--command", default="")
+    ap.add_argument("--calib", nargs="*", default=None,
+                    help="<calib_plain.jsonl> <pmc dirs...>: summarise tools/fetch_calib.sh into --out")
     ap.add_argument("--workload", default="C4", help="bench.py --workload of the profiled command (bench.py keys "
                                                       "the PMC lookups by it)")
     a = ap.parse_args()
+    if a.calib:
+        res = {"command": a.command or "tools/fetch_calib.sh", "table_bytes": 1 << 30,
+               "note": "per pattern: the known accesses / requested bytes of tools/fetch_calib.hip against FETCH_SIZE and "
+                       "the TCC request-size counters of the same (second, timed) dispatch",
+               "patterns": calib(a.calib[0], a.calib[1:])}
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1, sort_keys=True)
+        print(f"wrote {a.out}")
+        return
     if a.out:
         res = {"command": a.command, "workload": a.workload, "passes": a.pmc_dir,
                "hbm_formula": "(2*FETCH_SIZE + WRITE_SIZE) * 1024 bytes (gfx950 FETCH_SIZE reports 1/2)",

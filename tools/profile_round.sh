@@ -12,11 +12,11 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 WA="--workload $W"
 [ "$W" = "C2u" ] && WA="--workload C2 --c2-cloud unique"
-B="python3 bench.py $WA --steps 3 --warmup 1 --cpu-baseline off --secondary off"
+B="python3 bench.py $WA --steps 3 --warmup 1 --cpu-baseline off --secondary off --pair-cache /tmp/se3icp_pairs"
 SQ1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU"
 SQ2="SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_SALU SQ_WAIT_INST_LDS"
 T="${TAG}_${W}"
-BENCH_CMD="python3 bench.py $WA"
+BENCH_CMD="python3 bench.py $WA --pair-cache /tmp/se3icp_pairs"
 STATS_CMD="rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$T -o run -- $B"
 printf 'bench: %s\nstats: %s\npmc: rocprofv3 --pmc <FETCH_SIZE | WRITE_SIZE | %s | %s> --output-format csv -- %s\n' \
   "$BENCH_CMD" "$STATS_CMD" "$SQ1" "$SQ2" "$B" > "gpurun_out/cmd_$T.txt"
