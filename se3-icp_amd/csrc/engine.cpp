@@ -128,7 +128,7 @@ Engine::~Engine() {
     if (!ok_) return;
     (void)hipSetDevice(dev_);
     DevBuf* all[] = {&d_clouds_, &d_setup_, &d_pairs_, &d_cloud_of_, &d_inptr_, &d_in_, &d_xyz64_, &d_xyz32_,
-                     &d_fr64_, &d_fr32_, &d_nrm64_, &d_conf64_, &d_knn_,
+                     &d_fr64_, &d_fr32_, &d_nrm64_, &d_tgeo_, &d_conf64_, &d_knn_,
                      &d_corr_idx_, &d_corr_dist_, &d_flag_count_, &d_gcost_, &d_cls_, &d_trim_key_, &d_red_partial_,
                      &d_red_out_, &d_work_, &d_wb_, &d_wn_, &d_chunks_, &d_partial_, &d_centers_,
                      &d_rechecked_, &d_keys0_, &d_vals1_, &d_sort_tmp_, &d_stats_,
@@ -180,7 +180,7 @@ int Engine::alloc_points(int64_t ntot, int kmax, bool knn_list) {
     const size_t L = (size_t)ld_;
     bool ok = ensure<int32_t>(d_cloud_of_, L) && ensure<double>(d_in_, 3 * L) && ensure<double>(d_xyz64_, 3 * L) &&
               ensure<float>(d_xyz32_, 3 * L) && ensure<double>(d_fr64_, 12 * L) && ensure<float>(d_fr32_, 12 * L) &&
-              ensure<double>(d_nrm64_, 3 * L) && ensure<double>(d_conf64_, L) &&
+              ensure<double>(d_nrm64_, 3 * L) && ensure<double>(d_conf64_, L) && ensure<double>(d_tgeo_, 8 * L) &&
               (!knn_list || ensure<int32_t>(d_knn_, L * kmax_)) && ensure<int32_t>(d_corr_idx_, L) && ensure<float>(d_corr_dist_, L) &&
               ensure<int32_t>(d_flag_count_, 4) &&
               ensure<uint32_t>(d_keys0_, L) &&
@@ -211,6 +211,7 @@ View Engine::view() const {
     v.fr32 = (float*)d_fr32_.p;
     v.nrm64 = (double*)d_nrm64_.p;
     v.conf64 = (double*)d_conf64_.p;
+    v.tgeo = (double*)d_tgeo_.p;
     v.knn = knn_list_ ? (int32_t*)d_knn_.p : nullptr;
     v.corr_idx = (int32_t*)d_corr_idx_.p;
     v.corr_dist = (float*)d_corr_dist_.p;
@@ -676,6 +677,7 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemsetAsync((uint64_t*)d_trim_key_.p + npairs, 0, sizeof(uint64_t) * npairs, s));  // no trim window yet
     HIPCHK(hipMemsetAsync(d_trim_ctr_.p, 0, sizeof(unsigned) * 4 * npairs, s));
+    launch_geo_rows(view(), s);  // (after the setup's normals and confidences)
     HIPCHK(hipMemsetAsync(d_trim_hist_.p, 0, sizeof(unsigned) * 4096 * npairs, s));
     View v = view();
     double nn_ms = 0;

@@ -124,7 +124,7 @@ class Engine {
     std::vector<const double*> h_inptr_;
 
     // device buffers
-    DevBuf d_clouds_, d_setup_, d_pairs_, d_cloud_of_, d_inptr_, d_in_, d_xyz64_, d_xyz32_, d_fr64_, d_fr32_, d_nrm64_,
+    DevBuf d_clouds_, d_setup_, d_pairs_, d_cloud_of_, d_inptr_, d_in_, d_xyz64_, d_xyz32_, d_fr64_, d_fr32_, d_nrm64_, d_tgeo_,
         d_conf64_, d_knn_, d_corr_idx_, d_corr_dist_, d_flag_count_, d_gcost_, d_cls_,
         d_trim_key_, d_red_partial_, d_red_out_, d_work_, d_wb_, d_wn_, d_chunks_, d_partial_, d_centers_,
         d_rechecked_, d_keys0_, d_vals1_, d_sort_tmp_, d_stats_, d_qlist_, d_qcount_, d_hist_, d_cert_,

@@ -530,6 +530,26 @@ __device__ __forceinline__ void corr_terms(int est, bool cf, const double* T, co
     acc[27] += cf ? sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2]) : dist;
 }
 
+// The target points' geometry rows for k_reduce's gathers (View::tgeo): one 64-B row per
+// point of a target cloud -- a kept correspondence then touches one 128-B line of target
+// data instead of up to seven (measured: every fabric read on gfx950 is a 128-B request,
+// profiles/r05_fetch_calib.json).  Four lanes per row, one 16-B part each, so every store
+// instruction writes 1 KB of consecutive rows; source clouds are skipped (their rows are
+// never read).
+__global__ __launch_bounds__(256) void k_geo_rows(View v) {
+    const int i = blockIdx.x * 64 + (int)(threadIdx.x >> 2), part = (int)(threadIdx.x & 3);
+    if (i >= v.npts) return;
+    const CloudSetup* st = v.setup + v.cloud_of[i];
+    if (!st->is_target) return;
+    const size_t ld = v.ld;
+    double2 r;
+    if (part == 0) r = make_double2(v.xyz64[i], v.xyz64[ld + i]);
+    else if (part == 1) r = make_double2(v.xyz64[2 * ld + i], v.nrm64[i]);
+    else if (part == 2) r = make_double2(v.nrm64[ld + i], v.nrm64[2 * ld + i]);
+    else r = make_double2(st->want_conf ? v.conf64[i] : 0.0, 0.0);
+    reinterpret_cast<double2*>(v.tgeo)[(size_t)i * 4 + part] = r;
+}
+
 // Block b sums the terms of its pair's queries q0 + threadIdx.x + kRedThreads u (u < kRedPer,
 // below q1).  Every input of the thread's kRedPer correspondences is loaded before the
 // first is used: a wave's latency is a few dependent round trips (work record -> index and
@@ -565,15 +585,18 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce(View v) {
     double xs[kRedPer][3], xt[kRedPer][3], n0[kRedPer][3], nt[kRedPer][3], w2[kRedPer];
 #pragma unroll
     for (int u = 0; u < kRedPer; ++u) {
+        // the target's point, normal and confidence: one 64-B geometry row (k_geo_rows)
+        const double2* tr = reinterpret_cast<const double2*>(v.tgeo + (size_t)gt[u] * 8);
+        const double2 t01 = tr[0], t23 = tr[1], t45 = tr[2];
+        xt[u][0] = t01.x; xt[u][1] = t01.y; xt[u][2] = t23.x;
+        nt[u][0] = t23.y; nt[u][1] = t45.x; nt[u][2] = t45.y;
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
             xs[u][a] = v.xyz64[a * ld + g[u]];
-            xt[u][a] = v.xyz64[a * ld + gt[u]];
             n0[u][a] = est == EST_GICP ? v.nrm64[a * ld + g[u]] : 0.0;
-            nt[u][a] = est != EST_PT2PT ? v.nrm64[a * ld + gt[u]] : 0.0;
         }
         if (cf) {
-            const double wc = (v.conf64[g[u]] + v.conf64[gt[u]]) / 2.0;  // ISR.cpp:913
+            const double wc = (v.conf64[g[u]] + tr[3].x) / 2.0;  // ISR.cpp:913
             w2[u] = wc * wc;
         } else {
             w2[u] = 1.0;
@@ -697,6 +720,9 @@ void trim_prof_report() {
 void launch_trim(const View& v, hipStream_t s) {
     hipLaunchKernelGGL(k_trim_window, dim3(v.npairs * kTrimBlocks), dim3(256), 0, s, v);
     hipLaunchKernelGGL(k_trim, dim3(v.npairs), dim3(1024), 0, s, v);
+}
+void launch_geo_rows(const View& v, hipStream_t s) {
+    if (v.npts > 0) hipLaunchKernelGGL(k_geo_rows, dim3((v.npts + 63) / 64), dim3(256), 0, s, v);
 }
 void launch_reduce(const View& v, const int32_t* pair_wb, const int32_t* pair_wn, PairState* state, double* hist,
                    int32_t* next_phase, hipStream_t s) {

@@ -109,6 +109,25 @@ __device__ __forceinline__ float box_lb_u(const float* lo_, const float* hi_, co
     return s;
 }
 
+// min / max of values the compiler cannot prove canonical (DPP moves, LDS reads): fminf /
+// fmaxf would quiet a possible signalling NaN first (a v_max_f32 x, x, x per operand); the
+// distances here are finite or quiet NaNs, for which the raw instructions agree
+__device__ __forceinline__ float fmin_raw(float a, float b) {
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float fmax_raw(float a, float b) {
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float fmin3_raw(float a, float b, float c) {
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
 // f32 squared 12-D distance of a query (dimension pairs) to a staged target: two
 // interleaved FMA chains (even / odd dimensions) and one add, within the D-term chain
 // bound f32_err assumes
@@ -172,9 +191,9 @@ __device__ __forceinline__ void compact_sweep(const float4* tile, const float4* 
             const float p1 = xor_lane(a1, m), p2 = xor_lane(a2, m);
             const int pb = xor_lane(b1, m);
             const bool lt = (bool)((int)(p1 < a1) | ((int)(p1 == a1) & (int)(pb < b1)));
-            a2 = fminf(fmaxf(a1, p1), fminf(a2, p2));
+            a2 = fmin3_raw(fmax_raw(a1, p1), a2, p2);
             b1 = lt ? pb : b1;
-            a1 = fminf(a1, p1);
+            a1 = fmin_raw(a1, p1);
         }
         if ((int)(sub == 0) & (int)(slot < w)) {
             r1[qi] = a1;
@@ -327,48 +346,60 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
         m = (float)(kExpand * sqrt(a2 * rot_frob2(T, Tp) + dt * dt));
     }
     cp->margin = m;
-    // No previous match (a pair's first search): seed one from a greedy descent of the
-    // target tree (the child whose f32 box bound is smaller, down to a leaf; a target of
-    // that leaf).  The search only uses it for its first pruning threshold, so any target
-    // is valid; a near one spares the group walk the nodes an infinite threshold opens.
-    // (only a run's first iteration can lack one: corr_idx is reset to -1 when the run
-    // starts and every search writes it, so later iterations skip this dependent gather)
-    if ((int)(it == 1) & (int)(ct.n > 0) && v.corr_idx[g] < 0) {
-        double m0[D], Q[D];
-        load_m0<D>(v, TR, gx, g, m0);
-        pose_m0<D>(T, m0, Q);
-        float qf[D];
+    return false;
+}
+
+// No previous match (a pair's first search, it == 1): seed one from a greedy descent of the
+// target tree (the child whose f32 box bound is smaller, down to a leaf; a target of that
+// leaf).  The search only uses it for its first pruning threshold, so any target is valid;
+// a near one spares the group walk the nodes an infinite threshold opens.  One descent per
+// kSeedShare consecutive source tree positions (close together in the search space), by the
+// block's first threads: the chunk's 1,024 per-query descents -- a chain of 2L dependent box
+// loads each -- made the first k_nn_prep ~4x the cost of a later one (C4 64 pairs, same-box
+// A/B: one seed per 16 positions saved 0.4 ms/step of k_nn_prep but cost the first search
+// as much).
+#ifndef SE3ICP_SEED_SHARE
+#define SE3ICP_SEED_SHARE 4
+#endif
+constexpr int kSeedShare = SE3ICP_SEED_SHARE;
+template <int D>
+__device__ __forceinline__ int seed_descent(const View& v, const TreeRef& TR, const PairDev* P, const CloudDev& ct,
+                                            int gx, int g) {
+    double T[12], m0[D], Q[D];
+    load_T(P, T);
+    load_m0<D>(v, TR, gx, g, m0);
+    pose_m0<D>(T, m0, Q);
+    float qf[D];
 #pragma unroll
-        for (int r = 0; r < D; ++r) qf[r] = (float)((D == 3) ? Q[r] - P->f32_center[r] : Q[r]);
-        const float* lo = TR.lo + (size_t)P->tgt * TR.nnodes * D;
-        const float* hi = TR.hi + (size_t)P->tgt * TR.nnodes * D;
-        int h = 0;
-        for (int lv = 0; lv < TR.L; ++lv) {
-            const int a = 2 * h + 1;
-            const float la = box_lb<D>(lo + (size_t)a * D, hi + (size_t)a * D, qf);
-            const float lb = box_lb<D>(lo + (size_t)(a + 1) * D, hi + (size_t)(a + 1) * D, qf);
-            h = la <= lb ? a : a + 1;
-        }
-        const int li = h - ((1 << TR.L) - 1);
-        const int ta = min(tree_first(ct.n, TR.L, li), ct.n - 1);
-        const int cnt = max(tree_first(ct.n, TR.L, li + 1) - ta, 1);
-        // the nearest of kSeedTargets targets spread over the leaf
-        const float* tv = TR.tvec + tree_tv_ix<D>(0, ct.off, 0);  // (the cloud's first slot)
-        int best = ta;
-        float bd = INFINITY;
-        for (int k = 0; k < kSeedTargets; ++k) {
-            const int t = ta + (2 * k + 1) * cnt / (2 * kSeedTargets);
-            float d = 0.f;
-#pragma unroll
-            for (int r = 0; r < D; ++r) {
-                const float e = qf[r] - tv[tree_tv_ix<D>(v.ld, t, r)];
-                d = fmaf(e, e, d);
-            }
-            best = d < bd ? t : best;
-            bd = fminf(d, bd);
-        }
-        v.corr_idx[g] = TR.perm[ct.off + best];
+    for (int r = 0; r < D; ++r) qf[r] = (float)((D == 3) ? Q[r] - P->f32_center[r] : Q[r]);
+    const float* lo = TR.lo + (size_t)P->tgt * TR.nnodes * D;
+    const float* hi = TR.hi + (size_t)P->tgt * TR.nnodes * D;
+    int h = 0;
+    for (int lv = 0; lv < TR.L; ++lv) {
+        const int a = 2 * h + 1;
+        const float la = box_lb<D>(lo + (size_t)a * D, hi + (size_t)a * D, qf);
+        const float lb = box_lb<D>(lo + (size_t)(a + 1) * D, hi + (size_t)(a + 1) * D, qf);
+        h = la <= lb ? a : a + 1;
     }
+    const int li = h - ((1 << TR.L) - 1);
+    const int ta = min(tree_first(ct.n, TR.L, li), ct.n - 1);
+    const int cnt = max(tree_first(ct.n, TR.L, li + 1) - ta, 1);
+    // the nearest of kSeedTargets targets spread over the leaf
+    const float* tv = TR.tvec + tree_tv_ix<D>(0, ct.off, 0);  // (the cloud's first slot)
+    int best = ta;
+    float bd = INFINITY;
+    for (int k = 0; k < kSeedTargets; ++k) {
+        const int t = ta + (2 * k + 1) * cnt / (2 * kSeedTargets);
+        float d = 0.f;
+#pragma unroll
+        for (int r = 0; r < D; ++r) {
+            const float e = qf[r] - tv[tree_tv_ix<D>(v.ld, t, r)];
+            d = fmaf(e, e, d);
+        }
+        best = d < bd ? t : best;
+        bd = fminf(d, bd);
+    }
+    return TR.perm[ct.off + best];
     return false;
 }
 
@@ -422,6 +453,29 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
                                           : !prep_settle<3>(v, TR, P, pair, ct, gx, g, 0.0);
             l = tree_node_of(x, cs.n, TR.GL) - (ci << (TR.GL - v.chunk_level));
             if (active) atomicAdd(&s_cnt[l], 1);
+        }
+    }
+    // a run's first search: shared seeds (seed_descent), one per kSeedShare positions
+    if ((int)(phase != PHASE_IDLE) & (int)(P->iter == 1)) {  // (block-uniform)
+        static_assert(kSeedShare >= 1 && kChunkQ % kSeedShare == 0, "a thread per seed");
+        __shared__ int s_seed[kChunkQ / kSeedShare];
+        const CloudDev cs = v.clouds[P->src], ct = v.clouds[P->tgt];
+        const TreeRef TR = (phase == PHASE_SE3) ? v.t12 : v.t3;
+        const int ci = c & ((1 << v.chunk_level) - 1);
+        const int a = tree_first(cs.n, v.chunk_level, ci), b = tree_first(cs.n, v.chunk_level, ci + 1);
+        if ((int)threadIdx.x < kChunkQ / kSeedShare) {
+            const int xr = a + kSeedShare * (int)threadIdx.x;
+            int sd = -1;
+            if ((int)(xr < b) & (int)(ct.n > 0)) {
+                const int gxr = cs.off + xr, gr = cs.off + TR.perm[gxr];
+                sd = (phase == PHASE_SE3) ? seed_descent<12>(v, TR, P, ct, gxr, gr) : seed_descent<3>(v, TR, P, ct, gxr, gr);
+            }
+            s_seed[threadIdx.x] = sd;
+        }
+        __syncthreads();
+        if ((int)active & (int)(ct.n > 0)) {
+            const int g = cs.off + TR.perm[cs.off + x];
+            if (v.corr_idx[g] < 0) v.corr_idx[g] = s_seed[(x - a) / kSeedShare];
         }
     }
     const unsigned long long m = __ballot(active);
@@ -753,9 +807,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
                     if ((W >> lane) & 1ull) {
                         const float r1 = s_r1[lane], r2 = s_r2[lane];
                         const int rb = s_rb[lane];
-                        d2 = fminf(fmaxf(d1, r1), fminf(d2, r2));
+                        d2 = fmin3_raw(fmax_raw(d1, r1), d2, r2);
                         i1 = r1 < d1 ? rb : i1;
-                        d1 = fminf(d1, r1);
+                        d1 = fmin_raw(d1, r1);
                     }
                     __builtin_amdgcn_wave_barrier();
                     {  // 64-lane evaluation slots issued

@@ -767,6 +767,9 @@ __global__ __launch_bounds__(kLevThreads) void k_tree_level(TreeView t, int leve
 // in place of k_tree_finish / k_tree_leafbox / k_tree_up: the final permutation and its
 // inverse, the tree-ordered f32 (and f64) vectors, and the boxes of every leaf and inner
 // node below level G.  s_val holds level-G positions e (s_p[e]: the point).
+#ifndef SE3ICP_TREE_LDS_SAMPLE
+#define SE3ICP_TREE_LDS_SAMPLE 1
+#endif
 constexpr int kLocalMax = 4096;  // power of two
 constexpr int kWaveSortPer = 8;  // sub-nodes of <= 512 points: register sort by one wave
 constexpr int kLocalThreads = 512;
@@ -780,6 +783,13 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
     __shared__ int32_t s_p[kLocalMax];
     __shared__ int s_best[128];
     __shared__ float s_mu[128], s_sd[128];  // the split coordinate's sample mean and sd (variance splits)
+    // the split-dimension sample: the vectors of the level-G positions 16 j, kept in LDS for
+    // every level (round 4 gathered every 16th point of each sub-node from the node's 12
+    // columns at every level: scattered 4-B reads that fetched ~40 B of 128-B lines per
+    // point and level, a third of the kernel's traffic), and their current positions
+    constexpr int kSmp = kLocalMax / 16;
+    __shared__ float s_smp[D][kSmp];
+    __shared__ int32_t s_spos[kSmp];
     const int nG = 1 << G;
     const int c = blockIdx.x / nG, i = blockIdx.x % nG;
     const CloudDev cl = t.clouds[c];
@@ -839,6 +849,10 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
                 if (pl[u0 + u] >= 0) {
 #pragma unroll
                     for (int d = 0; d < D; ++d) col0[d * m + e] = x[u][d];
+                    if ((e & 15) == 0) {
+#pragma unroll
+                        for (int d = 0; d < D; ++d) s_smp[d][e >> 4] = x[u][d];
+                    }
                 }
             }
         }
@@ -860,22 +874,39 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
         }
 #endif
         const int nsub = 1 << r;  // sub-nodes of this level under the WG's node (<= 128: see the host)
-        // split dimension of each sub-node: widest extent of the box of every
-        // kSplitSample-th point (the sample of the global levels), a wave per sub-node
+        // the sample's current positions (the sub-node of each sample point)
+        const int nsmp = (m + 15) >> 4;
+        for (int e = tid; e < m; e += kLocalThreads) {
+            const int q = s_val[e];
+            if ((q & 15) == 0) s_spos[q >> 4] = e;
+        }
+        __syncthreads();
+        // split dimension of each sub-node: the dimension of largest variance over the
+        // sample points it holds (1 in 16: denser samples measured slower overall -- strides
+        // 1, 4, 8, 16, 32, 64 tried in round 2), a wave per sub-node, LDS reads only
         {
             const int lane = tid & 63, wv = tid >> 6;
             for (int k = wv; k < nsub; k += kLocalThreads / 64) {
                 const int a0 = tree_first(n, l, (i << r) + k) - A, a1 = tree_first(n, l, (i << r) + k + 1) - A;
-                // every 16th point: denser samples measured slower overall (strides 1, 4, 8,
-                // 16, 32, 64 tried) -- the 12-D gathers cost build time and did not buy
-                // better trees
-                constexpr int stride = 16;
                 // widest spread: the dimension of largest sample variance
                 float s1[D], s2[D];
 #pragma unroll
                 for (int d = 0; d < D; ++d) { s1[d] = 0.f; s2[d] = 0.f; }
                 int cnt = 0;
-                for (int e = a0 + lane * stride; e < a1; e += 64 * stride) {
+#if SE3ICP_TREE_LDS_SAMPLE
+                for (int j = lane; j < nsmp; j += 64) {
+                    const int e = s_spos[j];
+                    if ((int)(e < a0) | (int)(e >= a1)) continue;
+                    ++cnt;
+#pragma unroll
+                    for (int d = 0; d < D; ++d) {
+                        const float x = s_smp[d][j];
+                        s1[d] += x;
+                        s2[d] = fmaf(x, x, s2[d]);
+                    }
+                }
+#else
+                for (int e = a0 + lane * 16; e < a1; e += 64 * 16) {  // (round 4: every 16th point from the columns)
                     const int p = s_val[e];
                     ++cnt;
 #pragma unroll
@@ -885,6 +916,7 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
                         s2[d] = fmaf(x, x, s2[d]);
                     }
                 }
+#endif
                 for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
                 const float inv = cnt > 0 ? 1.f / (float)cnt : 0.f;
                 int best = 0;

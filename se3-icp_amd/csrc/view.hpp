@@ -70,6 +70,10 @@ struct View {
     float* fr32;   // [ld][12] their f32 copies (the 12-D trees' input)
     double* nrm64;
     double* conf64;
+    // [ld][8] geometry rows of the target points (x y z nx ny nz conf 0, normalized frame),
+    // written once per batch by k_geo_rows: k_reduce gathers one 64-B row per kept
+    // correspondence instead of seven 8-B words from seven SoA rows (one 128-B line each)
+    double* tgeo;
     int32_t* knn;
     // per-cloud f32 error-bound norms (float bits, atomicMax)
     // loop
@@ -163,6 +167,8 @@ void launch_nn(const View& v, int D, hipStream_t s);
 // words of View::cls for nchunks chunks (counts + per-XCD class lists)
 size_t nn_cls_words(int nchunks);
 void launch_trim(const View& v, hipStream_t s);
+// the target points' geometry rows (View::tgeo) from xyz64 / nrm64 / conf64
+void launch_geo_rows(const View& v, hipStream_t s);
 // reduce + (k_reduce_final) per-pair solve and loop state machine; next_phase[p] receives
 // pair p's phase in the next iteration (PHASE_IDLE: finished)
 struct PairState;
