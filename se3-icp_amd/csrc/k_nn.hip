@@ -47,7 +47,10 @@ using namespace loopdev;
 //   28.7 KB blocks): SE(3) NN -9 %.
 constexpr int kTPL = 4;        // targets per lane in the compacted leaf sweeps (kept in registers across queries)
 constexpr int kCompact = 40;   // a leaf wanted by at most this many lanes takes the compacted sweep (12-D and 3-D)
-constexpr int kSeedTargets = 1;  // first searches: seeded by a greedy tree descent and this many leaf targets
+#ifndef SE3ICP_SEED_TARGETS
+#define SE3ICP_SEED_TARGETS 1
+#endif
+constexpr int kSeedTargets = SE3ICP_SEED_TARGETS;  // first searches: seeded by a greedy tree descent and this many leaf targets
 
 // packed f32 pairs: v_pk_add_f32 / v_pk_fma_f32 issue two lanes' worth of f32 math per
 // instruction (the f32 vector peak of gfx950 assumes them)
@@ -224,6 +227,12 @@ constexpr int kSmall = 4;      // groups of at most this many queries are search
 constexpr int kSingleWaves = 4096;
 static_assert(kSingleWaves % 8 == 0, "single_list deals the list to the 8 XCDs in whole eighths of its waves");
 constexpr double kExpand = 1.0;      // search widening, in units of the query's displacement this iteration
+#ifndef SE3ICP_WIDEN_FROM
+#define SE3ICP_WIDEN_FROM 4
+#endif
+// first iteration of the SE(3) phase whose searches are widened for certificates (a run's
+// first search has no displacement yet and is a plain 1-NN search either way)
+constexpr int kWidenFrom = SE3ICP_WIDEN_FROM;
 
 // Cost-ordered dispatch of the SE(3) group waves: k_nn_prep files each group under its XCD
 // (the block -> XCD map of the run-dealt order) and a cost class (its wave's duration in the
@@ -338,7 +347,7 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
         }
     }
     float m = 0.f;
-    if (it >= 2) {
+    if ((int)(it >= 2) & ((int)(D == 3) | (int)(it - P->phase_start + 1 >= kWidenFrom))) {
         double Tp[12], Qp[3];
         load_hist(v, it - 1, pair, Tp);
         pose_point(Tp, mt[0], mt[1], mt[2], Qp);
