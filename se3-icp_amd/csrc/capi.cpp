@@ -36,9 +36,12 @@ int current_device() {
     return d;
 }
 
+// device = ordinal | slot << 8: slot s > 0 is a further engine on the same GPU (its own
+// stream and buffers), so independent batches can be queued side by side
 Engine* usable_engine(int device) {
     int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n) return nullptr;
+    const int ord = device & 0xff;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || ord >= n || (device >> 8) > 15) return nullptr;
     return engine_for(device);
 }
 

@@ -1132,7 +1132,7 @@ Engine* engine_for(int device) {
     std::lock_guard<std::mutex> lk(reg_mu);
     auto it = reg.find(device);
     if (it != reg.end()) return it->second.get();
-    auto e = std::make_unique<Engine>(device);
+    auto e = std::make_unique<Engine>(device & 0xff);  // (slots: see capi.cpp usable_engine)
     Engine* raw = e.get();
     reg[device] = std::move(e);
     return raw;
