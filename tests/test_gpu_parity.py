@@ -625,3 +625,30 @@ def test_lrf_fast_path_equals_exact_kernel_in_a_batch(se3icp_mod):
     for i, (a, b) in enumerate(zip(fast, exact)):
         assert np.array_equal(a.T, b.T), (i, a.T - b.T)
         assert (a.num_iterations, a.num_pure_se3_iterations) == (b.num_iterations, b.num_pure_se3_iterations)
+
+
+def test_engine_slots_are_independent_engines(se3icp_mod):
+    """device | slot << 8 selects a further engine on the same GPU (own stream and buffers,
+    capi.cpp usable_engine): two slots registering two halves of a batch from two host
+    threads return bitwise the poses of one call over the whole batch."""
+    import threading
+    from se3icp import datasets
+    pairs, _ = datasets.kitti_like_pairs(4, seed=4, n_az=600)
+    p = se3icp_mod.kitti_params()
+    whole = se3icp_mod.register_batch(pairs, "se3_gicp", p)
+    out = {}
+
+    def run(slot, part):
+        out[slot] = se3icp_mod.register_batch(part, "se3_gicp", p, device=slot << 8)
+
+    th = [threading.Thread(target=run, args=(s, pairs[2 * s:2 * s + 2])) for s in (1, 2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    got = out[1] + out[2]
+    for i, (a, b) in enumerate(zip(got, whole)):
+        assert np.array_equal(a.T, b.T), (i, a.T - b.T)
+        assert a.num_iterations == b.num_iterations
+    with pytest.raises(Exception):
+        se3icp_mod.register_batch(pairs[:1], "se3_gicp", p, device=(16 << 8))  # slots 0..15
