@@ -47,6 +47,9 @@ using namespace loopdev;
 //   28.7 KB blocks): SE(3) NN -9 %.
 constexpr int kTPL = 4;        // targets per lane in the compacted leaf sweeps (kept in registers across queries)
 constexpr int kCompact = 40;   // a leaf wanted by at most this many lanes takes the compacted sweep (12-D and 3-D)
+#ifndef SE3ICP_NN_KEYMERGE
+#define SE3ICP_NN_KEYMERGE 1
+#endif
 #ifndef SE3ICP_SEED_TARGETS
 #define SE3ICP_SEED_TARGETS 1
 #endif
@@ -189,6 +192,27 @@ __device__ __forceinline__ void compact_sweep(const float4* tile, const float4* 
             a1 = lt ? acc : a1;
             b1 = lt ? j : b1;
         }
+#if SE3ICP_NN_KEYMERGE
+        // the group's top-2: the best as one u64 key (f32 distance bits | target: the lowest
+        // index among equal distances), then the second-best distance as a plain minimum of
+        // every lane's best except the winner's, whose own second counts instead -- two
+        // butterflies of 5 + 2 VALU per step instead of one of ~12
+        {
+            const unsigned long long mine = ((unsigned long long)__float_as_uint(a1) << 32) | (unsigned)b1;
+            unsigned long long key = mine;
+#pragma unroll
+            for (int m = 1; m < LPQ; m <<= 1) {
+                const unsigned long long pk = xor_lane(key, m);
+                key = pk < key ? pk : key;
+            }
+            float c = key == mine ? a2 : a1;
+#pragma unroll
+            for (int m = 1; m < LPQ; m <<= 1) c = fmin_raw(c, xor_lane(c, m));
+            a1 = __uint_as_float((unsigned)(key >> 32));
+            b1 = (int)(unsigned)key;
+            a2 = c;
+        }
+#else
 #pragma unroll
         for (int m = 1; m < LPQ; m <<= 1) {
             const float p1 = xor_lane(a1, m), p2 = xor_lane(a2, m);
@@ -198,6 +222,7 @@ __device__ __forceinline__ void compact_sweep(const float4* tile, const float4* 
             b1 = lt ? pb : b1;
             a1 = fmin_raw(a1, p1);
         }
+#endif
         if ((int)(sub == 0) & (int)(slot < w)) {
             r1[qi] = a1;
             r2[qi] = a2;

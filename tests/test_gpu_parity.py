@@ -641,7 +641,7 @@ def test_engine_slots_are_independent_engines(se3icp_mod):
     def run(slot, part):
         out[slot] = se3icp_mod.register_batch(part, "se3_gicp", p, device=slot << 8)
 
-    th = [threading.Thread(target=run, args=(s, pairs[2 * s:2 * s + 2])) for s in (1, 2)]
+    th = [threading.Thread(target=run, args=(s, pairs[2 * s - 2:2 * s])) for s in (1, 2)]
     for t in th:
         t.start()
     for t in th:
