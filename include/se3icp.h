@@ -136,7 +136,10 @@ int se3icp_get_result(const se3icp_registration* r, se3icp_result* out);
 
 /* ------------------------------------------------------------- batch surface
  * Register n_pairs independent (source, target) pairs with one method and one
- * parameter set, on device `device` (HIP ordinal).  Host buffers. */
+ * parameter set, on device `device` (HIP ordinal).  Host buffers.
+ * Every entry taking `device` accepts `ordinal | slot << 8` (slot 0..15): slot s > 0 is a
+ * further engine on the same GPU with its own stream and buffers, so independent batches
+ * may be registered from several host threads at once (one engine serialises its calls). */
 int se3icp_register_batch(int device, int32_t n_pairs, const double* const* src_xyz, const int64_t* n_src,
                           const double* const* tgt_xyz, const int64_t* n_tgt, int method,
                           const se3icp_params* params, se3icp_result* results);

@@ -533,21 +533,38 @@ __device__ __forceinline__ void corr_terms(int est, bool cf, const double* T, co
 // The target points' geometry rows for k_reduce's gathers (View::tgeo): one 64-B row per
 // point of a target cloud -- a kept correspondence then touches one 128-B line of target
 // data instead of up to seven (measured: every fabric read on gfx950 is a 128-B request,
-// profiles/r05_fetch_calib.json).  Four lanes per row, one 16-B part each, so every store
-// instruction writes 1 KB of consecutive rows; source clouds are skipped (their rows are
-// never read).
+// profiles/r05_fetch_calib.json).  A lane per row reads the SoA columns (coalesced), the
+// wave's 64 rows are transposed through LDS so that every store instruction writes 1 KB of
+// consecutive rows (four lanes per row end to end: 361 us per 64-pair batch against 300 us
+// for one lane per row storing its own 64 B; source clouds are skipped, their rows are never
+// read).
 __global__ __launch_bounds__(256) void k_geo_rows(View v) {
-    const int i = blockIdx.x * 64 + (int)(threadIdx.x >> 2), part = (int)(threadIdx.x & 3);
-    if (i >= v.npts) return;
-    const CloudSetup* st = v.setup + v.cloud_of[i];
-    if (!st->is_target) return;
-    const size_t ld = v.ld;
-    double2 r;
-    if (part == 0) r = make_double2(v.xyz64[i], v.xyz64[ld + i]);
-    else if (part == 1) r = make_double2(v.xyz64[2 * ld + i], v.nrm64[i]);
-    else if (part == 2) r = make_double2(v.nrm64[ld + i], v.nrm64[2 * ld + i]);
-    else r = make_double2(st->want_conf ? v.conf64[i] : 0.0, 0.0);
-    reinterpret_cast<double2*>(v.tgeo)[(size_t)i * 4 + part] = r;
+    __shared__ double2 s_rows[4][64 * 4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int r0 = (blockIdx.x * 4 + wv) * 64;  // the wave's first row
+    const int i = r0 + lane;
+    bool tgt = false;
+    if (i < v.npts) {
+        const CloudSetup* st = v.setup + v.cloud_of[i];
+        tgt = st->is_target != 0;
+        if (tgt) {
+            const size_t ld = v.ld;
+            double2* r = &s_rows[wv][lane * 4];
+            r[0] = make_double2(v.xyz64[i], v.xyz64[ld + i]);
+            r[1] = make_double2(v.xyz64[2 * ld + i], v.nrm64[i]);
+            r[2] = make_double2(v.nrm64[ld + i], v.nrm64[2 * ld + i]);
+            r[3] = make_double2(st->want_conf ? v.conf64[i] : 0.0, 0.0);
+        }
+    }
+    const unsigned long long tm = __ballot(tgt);
+    __builtin_amdgcn_wave_barrier();
+    if (tm == 0ull) return;
+    double2* out = reinterpret_cast<double2*>(v.tgeo) + (size_t)r0 * 4;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int e = k * 64 + lane;  // part e & 3 of row e >> 2
+        if ((tm >> (e >> 2)) & 1ull) out[e] = s_rows[wv][e];
+    }
 }
 
 // Block b sums the terms of its pair's queries q0 + threadIdx.x + kRedThreads u (u < kRedPer,
@@ -722,7 +739,7 @@ void launch_trim(const View& v, hipStream_t s) {
     hipLaunchKernelGGL(k_trim, dim3(v.npairs), dim3(1024), 0, s, v);
 }
 void launch_geo_rows(const View& v, hipStream_t s) {
-    if (v.npts > 0) hipLaunchKernelGGL(k_geo_rows, dim3((v.npts + 63) / 64), dim3(256), 0, s, v);
+    if (v.npts > 0) hipLaunchKernelGGL(k_geo_rows, dim3((v.npts + 255) / 256), dim3(256), 0, s, v);
 }
 void launch_reduce(const View& v, const int32_t* pair_wb, const int32_t* pair_wn, PairState* state, double* hist,
                    int32_t* next_phase, hipStream_t s) {

@@ -722,8 +722,14 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(6))) vo
                 PROF8_ADD(c_tight, t_t0, t_t1);
                 do_tighten = false;
                 tf = thr_f();  // the box-test bound changes only here
+#if defined(SE3ICP_LRF8_CUT) && SE3ICP_LRF8_CUT == 4
+                if (stage == 2) break;  // (measurement build: stop after the first bound)
+#endif
             }
             if (cur >= 0) {  // appending leaf cur (part)
+#if defined(SE3ICP_LRF8_CUT) && SE3ICP_LRF8_CUT == 5
+                if (stage >= 2) { cur = -1; part = 0; ++n_leaves; continue; }  // (measurement build: no scans after the first bound)
+#endif
                 if (scan_leaf(cur, part)) {
                     if (part == 1) part = 2;
                     else { cur = -1; part = 0; }
@@ -806,7 +812,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(6))) vo
     __builtin_amdgcn_wave_barrier();
 
     PROF8_NOW(t_a1);
-#if defined(SE3ICP_LRF8_CUT) && SE3ICP_LRF8_CUT == 1
+#if defined(SE3ICP_LRF8_CUT) && (SE3ICP_LRF8_CUT == 1 || SE3ICP_LRF8_CUT == 4 || SE3ICP_LRF8_CUT == 5)
     if (lane == 0 && n_leaves == 12345u) v.stats[0] = nlist;  // (measurement build: stop after the traversal)
     return;
 #endif
