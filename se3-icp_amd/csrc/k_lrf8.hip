@@ -46,6 +46,13 @@ using namespace knn;
 constexpr int kW = 4;     // waves per block
 constexpr int kQ = 8;     // queries per wave (eight lanes each in the group phases)
 constexpr int kCap = 192; // candidates buffered per query (u32: cut key | candidate id)
+#ifndef SE3ICP_LRF8_FILL
+#define SE3ICP_LRF8_FILL 192
+#endif
+// the accept-all fill stops before a leaf would pass this (round 5, C4 64 pairs: 128 or 160
+// instead of 192 -- a cheaper first tightening from fewer points -- made k_lrf8 8 % slower:
+// the looser first bound opens more leaves and costs more tightenings later)
+constexpr int kFill = SE3ICP_LRF8_FILL;
 // LDS stride of the lists: 196 entries = 49 16-B slots, odd, so that the lane-major
 // ds_read_b128 of a 128-entry run (lane l of group g: entries 16 l .. 16 l + 15) puts every
 // 16-lane bank group on 16 distinct slots of the 256-B bank row (conflict-free), and the
@@ -759,7 +766,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(6))) vo
                 const bool more_hi = s_hi < nleaf - 1, more_lo = s_lo > 0;
                 const int cand = (more_hi && (up || !more_lo)) ? s_hi + 1 : s_lo - 1;
                 const int csz = (more_hi || more_lo) ? tree_first(n, T.L, cand + 1) - tree_first(n, T.L, cand) : 0;
-                if ((more_hi || more_lo) && ((int)nbq[0] < Kw || (int)nbq[0] + csz <= kCap)) {
+                if ((more_hi || more_lo) && ((int)nbq[0] < Kw || (int)nbq[0] + csz <= kFill)) {
                     leaf = cand;
                     if (cand > s_hi) s_hi = cand; else s_lo = cand;
                     up = !up;

@@ -46,7 +46,10 @@ using namespace loopdev;
 //   4-wave blocks whose waves ended at different times stranded LDS (a CU held at most five
 //   28.7 KB blocks): SE(3) NN -9 %.
 constexpr int kTPL = 4;        // targets per lane in the compacted leaf sweeps (kept in registers across queries)
-constexpr int kCompact = 40;   // a leaf wanted by at most this many lanes takes the compacted sweep (12-D and 3-D)
+#ifndef SE3ICP_NN_COMPACT
+#define SE3ICP_NN_COMPACT 40
+#endif
+constexpr int kCompact = SE3ICP_NN_COMPACT;  // a leaf wanted by at most this many lanes takes the compacted sweep (12-D and 3-D)
 #ifndef SE3ICP_NN_KEYMERGE
 #define SE3ICP_NN_KEYMERGE 1
 #endif
