@@ -45,9 +45,15 @@ using namespace knn;
 
 constexpr int kW = 4;     // waves per block
 constexpr int kQ = 8;     // queries per wave (eight lanes each in the group phases)
-constexpr int kCap = 192; // candidates buffered per query (u32: cut key | candidate id)
+#ifndef SE3ICP_LRF8_CAP
+#define SE3ICP_LRF8_CAP 192
+#endif
+// candidates buffered per query (u32: cut key | candidate id); round 5, C4 64 pairs: 224
+// (5 waves per SIMD) +7 %, 256 (4 waves) +22 % k_lrf8 time -- occupancy beats the tighter
+// first bound a larger accept-all fill gives
+constexpr int kCap = SE3ICP_LRF8_CAP;
 #ifndef SE3ICP_LRF8_FILL
-#define SE3ICP_LRF8_FILL 192
+#define SE3ICP_LRF8_FILL SE3ICP_LRF8_CAP
 #endif
 // the accept-all fill stops before a leaf would pass this (round 5, C4 64 pairs: 128 or 160
 // instead of 192 -- a cheaper first tightening from fewer points -- made k_lrf8 8 % slower:
@@ -57,7 +63,8 @@ constexpr int kFill = SE3ICP_LRF8_FILL;
 // ds_read_b128 of a 128-entry run (lane l of group g: entries 16 l .. 16 l + 15) puts every
 // 16-lane bank group on 16 distinct slots of the 256-B bank row (conflict-free), and the
 // lane-major ds_read_b32 of an unaligned run is 4-way instead of 16-way
-constexpr int kStride = 196;
+constexpr int kStride = kCap + 4;
+static_assert(((kStride / 4) & 1) == 1, "an odd number of 16-B slots per list");
 constexpr int kLeaves = 64;              // leaves one wave may scan: candidate id = (list index << 6) | lane
 constexpr unsigned kIdBits = 0xfffu;     // low bits of a list entry: the candidate id
 // bound of the accept-all phase: every finite key (a lane past the leaf's end carries an
@@ -476,7 +483,7 @@ __device__ __forceinline__ bool final_group(unsigned* lists, const int* leaf_slo
 static_assert(kW >= 2 && kW * kQ <= 64, "the per-block epilogue: waves 0 and 1, a lane per query");
 
 // waves per SIMD: 6 = the LDS limit (26.6 KB per block); A/B 4 -> 5 -> 6: 6.73 -> 6.45 -> 6.38 ms
-__global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(6))) void k_lrf8(
+__global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <= 192 ? 6 : (kCap <= 224 ? 5 : 4)))) void k_lrf8(
     View v, const int32_t* __restrict__ cloud_of, const CloudSetup* __restrict__ setup,
     const CloudDev* __restrict__ clouds, const float* __restrict__ tlo, const float* __restrict__ thi,
     const double4* __restrict__ P4, const int32_t* __restrict__ wave_base, int w_lo, int nwaves,
@@ -530,7 +537,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(6))) vo
         qn = min(kQ, cl.off + cl.n - w0);
         if (K > 0 && qn > 0) {
             Kw = min(K, cl.n);
-            mode = (qn == kQ && Kw <= kCap - 64) ? 1 : 2;
+            mode = (qn == kQ && Kw <= 128) ? 1 : 2;  // (the final order holds <= 128 entries)
         }
     }
     bool fb_wave = mode == 2;
@@ -601,7 +608,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(6))) vo
             anyz |= mj == 0;
         }
         const bool presort = anyz || dmax > 128;
-        const int tail_per = presort ? (nmax <= 128 ? 0 : 8) : (dmax == 0 ? 0 : dmax <= 64 ? 8 : 16);
+        const int tail_per = presort ? (nmax <= 128 ? 0 : (nmax <= 192 ? 8 : 16)) : (dmax == 0 ? 0 : dmax <= 64 ? 8 : 16);
         const uint3 r3 = tighten_group_sorted(lists, g, l, (int)group_len(), mvv, (int)nmax, Kw, presort, tail_per, s_norm);
         mvv = (int)r3.z;
         __builtin_amdgcn_wave_barrier();
