@@ -254,6 +254,11 @@ constexpr int kSmall = 4;      // groups of at most this many queries are search
 // faster than 16,384 at C4: fewer empty waves to dispatch in iterations without sparse chunks)
 constexpr int kSingleWaves = 4096;
 static_assert(kSingleWaves % 8 == 0, "single_list deals the list to the 8 XCDs in whole eighths of its waves");
+#ifndef SE3ICP_NN_THB
+#define SE3ICP_NN_THB 1
+#endif
+constexpr float kBoxScale = SE3ICP_NN_THB ? 1.0000025f : 1.0f;  // (group search box tests, see thb)
+constexpr float kBoxMul = SE3ICP_NN_THB ? 1.0f : (1.f - 2e-6f);
 constexpr double kExpand = 1.0;      // search widening, in units of the query's displacement this iteration
 #ifndef SE3ICP_WIDEN_FROM
 #define SE3ICP_WIDEN_FROM 4
@@ -437,7 +442,6 @@ __device__ __forceinline__ int seed_descent(const View& v, const TreeRef& TR, co
         bd = fminf(d, bd);
     }
     return TR.perm[ct.off + best];
-    return false;
 }
 
 // One 1024-thread block per chunk (a node of level CL = GL - 4 of the source tree: 16
@@ -472,6 +476,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     const int pair = c >> v.chunk_level;
     const PairDev* P = v.pairs + pair;
     const int phase = P->phase;
+    // a finished pair's chunks have nothing to settle or list: the searches skip its groups
+    // by its phase, so its stale qcount rows are never read (block-uniform exit; the loop's
+    // last iterations run with few pairs left)
+    if (phase == PHASE_IDLE) return;
     const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (threadIdx.x < NL) s_cnt[threadIdx.x] = 0;
     __syncthreads();
@@ -741,6 +749,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
         float d1 = INFINITY, d2 = INFINITY;
         int i1 = -1;  // target tree position of the best candidate
         float thr = valid ? INFINITY : -1.f;
+        // box tests compare against thb = thr * kBoxScale instead of lb * (1 - 2e-6) < thr
+        // (one multiply per bound update instead of one per box): kBoxScale >= 1 / ((1 - 2e-6)
+        // (1 - 2^-24)^2), so every box the scaled form admits is still admitted (more visits at
+        // worst, never fewer)
+        float thb = thr;
         if (valid) {  // seed the pruning threshold with the previous match
             const int prev = v.corr_idx[g];
             if (prev >= 0 && prev < ct.n) {
@@ -754,6 +767,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
                 thr = widen(s, INFINITY);
             }
         }
+        thb = thr * kBoxScale;
 
         const float* box_lo = TR.lo + (size_t)P->tgt * TR.nnodes * D;
         const float* box_hi = TR.hi + (size_t)P->tgt * TR.nnodes * D;
@@ -769,22 +783,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
         const unsigned n_valid = (unsigned)__popcll(__ballot(valid));
         const unsigned long long t_w0 = __builtin_amdgcn_s_memrealtime();
     #endif
-        while (sp > 0) {
-            const int h = __builtin_amdgcn_readlane(stk, sp - 1);
-            --sp;
+        // a near leaf is swept right after its parent's box tests, with the lanes those tests
+        // admitted (no bound changed in between): no stack round trip, no box re-test
+        int pend = -1;
+        unsigned long long pendW = 0ull;
+        while ((int)(sp > 0) | (int)(pend >= 0)) {
+            int h;
+            const bool known = pend >= 0;
+            if (known) {
+                h = pend;
+                pend = -1;
+            } else {
+                h = __builtin_amdgcn_readlane(stk, sp - 1);
+                --sp;
+            }
             if (h >= first_leaf) {
                 const int li = h - first_leaf;
                 const int ta = tree_first(ct.n, TR.L, li), tb = tree_first(ct.n, TR.L, li + 1);
                 const int cnt = tb - ta;
                 if (cnt <= 0) continue;
                 // lanes whose own bound admits this leaf (box re-tested: the bounds shrank since the push)
-                unsigned long long W = ~0ull;
+                unsigned long long W = pendW;
                 int w = 64;
                 {
-                    float lbh;
-                    if constexpr (D == 12) lbh = box_lb12_u(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q2);
-                    else lbh = box_lb_u<D>(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q);
-                    W = __ballot(lbh * (1.f - 2e-6f) < thr);
+                    if (!known) {
+                        float lbh;
+                        if constexpr (D == 12) lbh = box_lb12_u(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q2);
+                        else lbh = box_lb_u<D>(box_lo + (size_t)h * D, box_hi + (size_t)h * D, q);
+                        W = __ballot(lbh * kBoxMul < thb);
+                    }
                     if (W == 0ull) continue;
                     w = __popcll(W);
                 }
@@ -854,7 +881,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
                         n_eval += kTPL * ((w + qpi - 1) / qpi);
                     }
                 }
-                if ((int)valid & (int)(d1 < INFINITY)) thr = fminf(thr, widen(d1, d2));
+                if ((int)valid & (int)(d1 < INFINITY)) {
+                    thr = fminf(thr, widen(d1, d2));
+                    thb = thr * kBoxScale;
+                }
     #ifdef SE3ICP_PROF
                 c_leaf += __builtin_amdgcn_s_memtime() - c_l0;
     #endif
@@ -871,13 +901,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
                 lr = box_lb_u<D>(box_lo + (size_t)hr * D, box_hi + (size_t)hr * D, q);
             }
             // the f32 bound is within (D+2) ulps of the exact distance to the (inflated) box
-            const bool vl = __ballot(ll * (1.f - 2e-6f) < thr) != 0ull;
-            const bool vr = __ballot(lr * (1.f - 2e-6f) < thr) != 0ull;
+            const unsigned long long Wl = __ballot(ll * kBoxMul < thb);
+            const unsigned long long Wr = __ballot(lr * kBoxMul < thb);
+            const bool vl = Wl != 0ull, vr = Wr != 0ull;
             const bool left_first = __builtin_amdgcn_readfirstlane(ll <= lr ? 1 : 0) != 0;
             const int nearh = left_first ? hl : hr, farh = left_first ? hr : hl;
             const bool vnear = left_first ? vl : vr, vfar = left_first ? vr : vl;
             if (vfar) { stk = (lane == sp) ? farh : stk; ++sp; }
-            if (vnear) { stk = (lane == sp) ? nearh : stk; ++sp; }
+            if (vnear) {
+                if (hl >= first_leaf) {  // (children are leaves)
+                    pend = nearh;
+                    pendW = left_first ? Wl : Wr;
+                } else {
+                    stk = (lane == sp) ? nearh : stk;
+                    ++sp;
+                }
+            }
         }
 
         if (lane == 0) {  // 64 lanes per evaluation; 64 counter slots against contention
