@@ -8,7 +8,8 @@ second to last, i.e. a timed step of bench.py rather than its extra profiled one
 setup / loop split, the time the GPU runs no kernel at all (union of dispatch intervals),
 and per kernel name: dispatches, summed duration, and the idle time in front of its
 dispatches (gap from the previous kernel's end to its start when nothing ran).
---full lists every dispatch of the step.
+--full lists every dispatch of the step; --iterations one line per loop iteration (from
+one k_nn_prep to the next): its span, the time no kernel ran, and each kernel's duration.
 """
 import argparse
 import collections
@@ -37,6 +38,7 @@ def main():
     ap.add_argument("trace_dir")
     ap.add_argument("--step", type=int, default=-2)
     ap.add_argument("--full", action="store_true")
+    ap.add_argument("--iterations", action="store_true")
     a = ap.parse_args()
     rows = load(a.trace_dir)
     starts = [i for i, r in enumerate(rows) if "k_ingest" in r[2]]
@@ -74,6 +76,18 @@ def main():
     print(f"{'kernel':40s} {'n':>5s} {'busy ms':>9s} {'avg us':>8s} {'idle-before ms':>15s}")
     for k, (c, b, g) in sorted(per.items(), key=lambda kv: -kv[1][1]):
         print(f"{k[:40]:40s} {c:5d} {b / 1e6:9.3f} {b / c / 1e3:8.1f} {g / 1e6:15.3f}")
+    if a.iterations:
+        its = []
+        for r in seg[loop_i:]:
+            if "k_nn_prep" in r[2] or not its:
+                its.append([])
+            its[-1].append(r)
+        print("\nper loop iteration (us): span, idle (no kernel running), then each dispatch")
+        for k, it in enumerate(its):
+            span = max(e for _, e, _ in it) - it[0][0]
+            busy = sum(e - s for s, e, _ in it)
+            ks = " ".join(f"{short(n).replace('k_', '')}:{(e - s) / 1e3:.1f}" for s, e, n in it)
+            print(f"{k:3d} span {span / 1e3:8.1f} idle {(span - busy) / 1e3:6.1f} | {ks}")
 
 
 if __name__ == "__main__":
