@@ -663,6 +663,11 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce(View v) {
 // So the slot is the only value the host may read without ordering: any host read of
 // other device state after finish() must stay stream-ordered (an async copy on the stream,
 // then a sync), as the engine's result copies are.
+#ifdef SE3ICP_PROF
+// k_reduce_final phases summed over launches and pairs (100 MHz ticks): [0] the block
+// partials' sums, [1] the one-lane close / open of the iteration, [2] pair blocks
+__device__ unsigned long long g_fin_prof[4];
+#endif
 constexpr int kFinThreads = 512;                    // (the solve's ~220 VGPRs allow two waves per SIMD)
 constexpr int kFinChunks = kFinThreads / kRedVals;  // 18 interleaved chunks of block partials
 __global__ __launch_bounds__(kFinThreads) void k_reduce_final(View v, const int32_t* pair_wb, const int32_t* pair_wn,
@@ -677,8 +682,15 @@ __global__ __launch_bounds__(kFinThreads) void k_reduce_final(View v, const int3
     }
     __shared__ double part[kFinChunks][kRedVals];
     __shared__ double tot[kRedVals];
+#ifdef SE3ICP_PROF
+    const unsigned long long tf0 = __builtin_amdgcn_s_memrealtime();
+#endif
     const int i = threadIdx.x % kRedVals, s = threadIdx.x / kRedVals;
     const int wb = pair_wb[p], wn = pair_wn[p];
+    // the pair's loop state, loaded by the closing lane before the sums (its round trip
+    // overlaps them instead of following them)
+    PairState S;
+    if (threadIdx.x == 0) S = state[p];
     if (s < kFinChunks) {  // eight independent chains per lane: eight loads in flight
         constexpr int C = kFinChunks, U = 8;
         double s8[U];
@@ -708,8 +720,20 @@ __global__ __launch_bounds__(kFinThreads) void k_reduce_final(View v, const int3
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        PairState S = state[p];
+#ifdef SE3ICP_PROF
+        const unsigned long long tf1 = __builtin_amdgcn_s_memrealtime();
+#endif
+#ifdef SE3ICP_PROF
+        const int est_ = P->est;
+        __builtin_amdgcn_s_waitcnt(0);
+        asm volatile("" :: "v"(S.mse_cur), "s"(est_));
+        const unsigned long long tfa = __builtin_amdgcn_s_memrealtime();
+        pair_close_iteration(S, est_, tot);
+        asm volatile("" :: "v"(S.T.m[0][0]), "v"(S.T.m[2][3]));
+        const unsigned long long tfb = __builtin_amdgcn_s_memrealtime();
+#else
         pair_close_iteration(S, P->est, tot);
+#endif
         pair_open_iteration(S, *P);
         state[p] = S;
         if (!S.done) {
@@ -717,6 +741,14 @@ __global__ __launch_bounds__(kFinThreads) void k_reduce_final(View v, const int3
             for (int k = 0; k < 12; ++k) h[k] = P->T[k];
         }
         if (next_phase) next_phase[p] = P->phase;
+#ifdef SE3ICP_PROF
+        __builtin_amdgcn_s_waitcnt(0);
+        const unsigned long long tf2 = __builtin_amdgcn_s_memrealtime();
+        atomicAdd(&g_fin_prof[0], tf1 - tf0);
+        atomicAdd(&g_fin_prof[1], tf2 - tf1);
+        atomicAdd(&g_fin_prof[2], 1ull);
+        atomicAdd(&g_fin_prof[3], ((tfa - tf1) << 42) | ((tfb - tfa) << 21) | (tf2 - tfb));
+#endif
     }
 }
 
@@ -732,6 +764,14 @@ void trim_prof_report() {
                  h[6] ? h[3] / 100.0 / h[6] : 0.0, h[6] ? h[4] / 100.0 / h[6] : 0.0);
     const unsigned long long z[8] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_trim_prof), z, sizeof(z));
+    unsigned long long f[4];
+    if (hipMemcpyFromSymbol(f, HIP_SYMBOL(g_fin_prof), sizeof(f)) == hipSuccess && f[2]) {
+        std::fprintf(stderr, "[prof] k_reduce_final per pair block (us): partial sums %.2f, close/open %.2f (state load %.2f, "
+                     "close %.2f, open + stores %.2f) (%llu)\n",
+                     f[0] / 100.0 / f[2], f[1] / 100.0 / f[2], (double)(f[3] >> 42) / 100.0 / f[2],
+                     (double)((f[3] >> 21) & 0x1fffff) / 100.0 / f[2], (double)(f[3] & 0x1fffff) / 100.0 / f[2], f[2]);
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_fin_prof), z, sizeof(f));
+    }
 #endif
 }
 void launch_trim(const View& v, hipStream_t s) {
