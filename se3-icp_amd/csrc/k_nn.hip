@@ -234,11 +234,25 @@ __device__ __forceinline__ void compact_sweep(const float4* tile, const float4* 
     }
 }
 
-// chunks with at least kDense searched queries are searched 64 per wave, sparser ones one query per wave (k_nn_search)
-// (measured: a 12-D wave-per-query search costs ~5x the lanes' share of a group's, a 3-D
-// one far more, but a group's latency bounds an iteration with few groups; A/B 64 / 128 /
-// 256 within 1 % of each other with one-wave group blocks)
-constexpr int kDense = 256;
+// A chunk with at least dense_min searched queries is searched 64 per wave, a sparser one
+// one query per wave (k_nn_search's first kSingleWaves blocks).  A wave-per-query search costs
+// far more wave time per query than a group's lane (C4 64 pairs, make prof: ~10 us against
+// ~0.6 us in the 3-D search), but its latency is short, and with few groups a group wave's
+// latency bounds the launch.  The single-query list is served by a fixed 4,096 waves, so the
+// threshold scales down with the batch: dense_min = kDense * 1024 / nchunks in [kDenseMin,
+// kDense] -- 256 for 8 KITTI pairs (1,024 chunks), 32 for 64.  Same-box A/B at a fixed
+// threshold (iter/s): 64 pairs 256 / 128 / 64 / 32 = 13,500 / 13,870 / 14,060 / 14,080;
+// 8 pairs 10,570 / 10,420 / 10,340 / 10,180.
+#ifndef SE3ICP_NN_DENSE
+#define SE3ICP_NN_DENSE 256
+#endif
+#ifndef SE3ICP_NN_DENSE_MIN
+#define SE3ICP_NN_DENSE_MIN 32
+#endif
+constexpr int kDense = SE3ICP_NN_DENSE, kDenseMin = SE3ICP_NN_DENSE_MIN;
+__device__ __forceinline__ int dense_min(int nchunks) {
+    return max(kDenseMin, min(kDense, (int)(((long long)kDense * 1024) / max(nchunks, 1))));
+}
 constexpr int kWpe = 4;        // waves per SIMD of k_nn_search (its natural 128 VGPRs; 5 measured +8 %)
 // the 3-D search at 6 waves per SIMD (79 VGPRs, no scratch): same-box A/B x2, C2 (72 R3
 // iterations) 25,957 -> 26,257 iter/s, C4 within noise; 8 (64 VGPRs, 52 B of scratch) +0.8 %
@@ -253,6 +267,11 @@ constexpr int kSmall = 4;      // groups of at most this many queries are search
 // one-query-per-wave blocks at the front of the search grid (grid-strided; 4,096 measured
 // faster than 16,384 at C4: fewer empty waves to dispatch in iterations without sparse chunks)
 constexpr int kSingleWaves = 4096;
+#ifndef SE3ICP_SINGLE_BATCH
+#define SE3ICP_SINGLE_BATCH 16
+#endif
+constexpr int kSingleBatch = SE3ICP_SINGLE_BATCH;  // single-list entries set up together (1: one at a time)
+static_assert(kSingleBatch >= 1 && kSingleBatch <= 64, "one lane per entry");
 static_assert(kSingleWaves % 8 == 0, "single_list deals the list to the 8 XCDs in whole eighths of its waves");
 #ifndef SE3ICP_NN_THB
 #define SE3ICP_NN_THB 1
@@ -458,6 +477,9 @@ __device__ unsigned long long g_prep_span[2] = {~0ull, 0ull};
 // the launch span (earliest wave start, latest wave end)
 __device__ unsigned long long g_wave_hist[2][41];
 __device__ unsigned long long g_wave_span[2] = {~0ull, 0ull};
+// 3-D search waves per launch: [0] group waves, [1] single-query-list waves: count, summed
+// ticks, longest wave (ticks), queries
+__device__ unsigned long long g_r3_prof[2][4];
 #endif
 // (8 waves per SIMD: two 1024-thread blocks per CU, <= 64 VGPRs)
 // publish (may be null): the host's ring slot of the previous iteration, which receives
@@ -547,7 +569,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
         const int total = base;
         // a sparse chunk goes to the one-query-per-wave kernel instead (SE(3) list from the
         // front of sq_list, R3 from the back)
-        const bool dense = total >= kDense;
+        const bool dense = total >= dense_min(v.nchunks);
         if (lane < NL) {
             s_slot[lane] = slot_l;
             s_base[lane] = base_l;
@@ -644,7 +666,7 @@ __device__ __forceinline__ void nn_finish(const View& v, const PairDev* P, int p
 template <int D>
 __device__ __forceinline__ void single_one(const View& v, const PairDev* P, int pair, const TreeRef& TR,
                                            const CloudDev& ct, int gx, int g, int lane, unsigned* n_eval,
-                                           unsigned* n_box);
+                                           unsigned* n_box, int tp_pre = -2, float mrg_pre = 0.f);
 
 template <int D>
 __device__ __forceinline__ void single_list(const View& v, int bw);
@@ -942,6 +964,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
                 atomicAdd(v.stats + kStatCols * (gi & 63) + 12, c_leaf);   // shader cycles in leaf visits,
                 atomicAdd(v.stats + kStatCols * (gi & 63) + 14, c_lload);  // in their target loads,
                 atomicAdd(v.stats + kStatCols * (gi & 63) + 13, __builtin_amdgcn_s_memtime() - c_w0);  // in the wave
+            } else {
+                const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t_w0;
+                atomicAdd(&g_r3_prof[0][0], 1ull);
+                atomicAdd(&g_r3_prof[0][1], dt);
+                atomicMax(&g_r3_prof[0][2], dt);
+                atomicAdd(&g_r3_prof[0][3], (unsigned long long)n_valid);
             }
     #endif
         }
@@ -997,9 +1025,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
 // open one) and a target per lane in the leaf sweeps; each lane keeps the top-2 of the
 // targets it evaluated, the wave's (d1, d2) are two wave minima per leaf.
 template <int D>
+// tp_pre: the previous match's target tree position (-1 none) and mrg_pre the query's margin,
+// when the caller fetched them already (single_list); -2: load them here.
 __device__ __forceinline__ void single_one(const View& v, const PairDev* P, int pair, const TreeRef& TR,
                                            const CloudDev& ct, int gx, int g, int lane, unsigned* n_eval,
-                                           unsigned* n_box) {
+                                           unsigned* n_box, int tp_pre, float mrg_pre) {
     float q[D];
     float na;
     {
@@ -1020,7 +1050,7 @@ __device__ __forceinline__ void single_one(const View& v, const PairDev* P, int 
     f32x2 q2[(D + 1) / 2];
 #pragma unroll
     for (int r = 0; r < D / 2; ++r) q2[r] = f32x2{q[2 * r], q[2 * r + 1]};
-    const float mrg = v.cert[gx].margin;
+    const float mrg = tp_pre == -2 ? v.cert[gx].margin : mrg_pre;
     auto widen = [&](float a1, float a2) __attribute__((always_inline)) {
         const float e = sqrtf(a1) + 2.f * mrg;
         const float t = fmaxf(a1, fminf(e * e, a2));
@@ -1030,9 +1060,12 @@ __device__ __forceinline__ void single_one(const View& v, const PairDev* P, int 
     const size_t ld = v.ld;
     float thr = INFINITY;
     {  // seed with the previous match
-        const int prev = v.corr_idx[g];
-        if (prev >= 0 && prev < ct.n) {
-            const int tp = TR.pos[ct.off + prev];
+        int tp = tp_pre;
+        if (tp_pre == -2) {
+            const int prev = v.corr_idx[g];
+            tp = (prev >= 0 && prev < ct.n) ? TR.pos[ct.off + prev] : -1;
+        }
+        if (tp >= 0) {
             float s = 0.f;
 #pragma unroll
             for (int r = 0; r < D; ++r) {
@@ -1127,20 +1160,56 @@ __device__ __forceinline__ void single_list(const View& v, int bw) {
     const int nq = __builtin_amdgcn_readfirstlane(v.flag_count[D == 12 ? 1 : 2]);
     if (nq <= 0) return;
     constexpr int nbx = kSingleWaves >> 3;  // waves per XCD
+#ifdef SE3ICP_PROF
+    const unsigned long long t_s0 = __builtin_amdgcn_s_memrealtime();
+    unsigned n_sq = 0;
+#endif
     const int xcd = bw & 7;
     const int seg = (nq + 7) >> 3;
     const int f_end = min(nq, (xcd + 1) * seg);
     const int w0 = __builtin_amdgcn_readfirstlane(xcd * seg + (bw >> 3));
     unsigned n_eval = 0, n_box = 0;
-    for (int f = w0; f < f_end; f += nbx) {
-        const int gx = __builtin_amdgcn_readfirstlane(D == 12 ? v.sq_list[f] : v.sq_list[v.ld - 1 - f]);
-        const int pair = v.cloud_of[gx] >> 1;
-        const PairDev* P = v.pairs + pair;
-        const CloudDev cs = v.clouds[P->src], ct = v.clouds[P->tgt];
-        const TreeRef TR = (D == 12) ? v.t12 : v.t3;
-        const int g = cs.off + TR.perm[gx];
-        single_one<D>(v, P, pair, TR, ct, gx, g, lane, &n_eval, &n_box);
+    const TreeRef TR = (D == 12) ? v.t12 : v.t3;
+    // The wave's next kSingleBatch list entries are set up together, one per lane (list entry
+    // -> point -> pair -> clouds -> previous match -> its tree position, and the margin: a
+    // chain of dependent loads each query otherwise waited for in turn), then searched one
+    // after the other by the whole wave.
+    for (int f0 = w0; f0 < f_end; f0 += kSingleBatch * nbx) {
+        const int fj = f0 + lane * nbx;
+        int gxj = 0, gj = 0, pj = 0, tpj = -1;
+        float mj = 0.f;
+        if ((int)(lane < kSingleBatch) & (int)(fj < f_end)) {
+            gxj = D == 12 ? v.sq_list[fj] : v.sq_list[v.ld - 1 - fj];
+            pj = v.cloud_of[gxj] >> 1;
+            const PairDev* Pj = v.pairs + pj;
+            const CloudDev csj = v.clouds[Pj->src], ctj = v.clouds[Pj->tgt];
+            gj = csj.off + TR.perm[gxj];
+            const int prev = v.corr_idx[gj];
+            tpj = (prev >= 0 && prev < ctj.n) ? TR.pos[ctj.off + prev] : -1;
+            mj = v.cert[gxj].margin;
+        }
+        const int nbq = min(kSingleBatch, (f_end - f0 + nbx - 1) / nbx);
+        for (int j = 0; j < nbq; ++j) {
+            const int gx = __builtin_amdgcn_readlane(gxj, j), g = __builtin_amdgcn_readlane(gj, j);
+            const int pair = __builtin_amdgcn_readlane(pj, j), tp = __builtin_amdgcn_readlane(tpj, j);
+            const float mrg = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mj), j));
+            const PairDev* P = v.pairs + pair;
+            const CloudDev ct = v.clouds[P->tgt];
+            single_one<D>(v, P, pair, TR, ct, gx, g, lane, &n_eval, &n_box, kSingleBatch > 1 ? tp : -2, mrg);
+#ifdef SE3ICP_PROF
+            ++n_sq;
+#endif
+        }
     }
+#ifdef SE3ICP_PROF
+    if ((int)(D == 3) & (int)(lane == 0) & (int)(n_sq > 0)) {
+        const unsigned long long dt = __builtin_amdgcn_s_memrealtime() - t_s0;
+        atomicAdd(&g_r3_prof[1][0], 1ull);
+        atomicAdd(&g_r3_prof[1][1], dt);
+        atomicMax(&g_r3_prof[1][2], dt);
+        atomicAdd(&g_r3_prof[1][3], (unsigned long long)n_sq);
+    }
+#endif
     if ((int)(lane == 0) & (int)(n_eval + n_box > 0)) {
         unsigned long long* st = v.stats + kStatCols * (w0 & 63) + (D == 12 ? 0 : 2);
         atomicAdd(st, 64ull * n_eval);
@@ -1175,6 +1244,15 @@ void nn_wave_report(int it) {
     for (int b = 0; b < 41; ++b)
         if (h[0][b]) std::fprintf(stderr, " %d:%llu/%.1f%%", 25 * b, h[0][b], 100.0 * (double)h[1][b] / std::max(tot, 1.0));
     std::fprintf(stderr, "\n");
+    unsigned long long r3[2][4];
+    if (hipMemcpyFromSymbol(r3, HIP_SYMBOL(g_r3_prof), sizeof(r3)) == hipSuccess && (r3[0][0] | r3[1][0])) {
+        std::fprintf(stderr, "[nn] iter %d: R3 group waves %llu (%llu queries), mean %.1f us, longest %.1f us; single-list waves "
+                     "%llu (%llu queries), mean %.1f us, longest %.1f us\n", it, r3[0][0], r3[0][3],
+                     r3[0][0] ? r3[0][1] / 100.0 / r3[0][0] : 0.0, r3[0][2] / 100.0, r3[1][0], r3[1][3],
+                     r3[1][0] ? r3[1][1] / 100.0 / r3[1][0] : 0.0, r3[1][2] / 100.0);
+        const unsigned long long z3[2][4] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_r3_prof), z3, sizeof(z3));
+    }
     unsigned long long z[2][41] = {};
     const unsigned long long zs[2] = {~0ull, 0ull};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wave_hist), z, sizeof(z));
