@@ -263,7 +263,10 @@ __device__ __forceinline__ int group_xcd(int g, int nb) {
     const int whole = nb / (8 * kXcdRun) * (8 * kXcdRun);
     return g < whole ? (g / kXcdRun) & 7 : g & 7;
 }
-constexpr int kSmall = 4;      // groups of at most this many queries are searched one query at a time
+#ifndef SE3ICP_KSMALL
+#define SE3ICP_KSMALL 4
+#endif
+constexpr int kSmall = SE3ICP_KSMALL;  // groups of at most this many queries are searched one query at a time
 // one-query-per-wave blocks at the front of the search grid (grid-strided; 4,096 measured
 // faster than 16,384 at C4: fewer empty waves to dispatch in iterations without sparse chunks)
 constexpr int kSingleWaves = 4096;
@@ -279,12 +282,23 @@ static_assert(kSingleWaves % 8 == 0, "single_list deals the list to the 8 XCDs i
 constexpr float kBoxScale = SE3ICP_NN_THB ? 1.0000025f : 1.0f;  // (group search box tests, see thb)
 constexpr float kBoxMul = SE3ICP_NN_THB ? 1.0f : (1.f - 2e-6f);
 constexpr double kExpand = 1.0;      // search widening, in units of the query's displacement this iteration
+// First iteration of the SE(3) phase whose searches are widened for certificates (a run's
+// first search has no displacement yet and is a plain 1-NN search either way).  A widened
+// search costs more now and settles more queries in the next iterations: a large batch
+// (throughput-bound) gains from widening early, a small one (latency-bound: its longest
+// waves set the launches) loses.  Same-box A/B of the start iteration 4 / 3 / 2 (iter/s):
+// C4 KITTI 8 pairs 10,580 / 10,440 / 10,310, 16 pairs 11,700 / 11,820 / 11,770, 32 pairs
+// 13,270 / 13,500 / 13,490, 64 pairs 14,100 / 14,360 / 14,340; C3 (32 RGB-D pairs) 41,910 /
+// 42,870 / 41,310; C5 (256 RGB-D pairs) 55,220 / 57,330 / 58,350; C2 (8 bunny cases) 26,460 /
+// 26,240 / 26,030 -- the batch's pair count orders them (its chunk count does not: C3 and 8
+// KITTI pairs both have 1,024 chunks).  SE3ICP_WIDEN_FROM > 0 fixes it.
 #ifndef SE3ICP_WIDEN_FROM
-#define SE3ICP_WIDEN_FROM 4
+#define SE3ICP_WIDEN_FROM 0
 #endif
-// first iteration of the SE(3) phase whose searches are widened for certificates (a run's
-// first search has no displacement yet and is a plain 1-NN search either way)
-constexpr int kWidenFrom = SE3ICP_WIDEN_FROM;
+__device__ __forceinline__ int widen_from(int npairs) {
+    if (SE3ICP_WIDEN_FROM > 0) return SE3ICP_WIDEN_FROM;
+    return npairs >= 128 ? 2 : (npairs > 8 ? 3 : 4);
+}
 
 // Cost-ordered dispatch of the SE(3) group waves: k_nn_prep files each group under its XCD
 // (the block -> XCD map of the run-dealt order) and a cost class (its wave's duration in the
@@ -399,7 +413,7 @@ __device__ __forceinline__ bool prep_settle(const View& v, const TreeRef& TR, co
         }
     }
     float m = 0.f;
-    if ((int)(it >= 2) & ((int)(D == 3) | (int)(it - P->phase_start + 1 >= kWidenFrom))) {
+    if ((int)(it >= 2) & ((int)(D == 3) | (int)(it - P->phase_start + 1 >= widen_from(v.npairs)))) {
         double Tp[12], Qp[3];
         load_hist(v, it - 1, pair, Tp);
         pose_point(Tp, mt[0], mt[1], mt[2], Qp);
