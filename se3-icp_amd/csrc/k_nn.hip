@@ -281,7 +281,10 @@ static_assert(kSingleWaves % 8 == 0, "single_list deals the list to the 8 XCDs i
 #endif
 constexpr float kBoxScale = SE3ICP_NN_THB ? 1.0000025f : 1.0f;  // (group search box tests, see thb)
 constexpr float kBoxMul = SE3ICP_NN_THB ? 1.0f : (1.f - 2e-6f);
-constexpr double kExpand = 1.0;      // search widening, in units of the query's displacement this iteration
+#ifndef SE3ICP_EXPAND
+#define SE3ICP_EXPAND 1.0
+#endif
+constexpr double kExpand = SE3ICP_EXPAND;  // search widening, in units of the query's displacement this iteration
 // First iteration of the SE(3) phase whose searches are widened for certificates (a run's
 // first search has no displacement yet and is a plain 1-NN search either way).  A widened
 // search costs more now and settles more queries in the next iterations: a large batch
