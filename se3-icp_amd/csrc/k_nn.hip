@@ -311,6 +311,14 @@ __device__ __forceinline__ int widen_from(int npairs) {
 // step; C4 within noise; the R3 searches keep the run order -- ordered, C4's R3 NN was 10 %
 // slower: their short waves gain less than the L2 locality of the run order).
 constexpr int kClsHead = 2 * 8 * 16;  // counts [phase][XCD][class]
+// The 3-D group waves take the same cost-ordered dispatch in batches of at least
+// SE3ICP_NN_ORDER3 pairs (0: never): same-box A/B, ordered against the run order: C4 64
+// pairs +0.5 %, C5 (256 pairs) +1.0 %, C4 8 pairs -2.3 %, C2 -6 % (a small batch's short R3
+// waves gain less than the run order's L2 locality).
+#ifndef SE3ICP_NN_ORDER3
+#define SE3ICP_NN_ORDER3 64
+#endif
+__host__ __device__ inline bool order3(int npairs) { return (SE3ICP_NN_ORDER3 > 0) & (npairs >= SE3ICP_NN_ORDER3); }
 __host__ __device__ inline int cls_cap(int nchunks) { return nchunks * 16 / 8 + 1; }
 __device__ __forceinline__ int cost_class(unsigned t) {
     if (t == 0u) return 0;
@@ -592,9 +600,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
             s_base[lane] = base_l;
             v.qcount[c * NL + lane] = dense ? gcnt_l : 0;
         }
-        if ((int)dense & (int)(total > 0) & (int)(lane <= grp) & (int)(phase == PHASE_SE3)) {
+        if ((int)dense & (int)(total > 0) & (int)(lane <= grp) & ((int)(phase == PHASE_SE3) | ((int)order3(v.npairs) & (int)(phase == PHASE_R3)))) {
             const int g = c * NL + lane;
-            const int ph = 0;
+            const int ph = phase == PHASE_SE3 ? 0 : 1;
             const int row = (ph * 8 + group_xcd(g, v.nchunks * NL)) * 16 + cost_class(v.gcost[g]);
             const int at = atomicAdd(&v.cls[row], 1);
             v.cls[kClsHead + (size_t)row * cls_cap(v.nchunks) + at] = g;
@@ -1002,9 +1010,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
             recheck_one<D>(v, P, ct, __shfl(g, j, 64), __shfl(seed, j, 64), lane);
         }
     };
-    if (D == 12) {
+    if ((int)(D == 12) | (int)order3(v.npairs)) {
         const int bb = (int)blockIdx.x - kSingleWaves, x = bb & 7, i = bb >> 3;
-        const int row0 = x * 16;
+        const int row0 = ((D == 12 ? 0 : 1) * 8 + x) * 16;
         int acc = 0, k = -1, lo = 0;
         for (int j = 0; j < 16; ++j) {
             const int cj = __builtin_amdgcn_readfirstlane(v.cls[row0 + j]);
