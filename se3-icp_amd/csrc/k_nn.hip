@@ -308,8 +308,9 @@ __device__ __forceinline__ int widen_from(int npairs) {
 // previous search, half-octaves, longest first, unknown first); a group block then takes the
 // i-th item of its XCD's lists in class order, so the long waves start first and the
 // launch's tail is short waves (C2, two group waves per slot: SE(3) NN 8.4 -> 7.6 ms per
-// step; C4 within noise; the R3 searches keep the run order -- ordered, C4's R3 NN was 10 %
-// slower: their short waves gain less than the L2 locality of the run order).
+// step; C4 within noise).  The R3 searches of small batches keep the run order (ordered,
+// 8 KITTI pairs' R3 NN was 10 % slower: their short waves gain less than the L2 locality of
+// the run order); from 64 pairs they are ordered too (order3 below).
 constexpr int kClsHead = 2 * 8 * 16;  // counts [phase][XCD][class]
 // The 3-D group waves take the same cost-ordered dispatch in batches of at least
 // SE3ICP_NN_ORDER3 pairs (0: never): same-box A/B, ordered against the run order: C4 64
