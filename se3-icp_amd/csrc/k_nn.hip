@@ -702,7 +702,9 @@ __device__ __forceinline__ void single_list(const View& v, int bw);
 // launch's latency tail), the rest one 64-query group each.  (Round 3 ran the two parts as
 // two grids on two streams, joined by events: two extra launches and two cross-stream
 // waits per iteration.)
-template <int D>
+// ORD: the group waves take the cost-ordered lists (always for D = 12; for D = 3 in batches
+// of order3() pairs -- its own instantiation, so the run-order 3-D search keeps its registers)
+template <int D, bool ORD>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kWpe : kWpe3))) void k_nn_search(View v) {
     if (blockIdx.x < (unsigned)kSingleWaves) {
         single_list<D>(v, (int)blockIdx.x);
@@ -1011,7 +1013,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
             recheck_one<D>(v, P, ct, __shfl(g, j, 64), __shfl(seed, j, 64), lane);
         }
     };
-    if ((int)(D == 12) | (int)order3(v.npairs)) {
+    if constexpr (ORD) {
         const int bb = (int)blockIdx.x - kSingleWaves, x = bb & 7, i = bb >> 3;
         const int row0 = ((D == 12 ? 0 : 1) * 8 + x) * 16;
         int acc = 0, k = -1, lo = 0;
@@ -1300,8 +1302,9 @@ void launch_nn_prep(const View& v, int32_t* publish, hipStream_t s) {
 // kSingleWaves single-query waves, then 16 groups of 64 per chunk, one wave each
 void launch_nn(const View& v, int D, hipStream_t s) {
     const dim3 grid(kSingleWaves + v.nchunks * (kChunkQ / 64));
-    if (D == 12) hipLaunchKernelGGL(k_nn_search<12>, grid, dim3(64), 0, s, v);
-    else hipLaunchKernelGGL(k_nn_search<3>, grid, dim3(64), 0, s, v);
+    if (D == 12) hipLaunchKernelGGL((k_nn_search<12, true>), grid, dim3(64), 0, s, v);
+    else if (order3(v.npairs)) hipLaunchKernelGGL((k_nn_search<3, true>), grid, dim3(64), 0, s, v);
+    else hipLaunchKernelGGL((k_nn_search<3, false>), grid, dim3(64), 0, s, v);
 }
 
 }  // namespace se3icp
