@@ -381,7 +381,8 @@ def nn_roofline(ktot, kms, wl):
     flops = evals * flop_dist + boxes * flop_box
     achieved = flops / (t_ms / 1000.0) / 1e12 if t_ms > 0 else 0.0
     nl = max(1.0, nl)
-    traffic, src = pmc_traffic([f"k_nn_search<{D}>"], wl)
+    # ("k_nn_search<12" matches the kernel's instantiations, k_nn_search<12, true> since round 5)
+    traffic, src = pmc_traffic([f"k_nn_search<{D}"], wl)
     return {
         "kernel": kname,
         "bound": "valu",
