@@ -419,6 +419,33 @@ def test_c2_full_unique_bunny_se3_pt2pt(se3icp_mod, refcpu, bunny_unique):
     assert _rot_deg(g.T, T_gt) <= 2.0 and np.linalg.norm(g.T[:3, 3] - T_gt[:3, 3]) <= 0.25
 
 
+def test_c2_bench_workload_downsample_batch(se3icp_mod, refcpu, bunny_full):
+    """C2 as bench.py registers it (bench.py make_pairs): the reference's own problems
+    (B_SYN:91-160, its mt19937 / normal_distribution / RandomDownSample streams, pinned by
+    test_reference_streams) at RandomDownSample(0.2) of the 208,353-vertex bunny x50 =
+    41,670 points per cloud, easy ranges (B_SYN:106-108), noise var 0.005, the 8-case batch
+    registered together; cases 0 and 5 against their own oracle runs, case 5's
+    correspondences at every iteration."""
+    from se3icp import datasets
+    from test_gpu_trace import compare_traces
+    src, tgt, T_gt = datasets.synthetic_reference(bunny_full * 50.0, 8, ratio=0.2, noise_var=0.005, t_range=5.0,
+                                                  r_range=np.pi / 4)
+    assert src.shape == (8, 41670, 3)
+    pairs = [(src[i], tgt[i]) for i in range(8)]
+    res, gtr = se3icp_mod.register_batch_traced(pairs, "se3_pt2pt", se3icp_mod.cli_params(), pair=5)
+    for c in (0, 5):
+        ref = refcpu.register(src[c], tgt[c], refcpu.RUN_SE3_ICP, "pt2pt", refcpu.cli_params(),
+                              trace_iters=160 if c == 5 else 0, trace_margins=c == 5)
+        g = res[c]
+        assert np.linalg.norm(g.T - ref["T"]) <= 1e-5, (c, g.T, ref["T"])
+        assert (g.num_iterations, g.num_pure_se3_iterations) == (ref["num_iterations"],
+                                                                  ref["num_pure_se3_iterations"])
+        if c == 5:
+            compare_traces(gtr, ref, 1.0, "C2 bench workload case 5")
+    ok = sum(_rot_deg(r.T, T) <= 2.0 and np.linalg.norm(r.T[:3, 3] - T[:3, 3]) <= 0.25 for r, T in zip(res, T_gt))
+    assert ok >= 6, ok  # B_SYN:238-246 success thresholds on the easy ranges
+
+
 def test_c3_rgbd_batch32_se3_pt2pl(se3icp_mod, refcpu):
     """C3: a 32-pair se3_pt2pl batch of consecutive RGB-D frames at the default stride
     (~16k points, the lounge surrogate), examples/benchmark_lounge.cpp:183-189 parameters;
