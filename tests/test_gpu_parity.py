@@ -506,6 +506,30 @@ def test_batch_independence_16_vs_two_8(se3icp_mod):
         assert (f.num_iterations, f.num_pure_se3_iterations) == (h.num_iterations, h.num_pure_se3_iterations)
 
 
+@pytest.mark.parametrize("case", ["kitti64", "rgbd160"])
+def test_batch_independence_across_schedules(se3icp_mod, case):
+    """The NN scheduling adapts to the batch (k_nn.hip: the dense-chunk threshold from the
+    chunk count, the SE(3) phase's first widened search from the pair count -- from the 4th
+    iteration up to 8 pairs, the 3rd up to 127, the 2nd from 128 -- and the cost-ordered 3-D
+    dispatch from 64 pairs).  None of it may change a result: each large batch is bitwise
+    its pairs registered in 8- and 32-pair batches."""
+    from se3icp import datasets
+    if case == "kitti64":
+        pairs, _ = datasets.kitti_like_pairs(64, seed=4)
+        method, p, parts = "se3_gicp", se3icp_mod.kitti_params(), (8, 32)
+    else:
+        pairs, _ = datasets.rgbd_pairs(160, seed=5, stride=4)
+        method, p, parts = "se3_pt2pl", se3icp_mod.lounge_params(), (8, 32)
+    full = se3icp_mod.register_batch(pairs, method, p)
+    for size in parts:
+        got = []
+        for i in range(0, len(pairs), size):
+            got += se3icp_mod.register_batch(pairs[i:i + size], method, p)
+        for i, (f, h) in enumerate(zip(full, got)):
+            assert np.array_equal(f.T, h.T), (case, size, i, f.T - h.T)
+            assert (f.num_iterations, f.num_pure_se3_iterations) == (h.num_iterations, h.num_pure_se3_iterations)
+
+
 def test_profiled_and_event_modes_equal_the_plain_loop(se3icp_mod):
     """Per-stage HIP events (se3icp_set_profiling) and the SE(3) NN bracket
     (se3icp_set_nn_events) change only how the host follows the loop, never its results:
