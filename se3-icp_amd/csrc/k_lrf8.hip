@@ -46,31 +46,25 @@ using namespace knn;
 constexpr int kW = 4;     // waves per block
 constexpr int kQ = 8;     // queries per wave (eight lanes each in the group phases)
 #ifndef SE3ICP_LRF8_CAP
-#define SE3ICP_LRF8_CAP 176
+#define SE3ICP_LRF8_CAP 192
 #endif
-// candidates buffered per query (u32: cut key | candidate id).  Round 6: 176 (round 5: 192)
-// leaves LDS room for the tightening histograms at 6 waves per SIMD (round 5, C4 64 pairs:
-// 224 (5 waves per SIMD) +7 %, 256 (4 waves) +22 % k_lrf8 time -- occupancy beats the tighter
-// first bound a larger accept-all fill gives)
+// candidates buffered per query (u32: cut key | candidate id); round 5, C4 64 pairs: 224
+// (5 waves per SIMD) +7 %, 256 (4 waves) +22 % k_lrf8 time -- occupancy beats the tighter
+// first bound a larger accept-all fill gives
 constexpr int kCap = SE3ICP_LRF8_CAP;
 #ifndef SE3ICP_LRF8_FILL
 #define SE3ICP_LRF8_FILL SE3ICP_LRF8_CAP
 #endif
-// the accept-all fill stops before a leaf would pass this
+// the accept-all fill stops before a leaf would pass this (round 5, C4 64 pairs: 128 or 160
+// instead of 192 -- a cheaper first tightening from fewer points -- made k_lrf8 8 % slower:
+// the looser first bound opens more leaves and costs more tightenings later)
 constexpr int kFill = SE3ICP_LRF8_FILL;
-// LDS stride of the lists: an odd number of 16-B slots (180 entries = 45), so that the
-// lane-major ds_read_b128 of a run puts the lanes of a 16-lane bank group on distinct slots
+// LDS stride of the lists: 196 entries = 49 16-B slots, odd, so that the lane-major
+// ds_read_b128 of a 128-entry run (lane l of group g: entries 16 l .. 16 l + 15) puts every
+// 16-lane bank group on 16 distinct slots of the 256-B bank row (conflict-free), and the
+// lane-major ds_read_b32 of an unaligned run is 4-way instead of 16-way
 constexpr int kStride = kCap + 4;
 static_assert(((kStride / 4) & 1) == 1, "an odd number of 16-B slots per list");
-// the tightening reads a list lane-major, kPer entries per lane of the query's group
-constexpr int kPer = 24;
-static_assert(8 * kPer >= kCap && kPer % 4 == 0, "eight lanes cover a full list in 16-B loads");
-// a tightening refines its histogram until at most this many entries stay below the bound
-// (a leaf of 64 then fits the list), or the buckets cannot be split further
-#ifndef SE3ICP_LRF8_TGT
-#define SE3ICP_LRF8_TGT (kCap - 64)
-#endif
-constexpr int kTarget = SE3ICP_LRF8_TGT;
 constexpr int kLeaves = 64;              // leaves one wave may scan: candidate id = (list index << 6) | lane
 constexpr unsigned kIdBits = 0xfffu;     // low bits of a list entry: the candidate id
 // bound of the accept-all phase: every finite key (a lane past the leaf's end carries an
@@ -78,19 +72,15 @@ constexpr unsigned kIdBits = 0xfffu;     // low bits of a list entry: the candid
 constexpr unsigned kAll = 0x7f7fffffu;
 constexpr unsigned kPad = 0xffffffffu;   // sort padding (> every entry)
 
-// park slots per query: doubles in the list tail (P8_*), integers in the query's column of
-// the wave's histogram words (PI_*); both are free once the list is final
+// park slots per query (doubles)
 enum Park8 {
     P8_SUM = 0,     // 21 neighbour sums, later the 6 TOLDI axis sums
-    P8_R = 21, P8_ZN = 22,
-    P8_N = 25
+    P8_R = 21, P8_KK = 22, P8_GP = 23, P8_FLAGS = 24, P8_K = 25, P8_NTOP = 26, P8_ZN = 27,
+    P8_W = 30,                // the query's tree slot
+    P8_N = 31
 };
-enum ParkI { PI_KK = 0, PI_GP = 1, PI_FLAGS = 2, PI_NTOP = 3, PI_W = 4, PI_N = 5 };
 constexpr int kParkAt = 128;  // list entry where the park starts (8-byte aligned)
-static_assert(kStride >= kParkAt + 2 * P8_N, "the park overlays the list tail");
-// histogram words per query (64 byte-wide bucket counters; a list holds <= kCap < 256 entries)
-constexpr int kHistW = 16;
-static_assert(kCap < 256 && PI_N <= kHistW, "byte counters; the integer park fits the histogram words");
+static_assert(kCap >= kParkAt + 2 * P8_N && kStride >= kCap, "the park overlays the list tail");
 
 // lane ^ m within a group of eight lanes (m = 1..7 as used by the networks)
 __device__ __forceinline__ unsigned gx(unsigned x, int m) {
@@ -247,137 +237,84 @@ __device__ __forceinline__ unsigned widen_bound(unsigned t, float S) {
     const float b = __uint_as_float(t);
     return min((__float_as_uint(fmaf(2.02f, f32_err3(b, S), b)) + 2u) | kIdBits, kAll);
 }
-// exclusive prefix sum of x over the eight lanes of a group (lane order) and the group's total
-__device__ __forceinline__ unsigned gscan8(unsigned x, int l, unsigned& total) {
-    unsigned p = 0u, s = x;
-#pragma unroll
-    for (int d = 1; d <= 4; d <<= 1) {
-        const unsigned t = gx(s, d);
-        if (l & d) p += t;
-        s += t;
+// number of entries <= t in the sorted run A[0 .. n)
+__device__ __forceinline__ int upper_count(const unsigned* A, int n, unsigned t) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (A[m] <= t) lo = m + 1; else hi = m;
     }
-    total = s;
-    return p;
+    return lo;
 }
-// sum of the four bytes of x, plus acc (v_sad_u8 against zero)
-__device__ __forceinline__ unsigned bytesum(unsigned x, unsigned acc) {
-    unsigned r;
-    asm("v_sad_u8 %0, %1, 0, %2" : "=v"(r) : "v"(x), "v"(acc));
-    return r;
-}
-
-// One histogram pass of the bound tightening over the group's entries k[] (the list, kPer
-// per lane, padding kPad): 64 buckets of width 2^sh from the floor F -- bucket =
-// min((k -sat F) >> sh, 63), so entries below F count in bucket 0 and entries above the
-// range (and the padding) in bucket 63.  The counters are bytes, four per LDS word, the
-// words of the wave's eight groups interleaved (word 8 w + g holds buckets 4w .. 4w+3 of
-// group g: one v_and_or gives the address).  Returns, group-uniform, the bucket in which the
-// count reaches `need` | the entries below it << 8 | the entries in it << 16 (~0u when the
-// group holds fewer than `need`).
-__device__ __forceinline__ unsigned hist_pass(const unsigned (&k)[kPer], unsigned F, int sh, unsigned* hist0, unsigned gwb,
-                                              unsigned* histw, int g, int l, int lane, unsigned need) {
-    reinterpret_cast<uint2*>(histw)[lane] = make_uint2(0u, 0u);  // the wave's 128 words
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int s = 0; s < kPer; ++s) {
-        const unsigned b = min(__builtin_elementwise_sub_sat(k[s], F) >> sh, 63u);
-        const unsigned b8 = b << 3;
-        // (the LDS address by one v_and_or: gwb holds the wave's and group's base bits)
-        unsigned addr;
-        asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(addr) : "v"(b8), "s"(0x1e0u), "v"(gwb));
-        asm volatile("ds_add_u32 %0, %1" : : "v"(addr), "v"(1u << (b8 & 31u)) : "memory");
+// entry of rank r of the union of two sorted runs A (na) and B (nb) (distinct entries):
+// i entries of A and r+1-i of B are the r+1 smallest; binary search on i
+__device__ __forceinline__ unsigned kth_of_two(const unsigned* A, int na, const unsigned* B, int nb, int r) {
+    int lo = max(0, r + 1 - nb), hi = min(r + 1, na);
+    while (lo < hi) {
+        const int i = (lo + hi) >> 1;
+        if (A[i] < B[r - i]) lo = i + 1; else hi = i;
     }
-    __builtin_amdgcn_wave_barrier();
-    // the lane's buckets 8l .. 8l+7: words 2l and 2l+1 of the group
-    const unsigned w0 = histw[(2 * l) * kQ + g], w1 = histw[(2 * l + 1) * kQ + g];
-    unsigned tot;
-    const unsigned ex = gscan8(bytesum(w1, bytesum(w0, 0u)), l, tot);
-    unsigned res = ~0u, c = ex;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const unsigned cnt = ((i < 4 ? w0 : w1) >> (8 * (i & 3))) & 0xffu;
-        const unsigned c2 = c + cnt;
-        if ((int)(c < need) & (int)(c2 >= need)) res = (unsigned)(8 * l + i) | (c << 8) | (cnt << 16);
-        c = c2;
-    }
-    res = min(res, gx(res, 1));
-    res = min(res, gx(res, 2));
-    res = min(res, gx(res, 4));
-    __builtin_amdgcn_wave_barrier();
-    return res;
+    const int j = r + 1 - lo;
+    return max(lo > 0 ? A[lo - 1] : 0u, j > 0 ? B[j - 1] : 0u);
 }
-
-// Bound tightening by histogram selection (round 6; rounds 2-5 sorted the lists with bitonic
-// networks to find the Kw-th entry exactly).  The bound only has to be an upper bound of the
-// Kw-th smallest entry (the final order is exact), so the list is bucketed by the top bits
-// of its entries -- 1/8 binade of the squared distance per bucket, 64 buckets below the
-// group's current bound -- and the bound is the upper edge of the bucket where the count
-// reaches Kw, refined inside that bucket (6 more bits per pass) while more than `target`
-// entries would stay.  The entries at or below the widened bound are compacted in place
-// (stable: lane-major order).  No early exits: every lane takes part in the exchanges.
-// Returns (bound, kept) for the lane's group.
-__device__ __forceinline__ uint2 tighten_hist(unsigned* lists, unsigned* hist0, unsigned gwb, unsigned* histw, int g, int l,
-                                              int lane, int nbg, unsigned tcur, int Kw, int target, float S) {
+// Bound tightening over a list whose first mv entries are already sorted (the kept set of
+// the previous tightening): only the tail appended since is sorted, the Kw-th entry is
+// found by a merge-path search of the two runs, and the kept parts of both runs are merged
+// by a bitonic half-cleaner network (A ascending, padding, B descending: one bitonic
+// sequence of 128), so the kept list stays sorted for the next tightening.
+//   presort (wave-uniform): some list has no sorted prefix (the first tightening) or a
+//           tail over 128: list[0 .. min(nbg, 128)) is sorted first;
+//   tail_per (wave-uniform): 0 every tail empty, 8 every tail <= 64 entries, else 16.
+// Returns (bound, kept, new sorted prefix) for the group; kept sets over 128 entries (ties
+// at the bound) are compacted unmerged (prefix 0).
+__device__ __forceinline__ uint3 tighten_group_sorted(unsigned* lists, int g, int l, int nbg, int mv, int nmax, int Kw,
+                                                      bool presort, int tail_per, float S) {
     unsigned* list = lists + g * kStride;
-    unsigned k[kPer];
-    const int nv = nbg - l * kPer;  // valid entries among the lane's kPer
-#pragma unroll
-    for (int q = 0; q < kPer / 4; ++q) {
-        uint4 x = make_uint4(kPad, kPad, kPad, kPad);
-        if (l * kPer + 4 * q < kCap) x = *reinterpret_cast<const uint4*>(list + l * kPer + 4 * q);
-        k[4 * q] = 4 * q < nv ? x.x : kPad;
-        k[4 * q + 1] = 4 * q + 1 < nv ? x.y : kPad;
-        k[4 * q + 2] = 4 * q + 2 < nv ? x.z : kPad;
-        k[4 * q + 3] = 4 * q + 3 < nv ? x.w : kPad;
+    if (presort) {
+        mv = min(nbg, 128);
+        sort_head<16>(list, mv, l);
     }
-    const bool act = nbg >= Kw;
-    // the top bucket: the current bound's, or (no bound yet) the largest entry's
-    unsigned top = tcur >> 20;
-    if (__ballot(tcur >= kAll) != 0ull) {
-        unsigned m = 0u;
+    const int nb = nbg - mv;
+    unsigned* B = list + mv;
+    if (tail_per == 8) sort_run<8>(B, nb, l);
+    else if (tail_per == 16) sort_run<16>(B, nb, l);
+    const unsigned tg = nbg >= Kw ? widen_bound(kth_of_two(list, mv, B, nb, Kw - 1) | kIdBits, S) : kAll;
+    const int ka = upper_count(list, mv, tg), kb = upper_count(B, nb, tg);
+    const int kept = ka + kb;
+    if (__ballot(kept > 128) == 0ull) {
+        unsigned k[16];
+        load_head<16>(list, ka, l, k);
 #pragma unroll
-        for (int s = 0; s < kPer; ++s) m = max(m, k[s] + 1u);  // (padding wraps to 0)
-        m = max(m, gx(m, 1));
-        m = max(m, gx(m, 2));
-        m = max(m, gx(m, 4));
-        if (tcur >= kAll) top = (m - 1u) >> 20;
-    }
-    unsigned F = top >= 63u ? (top - 63u) << 20 : 0u;
-    int sh = 20;
-    unsigned edge = kAll;
-    bool more = act, first = true;
-    for (int pass = 0; pass < 4; ++pass) {
-        const unsigned r = hist_pass(k, F, sh, hist0, gwb, histw, g, l, lane, (unsigned)Kw);
-        if (more) {
-            const unsigned b = r & 0xffu, cum = ((r >> 8) & 0xffu) + ((r >> 16) & 0xffu);
-            edge = F + ((b + 1u) << sh) - 1u;  // (<= 0x7f7fffff: the top bucket is a finite key's)
-            if (cum <= (unsigned)target || cum <= (unsigned)Kw + 4u) {
-                more = false;
-            } else if (first && b == 0u && F > 0u) {  // bucket 0 holds everything below F: move the range down
-                F = F > (64u << 20) ? F - (64u << 20) : 0u;
-            } else if (sh >= 8) {  // split bucket b
-                F += b << sh;
-                sh -= 6;
-                first = false;
-            } else {
-                more = false;
-            }
+        for (int s = 0; s < 16; ++s) {
+            const int e = l * 16 + s;
+            if (e >= 128 - kb) k[s] = B[127 - e];
         }
-        if (__ballot(more) == 0ull) break;
+        __builtin_amdgcn_wave_barrier();
+        stage8<16, 128, 64>(k, l);
+        stage8<16, 128, 32>(k, l);
+        stage8<16, 128, 16>(k, l);
+        stage8<16, 128, 8>(k, l);
+        stage8<16, 128, 4>(k, l);
+        stage8<16, 128, 2>(k, l);
+        stage8<16, 128, 1>(k, l);
+        store_head<16>(list, kept, l, k);
+        __builtin_amdgcn_wave_barrier();
+        return make_uint3(tg, (unsigned)kept, (unsigned)kept);
     }
-    const unsigned tg = act ? min(widen_bound(edge, S), tcur) : tcur;
-    unsigned c = 0u;
-#pragma unroll
-    for (int s = 0; s < kPer; ++s) c += k[s] <= tg ? 1u : 0u;
-    unsigned total;
-    unsigned off = gscan8(c, l, total);
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int s = 0; s < kPer; ++s) {
-        if (k[s] <= tg) list[off++] = k[s];
+    // (rare) stable compaction in place, as tighten_group
+    unsigned keep_n = 0;
+    for (int r0 = 0; r0 < nmax; r0 += 8) {
+        const int e = r0 + l;
+        const unsigned ent = e < nbg ? list[e] : kPad;
+        const bool keep = ent <= tg;
+        const unsigned long long m = __ballot(keep);
+        const unsigned gm = (unsigned)(m >> (8 * g)) & 0xffu;
+        __builtin_amdgcn_wave_barrier();
+        if (keep) list[(int)keep_n + __popc(gm & ((1u << l) - 1u))] = ent;
+        keep_n += (unsigned)__popc(gm);
+        __builtin_amdgcn_wave_barrier();
     }
-    __builtin_amdgcn_wave_barrier();
-    return make_uint2(tg, total);
+    return make_uint3(tg, keep_n, 0u);
 }
 
 // the f64 point of tree slot i from its (x, y, z, 0) record: one 16-B and one 8-B load of
@@ -401,14 +338,39 @@ __device__ __forceinline__ p3 ld3(const double4* __restrict__ P4, int i) {
 // an f32 key and is not already in the exact order.
 __device__ __forceinline__ bool final_group(unsigned* lists, const int* leaf_slot, const double4* __restrict__ P4,
                                             const int32_t* __restrict__ perm, double qx, double qy, double qz, int off,
-                                            int g, int l, int nbg, int lim) {
+                                            int g, int l, int nbg, int mv, int fmode, int lim) {
     unsigned* list = lists + g * kStride;
     unsigned long long k[16];
     bool unsorted = false;
     {
         unsigned k32[16];
-        load_head<16>(list, nbg, l, k32);
-        sort8<16>(k32, l);
+        // fmode (wave-uniform): 0 a full sort; 1 the sorted prefix list[0 .. mv) (the last
+        // tightening's kept set) merged with the tail appended since (<= 64 entries, sorted
+        // first), as tighten_group_sorted merges; 2 the tail is empty (already in order)
+        if (fmode == 0) {
+            load_head<16>(list, nbg, l, k32);
+            sort8<16>(k32, l);
+        } else {
+            const int nb = nbg - mv;
+            unsigned* B = list + mv;
+            if (fmode == 1) sort_run<8>(B, nb, l);
+            load_head<16>(list, mv, l, k32);
+            if (fmode == 1) {
+#pragma unroll
+                for (int s = 0; s < 16; ++s) {
+                    const int e = l * 16 + s;
+                    if (e >= 128 - nb) k32[s] = B[127 - e];
+                }
+                __builtin_amdgcn_wave_barrier();
+                stage8<16, 128, 64>(k32, l);
+                stage8<16, 128, 32>(k32, l);
+                stage8<16, 128, 16>(k32, l);
+                stage8<16, 128, 8>(k32, l);
+                stage8<16, 128, 4>(k32, l);
+                stage8<16, 128, 2>(k32, l);
+                stage8<16, 128, 1>(k32, l);
+            }
+        }
 #pragma unroll
         for (int s = 0; s < 16; ++s) {
             const int e = l * 16 + s;
@@ -520,21 +482,17 @@ __device__ __forceinline__ bool final_group(unsigned* lists, const int* leaf_slo
 
 static_assert(kW >= 2 && kW * kQ <= 64, "the per-block epilogue: waves 0 and 1, a lane per query");
 
-// waves per SIMD: 6 = the LDS limit (26.5 KB per block); A/B 4 -> 5 -> 6: 6.73 -> 6.45 -> 6.38 ms
-__global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <= 176 ? 6 : (kCap <= 208 ? 5 : 4)))) void k_lrf8(
+// waves per SIMD: 6 = the LDS limit (26.6 KB per block); A/B 4 -> 5 -> 6: 6.73 -> 6.45 -> 6.38 ms
+__global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <= 192 ? 6 : (kCap <= 224 ? 5 : 4)))) void k_lrf8(
     View v, const int32_t* __restrict__ cloud_of, const CloudSetup* __restrict__ setup,
     const CloudDev* __restrict__ clouds, const float* __restrict__ tlo, const float* __restrict__ thi,
     const double4* __restrict__ P4, const int32_t* __restrict__ wave_base, int w_lo, int nwaves,
     int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_count) {
     // (a query's park overlays the tail of its list, free once the list is final: <= 128 entries)
     __shared__ __attribute__((aligned(16))) unsigned s_list[kW][kQ][kStride];
-    // the tightening histograms: per wave kHistW words per query, interleaved (word 8 w + g)
-    __shared__ __attribute__((aligned(512))) unsigned s_hist[kW][kHistW * kQ];
-    static_assert(kHistW * kQ * 4 == 512, "one wave's histogram words: 512 B");
     auto park_of = [&](int w, int j) __attribute__((always_inline)) {
         return reinterpret_cast<double*>(&s_list[w][j][kParkAt]);
     };
-    auto parki_of = [&](int w, int j) __attribute__((always_inline)) { return &s_hist[w][j]; };  // slot i at [i * kQ]
     __shared__ int s_leaf[kW][kLeaves];  // first tree slot of each scanned leaf
     __shared__ __attribute__((aligned(16))) float s_q[kW][3 * kQ];  // the queries' f32 x[8] y[8] z[8]
     // (wid through readfirstlane: the wave's LDS bases become scalar, not per-lane registers)
@@ -544,10 +502,6 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
     const TreeRef T = v.t3;
     const int first_leaf = (1 << T.L) - 1;
     unsigned* lists = &s_list[wid][0][0];
-    unsigned* histw = s_hist[wid];
-    // byte offset of the group's counter words from s_hist (see hist_pass)
-    // (LDS byte address; s_hist is 512-B aligned, so bits 5..8 are free for the bucket word)
-    const unsigned gwb = (unsigned)(uintptr_t)&s_hist[0][0] + (unsigned)(wid * kHistW * kQ * 4 + g * 4);
     int* leaves = s_leaf[wid];
     unsigned n_leaves = 0, n_sel = 0, n_cand = 0, n_q = 0;
 #ifdef SE3ICP_PROF
@@ -600,7 +554,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
         for (int j = 0; j < kQ; ++j) asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(x) : "s"(nbq[j]), "n"(8 * j));
         return (unsigned)__shfl(x, lane & ~7, 64);
     };
-    unsigned tgl = kAll;  // the bound of the lane's group
+    int mvv = 0;  // sorted prefix of the group's list
     float* qv = s_q[wid];
     float fqlo[3] = {0.f, 0.f, 0.f}, fqhi[3] = {0.f, 0.f, 0.f};
     int nlist = 0;
@@ -639,18 +593,29 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
     }
 
     // ---------------------------------------------------------------- bound tightening
-    // target: the most entries a tightening may leave (kTarget during the traversal, so that a
-    // leaf fits; 128 for the final order)
-    auto tighten = [&](int target) __attribute__((always_inline)) {
+    auto tighten = [&]() __attribute__((always_inline)) {
         ++n_sel;
+        unsigned nmax = 0;
+#pragma unroll
+        for (int j = 0; j < kQ; ++j) nmax = max(nmax, nbq[j]);
         __builtin_amdgcn_wave_barrier();
-        const uint2 r2 = tighten_hist(lists, &s_hist[0][0], gwb, histw, g, l, lane, (int)group_len(), tgl, Kw, target, s_norm);
-        tgl = r2.x;
+        int dmax = 0;
+        bool anyz = false;
+#pragma unroll
+        for (int j = 0; j < kQ; ++j) {
+            const int mj = __builtin_amdgcn_readlane(mvv, 8 * j);
+            dmax = max(dmax, (int)nbq[j] - mj);
+            anyz |= mj == 0;
+        }
+        const bool presort = anyz || dmax > 128;
+        const int tail_per = presort ? (nmax <= 128 ? 0 : (nmax <= 192 ? 8 : 16)) : (dmax == 0 ? 0 : dmax <= 64 ? 8 : 16);
+        const uint3 r3 = tighten_group_sorted(lists, g, l, (int)group_len(), mvv, (int)nmax, Kw, presort, tail_per, s_norm);
+        mvv = (int)r3.z;
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
         for (int j = 0; j < kQ; ++j) {
-            Tq[j] = (unsigned)__builtin_amdgcn_readlane((int)r2.x, 8 * j);
-            nbq[j] = (unsigned)__builtin_amdgcn_readlane((int)r2.y, 8 * j);
+            Tq[j] = (unsigned)__builtin_amdgcn_readlane((int)r3.x, 8 * j);
+            nbq[j] = (unsigned)__builtin_amdgcn_readlane((int)r3.y, 8 * j);
         }
     };
 
@@ -761,12 +726,12 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
         float lbA = INFINITY, lbL = INFINITY;
         OutwardBits itA(0ull, 0), itL(0ull, 0);
         int cur = -1, part = 0;
-        bool do_tighten = false, retried = false, at_end = false;
+        bool do_tighten = false, retried = false;
         float tf = INFINITY;  // f32 box-test bound of the union of the eight (set with each tightening)
         while (!fb_wave) {
             if (do_tighten) {
                 PROF8_NOW(t_t0);
-                tighten(at_end ? 128 : kTarget);
+                tighten();
                 PROF8_NOW(t_t1);
                 PROF8_ADD(c_tight, t_t0, t_t1);
                 do_tighten = false;
@@ -829,7 +794,6 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
 #endif
                             do_tighten = true;
                             retried = true;
-                            at_end = true;
                             continue;
                         }
                         if (nmax > 128) { fb_wave = true; PROF8_FB(2); }  // (ties at the bound)
@@ -882,7 +846,20 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
     if (mode == 1) qg = ld3(P4, wq);
     if (mode == 1 && !fb_wave) {
         __builtin_amdgcn_wave_barrier();
-        const bool exact = final_group(lists, leaves, P4, T.perm, qg.x, qg.y, qg.z, cl.off, g, l, nbg, min(nbg, max(kk, kn) + 1));
+        int fmode = 0;
+        {
+            int dmax = 0;
+            bool anyz = false;
+#pragma unroll
+            for (int j = 0; j < kQ; ++j) {
+                const int mj = __builtin_amdgcn_readlane(mvv, 8 * j);
+                dmax = max(dmax, (int)nbq[j] - mj);
+                anyz |= mj == 0;
+            }
+            fmode = anyz || dmax > 64 ? 0 : dmax == 0 ? 2 : 1;
+        }
+        const bool exact = final_group(lists, leaves, P4, T.perm, qg.x, qg.y, qg.z, cl.off, g, l, nbg, mvv, fmode,
+                                       min(nbg, max(kk, kn) + 1));
         fb_q = (bool)((int)!exact | (int)(nTop < Kw));
         n_cand += (unsigned)nbg;
 #ifdef SE3ICP_PROF
@@ -909,7 +886,6 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
     // (their live registers do not add up).
     const unsigned* rl = lists + g * kStride;
     double* pj = park_of(wid, g);
-    unsigned* pji = parki_of(wid, g);
     {
         double x[12];
 #pragma unroll
@@ -973,14 +949,15 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
         __builtin_amdgcn_wave_barrier();
         if (l == 0) {
             const int flags = mine ? ((want_t ? 1 : 0) | (want_n ? 2 : 0)) : 0;
-            pji[PI_FLAGS * kQ] = (unsigned)flags;
+            pj[P8_FLAGS] = (double)flags;
             if (mine) {
 #pragma unroll
                 for (int i = 0; i < 9; ++i) pj[P8_SUM + 12 + i] = x[i];
-                pji[PI_KK * kQ] = (unsigned)kk;
-                pji[PI_GP * kQ] = (unsigned)(cl.off + T.perm[wq]);
-                pji[PI_NTOP * kQ] = (unsigned)nTop;
-                pji[PI_W * kQ] = (unsigned)wq;
+                pj[P8_KK] = (double)kk;
+                pj[P8_GP] = (double)(cl.off + T.perm[wq]);
+                pj[P8_K] = (double)K;
+                pj[P8_NTOP] = (double)nTop;
+                pj[P8_W] = (double)wq;
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -1002,9 +979,9 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
     // TOLDI: C about the quirk centroid cl = (S' - q) / rz (ISR.cpp:259-272, see k_knn.hip),
     // its smallest eigenvector by cyclic Jacobi; normals: FastEigen3x3 of the kn-point
     // covariance (Open3D EstimateNormals, ISR.cpp:643) and the GICP covariance from it.
-    auto toldi_eig = [&](double* pb, const unsigned* pbi) __attribute__((always_inline)) {
-        const p3 q = ld3(P4, (int)pbi[PI_W * kQ]);  // the query's tree slot
-        const double rz = (double)((int)pbi[PI_KK * kQ] / 3);
+    auto toldi_eig = [&](double* pb) __attribute__((always_inline)) {
+        const p3 q = ld3(P4, (int)pb[P8_W]);  // the query's tree slot
+        const double rz = (double)((int)pb[P8_KK] / 3);
         const double q3[3] = {q.x, q.y, q.z};
         double cq[3], S[3];
 #pragma unroll
@@ -1023,10 +1000,10 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
         pb[P8_ZN + 1] = zn.y;
         pb[P8_ZN + 2] = zn.z;
     };
-    auto normal_eig = [&](const double* pb, const unsigned* pbi) __attribute__((always_inline)) {
-        const int wb = (int)pbi[PI_W * kQ];
+    auto normal_eig = [&](const double* pb) __attribute__((always_inline)) {
+        const int wb = (int)pb[P8_W];
         const int cc = cloud_of[wb];
-        const int knb = min(setup[cc].k_nrm, (int)pbi[PI_NTOP * kQ]);
+        const int knb = min(setup[cc].k_nrm, (int)pb[P8_NTOP]);
         double n6[6] = {1, 0, 0, 1, 0, 1};
         if (knb >= 3) {
             double cu[9];
@@ -1041,7 +1018,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
         }
         d3 nm = fast_eigen3x3(n6[0], n6[1], n6[2], n6[3], n6[4], n6[5]);
         if (sqrt(dot3(nm, nm)) == 0.0) nm = d3{0, 0, 1};
-        const int gp = (int)pbi[PI_GP * kQ];
+        const int gp = (int)pb[P8_GP];
         v.nrm64[gp] = nm.x;
         v.nrm64[v.ld + gp] = nm.y;
         v.nrm64[2 * (size_t)v.ld + gp] = nm.z;
@@ -1051,21 +1028,20 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
     __syncthreads();
     if (wid <= 1) {
         double* pb = park_of(lane < kW * kQ ? lane / kQ : 0, lane % kQ);
-        const unsigned* pbi = parki_of(lane < kW * kQ ? lane / kQ : 0, lane % kQ);
-        const int b_flags = lane < kW * kQ ? (int)pbi[PI_FLAGS * kQ] : 0;
-        if ((b_flags & 1) && wid == 0) toldi_eig(pb, pbi);
-        if ((b_flags & 2) && wid == 1) normal_eig(pb, pbi);
+        const int b_flags = lane < kW * kQ ? (int)pb[P8_FLAGS] : 0;
+        if ((b_flags & 1) && wid == 0) toldi_eig(pb);
+        if ((b_flags & 2) && wid == 1) normal_eig(pb);
     }
     __syncthreads();
 
     // ---------------------------------------------------------------- TOLDI axes (ISR.cpp:286-306)
     {
-        const int flags = (int)pji[PI_FLAGS * kQ];
+        const int flags = (int)pj[P8_FLAGS];
         double x6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         if (flags & 1) {
             const double nx = pj[P8_ZN], ny = pj[P8_ZN + 1], nz = pj[P8_ZN + 2];
             const double R = pj[P8_R];
-            const int kkq = (int)pji[PI_KK * kQ];
+            const int kkq = (int)pj[P8_KK];
             p3 pn = ld3(P4, (int)rl[max(min(1 + l, kkq - 1), 0)]);
             for (int r = 1 + l; r < kkq; r += 8) {  // ranks 1 .. kk-1
                 const p3 p = pn;
@@ -1094,10 +1070,9 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
     __syncthreads();
     if (wid == 0) {
         const double* pb = park_of(lane < kW * kQ ? lane / kQ : 0, lane % kQ);
-        const unsigned* pbi = parki_of(lane < kW * kQ ? lane / kQ : 0, lane % kQ);
-        const int b_flags = lane < kW * kQ ? (int)pbi[PI_FLAGS * kQ] : 0;
+        const int b_flags = lane < kW * kQ ? (int)pb[P8_FLAGS] : 0;
         if (b_flags & 1) {
-            const int w = (int)pbi[PI_W * kQ];
+            const int w = (int)pb[P8_W];
             const CloudSetup sw = setup[cloud_of[w]];
             const p3 q = ld3(P4, w);
             d3 nrm{pb[P8_ZN], pb[P8_ZN + 1], pb[P8_ZN + 2]};
@@ -1111,7 +1086,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
             const double al = sw.alpha, be = sw.beta;
             const double f12[12] = {al * xax.x, al * xax.y, al * xax.z, al * yax.x, al * yax.y, al * yax.z,
                                     al * zax.x, al * zax.y, al * zax.z, be * q.x, be * q.y, be * q.z};
-            store_frame_rows(v.fr64, v.fr32, (int)pbi[PI_GP * kQ], f12, sw.cf_target, q.x, q.y, q.z);
+            store_frame_rows(v.fr64, v.fr32, (int)pb[P8_GP], f12, sw.cf_target, q.x, q.y, q.z);
         }
     }
 #ifdef SE3ICP_PROF
