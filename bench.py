@@ -123,6 +123,20 @@ def pmc_counter(kernel_substr: str, counter: str, workload: str):
 C2_SETUPS = {"easy": (5.0, np.pi / 4), "moderate": (10.0, np.pi / 2)}  # B_SYN:106-108, :111-112
 
 
+def datasets_tag() -> str:
+    """Short hash of the pair generators' sources (se3icp/datasets.py and the C2 reference
+    generator): part of the --pair-cache file name, so that a generator change never reuses
+    stale pairs and ground truths (the seeds are fixed per workload in make_pairs)."""
+    import hashlib
+    h = hashlib.sha1()
+    for f in ("se3-icp_amd/se3icp/datasets.py", "se3-icp_amd/csrc/k_gen.hip", "se3-icp_amd/csrc/gen_ref.cpp"):
+        try:
+            h.update(open(os.path.join(ROOT, f), "rb").read())
+        except OSError:
+            pass
+    return h.hexdigest()[:10]
+
+
 def make_pairs(wl: str, total: int, first: int, count: int, n_az: int, c2_setup: str = "easy", device: int = 0,
                c2_cloud: str = "downsample"):
     """The rank's pairs [first, first + count) of a `total`-pair sequence, with ground truths."""
@@ -169,6 +183,9 @@ def main():
     ap.add_argument("--c2-cloud", choices=["downsample", "unique"], default="downsample",
                     help="C2 cloud: RandomDownSample(0.2) of the 208,353-vertex bunny (41,670 pts, round 3 on) or "
                          "BASELINE.md's 34,834 unique vertices (rounds 1-2); the bench line's workload is then 'C2u'")
+    ap.add_argument("--shard", choices=["contiguous", "balanced"], default="contiguous",
+                    help="pairs per rank: contiguous blocks of the batch, or a cost-balanced assignment (greedy by "
+                         "point count over the whole batch, sharding.shard_balanced)")
     ap.add_argument("--secondary", choices=["auto", "off"], default="auto",
                     help="C4 at N=1: also time one 8-pair shard on this GPU (the per-GPU work of the 8-GPU job)")
     args = ap.parse_args()
@@ -213,19 +230,32 @@ def main():
     scaling, global_batch, first, count = sharding.plan(world, rank, W["batch"], args.global_batch,
                                                         args.pairs_per_gpu)
     t0 = time.time()
-    cache = (os.path.join(args.pair_cache, f"{args.workload}_{args.c2_cloud}_{args.c2_setup}_{args.n_az}_"
-                          f"{global_batch}_{first}_{count}.npz") if args.pair_cache else "")
-    if cache and os.path.exists(cache):  # (A/B runs on one box: the same synthetic pairs, generated once)
-        z = np.load(cache)
-        pairs = [(z[f"s{i}"], z[f"t{i}"]) for i in range(count)]
-        gts = [z["gts"][i] for i in range(count)]
-    else:
-        pairs, gts = make_pairs(args.workload, global_batch, first, count, args.n_az, args.c2_setup, devi,
+    pair_ids = None  # (balanced shards: the rank's pair indices in the batch)
+    if args.shard == "balanced" and world > 1:
+        # every rank generates the whole batch (deterministic), balances it by point count and
+        # keeps its own pairs
+        allp, allg = make_pairs(args.workload, global_batch, 0, global_batch, args.n_az, args.c2_setup, devi,
                                 args.c2_cloud)
-        if cache:
-            os.makedirs(args.pair_cache, exist_ok=True)
-            np.savez(cache, gts=np.stack(gts), **{f"s{i}": p[0] for i, p in enumerate(pairs)},
-                     **{f"t{i}": p[1] for i, p in enumerate(pairs)})
+        plan_b = sharding.shard_balanced([p[0].shape[0] + p[1].shape[0] for p in allp], world)
+        pair_ids = plan_b[rank]
+        pairs, gts = [allp[i] for i in pair_ids], [allg[i] for i in pair_ids]
+        first, count = pair_ids[0], len(pair_ids)
+        del allp, allg
+        log(f"rank {rank}: balanced shard of {count} pairs {pair_ids}")
+    else:
+        cache = (os.path.join(args.pair_cache, f"{args.workload}_{args.c2_cloud}_{args.c2_setup}_{args.n_az}_"
+                              f"{global_batch}_{first}_{count}_{datasets_tag()}.npz") if args.pair_cache else "")
+        if cache and os.path.exists(cache):  # (A/B runs on one box: the same synthetic pairs, generated once)
+            z = np.load(cache)
+            pairs = [(z[f"s{i}"], z[f"t{i}"]) for i in range(count)]
+            gts = [z["gts"][i] for i in range(count)]
+        else:
+            pairs, gts = make_pairs(args.workload, global_batch, first, count, args.n_az, args.c2_setup, devi,
+                                    args.c2_cloud)
+            if cache:
+                os.makedirs(args.pair_cache, exist_ok=True)
+                np.savez(cache, gts=np.stack(gts), **{f"s{i}": p[0] for i, p in enumerate(pairs)},
+                         **{f"t{i}": p[1] for i, p in enumerate(pairs)})
     npts = [p[0].shape[0] for p in pairs] + [p[1].shape[0] for p in pairs]
     log(f"rank {rank}: {args.workload} generated {count} pairs in {time.time() - t0:.1f}s, points/cloud "
         f"min {min(npts)} mean {np.mean(npts):.0f} max {max(npts)}")
@@ -289,7 +319,7 @@ def main():
 
     # ---- cross-rank: max time, summed work, RCCL gather of the per-pair results
     elapsed, loop_s, iters_all, gathered = sharding.exchange_results(
-        dist, xdev, elapsed, loop_ms / 1000.0, iters, sharding.pair_records(last))
+        dist, xdev, elapsed, loop_ms / 1000.0, iters, sharding.pair_records(last), pair_ids)
 
     if rank == 0:
         if args.dump_poses:
@@ -335,6 +365,7 @@ def main():
                 "method": W["method"],
                 "pairs_per_gpu": (global_batch // world if global_batch % world == 0
                                   else [sharding.shard(global_batch, world, r)[1] for r in range(world)]),
+                "shard": args.shard if world > 1 else "one rank",
                 "global_batch_pairs": global_batch,
                 "points_per_cloud_mean": int(np.mean(npts)),
                 "parallelism": f"pair-sharded dp{world} ({'RCCL' if args.backend == 'nccl' else 'gloo'} "
@@ -358,7 +389,9 @@ def main():
         }
         if args.workload == "C4" and world == 1 and args.secondary == "auto" and len(pairs) > 8:
             out["secondary_8_pair_shard_one_gpu"] = bench_shard8(pairs, W, params, dev, devi)
-        if world == 1 and args.cpu_baseline == "auto":
+        if args.cpu_baseline == "auto":
+            # rank 0's own pairs on the node's host (the same host for every rank), after the
+            # timed region; at N > 1 the whole job's value is compared with it
             out["cpu_baseline"], out["parity_vs_cpu"] = cpu_baseline(pairs, last, W, value, params, devi)
         print(json.dumps(out), flush=True)
     if dist:

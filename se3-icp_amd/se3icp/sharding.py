@@ -55,6 +55,29 @@ def shard(n_pairs_total: int, world: int, rank: int) -> tuple[int, int]:
     return first, count
 
 
+def shard_balanced(costs, world: int) -> list[list[int]]:
+    """Cost-balanced assignment of pairs to ranks: longest-processing-time greedy over the
+    pairs' costs (their point counts: the setup and every loop stage are per point), each
+    pair to the rank with the least cost so far (ties: the lower rank), the pairs in order of
+    decreasing cost (ties: the lower pair index).  Deterministic; every rank gets
+    floor(n / world) or more pairs when the costs are equal.  Returns each rank's pair
+    indices in ascending order."""
+    costs = np.asarray(costs, dtype=np.float64)
+    n = costs.shape[0]
+    if world <= 0 or n < world:
+        raise ValueError(f"{n} pairs cannot be balanced over {world} ranks")
+    order = sorted(range(n), key=lambda i: (-costs[i], i))
+    load = [0.0] * world
+    cnt = [0] * world
+    out: list[list[int]] = [[] for _ in range(world)]
+    for i in order:
+        r = min(range(world), key=lambda q: (load[q], cnt[q], q))
+        out[r].append(i)
+        load[r] += costs[i]
+        cnt[r] += 1
+    return [sorted(o) for o in out]
+
+
 def plan(world: int, rank: int, default_batch: int, global_batch: int = 0, pairs_per_gpu: int = 0):
     """The rank's share of a benchmark job: (scaling, global_batch, first, count).
 
@@ -73,7 +96,8 @@ def plan(world: int, rank: int, default_batch: int, global_batch: int = 0, pairs
     return scaling, total, first, count
 
 
-def exchange_results(dist, device, elapsed_s: float, loop_s: float, iterations: int, records: np.ndarray):
+def exchange_results(dist, device, elapsed_s: float, loop_s: float, iterations: int, records: np.ndarray,
+                     pair_ids=None):
     """Cross-rank reduction of one timed region.
 
     records: the rank's [n, REC] pair_records().  Returns (elapsed_max, loop_max,
@@ -82,12 +106,18 @@ def exchange_results(dist, device, elapsed_s: float, loop_s: float, iterations: 
     (cuda for nccl/RCCL, cpu for gloo).  Ranks may hold different numbers of pairs (shard()
     of a batch that does not divide evenly): the pair counts are gathered first and every
     rank's records are padded to the largest count for the fixed-size all-gather, then cut
-    back.
+    back.  pair_ids: the rank's pairs' indices in the global batch (shard_balanced); the
+    gathered records are then put in pair order.
     """
     import torch
 
     records = np.ascontiguousarray(records, dtype=np.float64).reshape(-1, REC)
+    if pair_ids is not None:
+        # the pair index rides in an extra column (exact in float64)
+        records = np.concatenate([records, np.asarray(pair_ids, dtype=np.float64).reshape(-1, 1)], axis=1)
     if dist is None:
+        if pair_ids is not None:
+            records = records[np.argsort(records[:, REC], kind="stable"), :REC]
         return float(elapsed_s), float(loop_s), int(iterations), unpack_records(records)
     t_max = torch.tensor([float(elapsed_s), float(loop_s)], dtype=torch.float64, device=device)
     dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
@@ -98,10 +128,12 @@ def exchange_results(dist, device, elapsed_s: float, loop_s: float, iterations: 
     counts = [torch.empty_like(cnt) for _ in range(world)]
     dist.all_gather(counts, cnt)
     counts = [int(c.item()) for c in counts]
-    pad = np.zeros((max(counts), REC))
+    pad = np.zeros((max(counts), records.shape[1]))
     pad[:records.shape[0]] = records
     mine = torch.from_numpy(pad).to(device)
     gathered = [torch.empty_like(mine) for _ in range(world)]
     dist.all_gather(gathered, mine)
     allr = np.concatenate([g.cpu().numpy()[:c] for g, c in zip(gathered, counts)])
+    if pair_ids is not None:
+        allr = allr[np.argsort(allr[:, REC], kind="stable"), :REC]
     return float(t_max[0]), float(t_max[1]), int(round(float(tot[0]))), unpack_records(allr)

@@ -174,3 +174,66 @@ def test_strong_shard_64_over_3_gloo(tmp_path):
         assert int(d["iters"]) == sum(range(total))        # every pair counted once
         np.testing.assert_array_equal(d["it"], np.arange(total))
         np.testing.assert_array_equal(d["poses"], np.stack([np.eye(4) * k for k in range(total)]))
+
+
+def test_balanced_shard_is_a_deterministic_partition():
+    """sharding.shard_balanced: every pair exactly once, deterministic, and the largest
+    rank load within one pair's cost of the smallest (LPT greedy)."""
+    rng = np.random.default_rng(0)
+    for n, world in ((64, 3), (64, 8), (7, 2), (256, 8), (8, 8)):
+        costs = rng.integers(100_000, 130_000, n)
+        plan = sharding.shard_balanced(costs, world)
+        assert plan == sharding.shard_balanced(costs, world)
+        assert sorted(i for p in plan for i in p) == list(range(n))
+        assert all(p == sorted(p) and p for p in plan)
+        loads = [int(costs[p].sum()) for p in plan]
+        assert max(loads) - min(loads) <= int(costs.max())
+    # equal costs: the counts of a contiguous split (22 + 21 + 21 for 64 over 3)
+    assert sorted(len(p) for p in sharding.shard_balanced([1] * 64, 3)) == [21, 21, 22]
+    with pytest.raises(ValueError):
+        sharding.shard_balanced([1, 2], 3)
+
+
+def _balanced_rank_main(rank, world, port, out_dir, costs):
+    """One rank of a balanced job: its shard_balanced() pairs, each identified by its global
+    index in the record, through the result exchange with the pair ids."""
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ids = sharding.shard_balanced(costs, world)[rank]
+    res = [_Res(np.eye(4) * i, i, i % 5, 0) for i in ids]
+    out = sharding.exchange_results(dist, torch.device("cpu"), elapsed_s=float(sum(costs[i] for i in ids)),
+                                    loop_s=0.0, iterations=sum(r.num_iterations for r in res),
+                                    records=sharding.pair_records(res), pair_ids=ids)
+    dist.barrier()
+    dist.destroy_process_group()
+    g = out[3]
+    np.savez(os.path.join(out_dir, f"b{rank}.npz"), elapsed=out[0], iters=out[2], poses=g.T, it=g.num_iterations,
+             pure=g.num_pure_se3_iterations)
+
+
+def test_balanced_shard_64_over_3_gloo(tmp_path):
+    """A cost-balanced 64-pair batch over 3 ranks with uneven pair costs: the gather returns
+    all 64 records in batch order (not rank order), and the job time is the max rank load."""
+    import torch.multiprocessing as mp
+
+    world, total = 3, 64
+    costs = [int(c) for c in np.random.default_rng(1).integers(100_000, 130_000, total)]
+    mp.start_processes(_balanced_rank_main, args=(world, _free_port(), str(tmp_path), costs), nprocs=world,
+                       join=True, start_method="spawn")
+    plan = sharding.shard_balanced(costs, world)
+    for r in range(world):
+        d = np.load(tmp_path / f"b{r}.npz")
+        assert float(d["elapsed"]) == max(sum(costs[i] for i in p) for p in plan)
+        assert int(d["iters"]) == sum(range(total))
+        np.testing.assert_array_equal(d["it"], np.arange(total))
+        np.testing.assert_array_equal(d["pure"], np.arange(total) % 5)
+        np.testing.assert_array_equal(d["poses"], np.stack([np.eye(4) * k for k in range(total)]))
+
+
+def test_exchange_results_single_rank_reorders_by_pair_id():
+    res = [_Res(np.eye(4) * i, i, 0, 0) for i in (5, 2, 9)]
+    _, _, _, g = sharding.exchange_results(None, None, 1.0, 0.0, 16, sharding.pair_records(res), pair_ids=[5, 2, 9])
+    assert list(g.num_iterations) == [2, 5, 9]
