@@ -46,32 +46,25 @@ using namespace knn;
 constexpr int kW = 4;     // waves per block
 constexpr int kQ = 8;     // queries per wave (eight lanes each in the group phases)
 #ifndef SE3ICP_LRF8_CAP
-#define SE3ICP_LRF8_CAP 160
+#define SE3ICP_LRF8_CAP 192
 #endif
-// candidates buffered per query (u32: cut key | candidate id).  Round 6: the lists hold the
-// final candidates only (the collect pass, below), ~Kw plus one histogram bucket; rounds 2-5
-// held up to 192 during the whole traversal
+// candidates buffered per query (u32: cut key | candidate id); round 5, C4 64 pairs: 224
+// (5 waves per SIMD) +7 %, 256 (4 waves) +22 % k_lrf8 time -- occupancy beats the tighter
+// first bound a larger accept-all fill gives
 constexpr int kCap = SE3ICP_LRF8_CAP;
-#ifndef SE3ICP_LRF8_SEED
-#define SE3ICP_LRF8_SEED 192
+#ifndef SE3ICP_LRF8_FILL
+#define SE3ICP_LRF8_FILL SE3ICP_LRF8_CAP
 #endif
-// the seed (the queries' own leaves and their tree-order neighbours, every point counted)
-// stops before a leaf would take it past this many points, once it holds Kw
-constexpr int kSeed = SE3ICP_LRF8_SEED;
-// LDS stride of the lists: an odd number of 16-B slots, so that the lane-major
+// the accept-all fill stops before a leaf would pass this (round 5, C4 64 pairs: 128 or 160
+// instead of 192 -- a cheaper first tightening from fewer points -- made k_lrf8 8 % slower:
+// the looser first bound opens more leaves and costs more tightenings later)
+constexpr int kFill = SE3ICP_LRF8_FILL;
+// LDS stride of the lists: 196 entries = 49 16-B slots, odd, so that the lane-major
 // ds_read_b128 of a 128-entry run (lane l of group g: entries 16 l .. 16 l + 15) puts every
 // 16-lane bank group on 16 distinct slots of the 256-B bank row (conflict-free), and the
 // lane-major ds_read_b32 of an unaligned run is 4-way instead of 16-way
 constexpr int kStride = kCap + 4;
 static_assert(((kStride / 4) & 1) == 1, "an odd number of 16-B slots per list");
-// Counting histograms (round 6): per query 64 buckets of 2^kHSh squared-distance key units
-// (1/8 binade at 20: three mantissa bits) above a floor, 16-bit counters, two per word, the
-// query's 32 words contiguous (128 B)
-#ifndef SE3ICP_LRF8_HSH
-#define SE3ICP_LRF8_HSH 20
-#endif
-constexpr int kHSh = SE3ICP_LRF8_HSH;
-constexpr int kHistW = 32;
 constexpr int kLeaves = 64;              // leaves one wave may scan: candidate id = (list index << 6) | lane
 constexpr unsigned kIdBits = 0xfffu;     // low bits of a list entry: the candidate id
 // bound of the accept-all phase: every finite key (a lane past the leaf's end carries an
@@ -79,24 +72,15 @@ constexpr unsigned kIdBits = 0xfffu;     // low bits of a list entry: the candid
 constexpr unsigned kAll = 0x7f7fffffu;
 constexpr unsigned kPad = 0xffffffffu;   // sort padding (> every entry)
 
-// park slots per query, free once the list is final (<= 128 entries) and the histograms
-// are dead: doubles 0 .. 15 in the query's histogram words, 16 .. P8_N-1 in the list tail
-// from entry kParkAt, then the integers (PI_*)
+// park slots per query (doubles)
 enum Park8 {
     P8_SUM = 0,     // 21 neighbour sums, later the 6 TOLDI axis sums
-    P8_R = 21, P8_ZN = 22,
-    P8_N = 25
+    P8_R = 21, P8_KK = 22, P8_GP = 23, P8_FLAGS = 24, P8_K = 25, P8_NTOP = 26, P8_ZN = 27,
+    P8_W = 30,                // the query's tree slot
+    P8_N = 31
 };
-enum ParkI { PI_KK = 0, PI_GP = 1, PI_FLAGS = 2, PI_NTOP = 3, PI_W = 4, PI_N = 5 };
-constexpr int kParkAt = 128;  // list entry where the park's tail starts (8-byte aligned)
-constexpr int kParkA = 2 * kHistW / 2 / 2 * 2 / 2;  // doubles in the histogram words (16)
-static_assert(kParkA == 16 && kStride >= kParkAt + 2 * (P8_N - kParkA) + PI_N, "the park overlays the list tail");
-struct Park {
-    double* a;   // the query's histogram words
-    double* b;   // its list tail
-    unsigned* i;
-    __device__ __forceinline__ double& operator[](int k) const { return k < kParkA ? a[k] : b[k - kParkA]; }
-};
+constexpr int kParkAt = 128;  // list entry where the park starts (8-byte aligned)
+static_assert(kCap >= kParkAt + 2 * P8_N && kStride >= kCap, "the park overlays the list tail");
 
 // lane ^ m within a group of eight lanes (m = 1..7 as used by the networks)
 __device__ __forceinline__ unsigned gx(unsigned x, int m) {
@@ -253,19 +237,6 @@ __device__ __forceinline__ unsigned widen_bound(unsigned t, float S) {
     const float b = __uint_as_float(t);
     return min((__float_as_uint(fmaf(2.02f, f32_err3(b, S), b)) + 2u) | kIdBits, kAll);
 }
-// exclusive prefix sum of x over the eight lanes of a group (lane order) and the group's total
-__device__ __forceinline__ unsigned gscan8(unsigned x, int l, unsigned& total) {
-    unsigned p = 0u, s = x;
-#pragma unroll
-    for (int d = 1; d <= 4; d <<= 1) {
-        const unsigned t = gx(s, d);
-        if (l & d) p += t;
-        s += t;
-    }
-    total = s;
-    return p;
-}
-
 // number of entries <= t in the sorted run A[0 .. n)
 __device__ __forceinline__ int upper_count(const unsigned* A, int n, unsigned t) {
     int lo = 0, hi = n;
@@ -511,20 +482,16 @@ __device__ __forceinline__ bool final_group(unsigned* lists, const int* leaf_slo
 
 static_assert(kW >= 2 && kW * kQ <= 64, "the per-block epilogue: waves 0 and 1, a lane per query");
 
-// waves per SIMD: 6 = the LDS limit (26.5 KB per block); A/B 4 -> 5 -> 6: 6.73 -> 6.45 -> 6.38 ms
-__global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <= 160 ? 6 : (kCap <= 192 ? 5 : 4)))) void k_lrf8(
+// waves per SIMD: 6 = the LDS limit (26.6 KB per block); A/B 4 -> 5 -> 6: 6.73 -> 6.45 -> 6.38 ms
+__global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <= 192 ? 6 : (kCap <= 224 ? 5 : 4)))) void k_lrf8(
     View v, const int32_t* __restrict__ cloud_of, const CloudSetup* __restrict__ setup,
     const CloudDev* __restrict__ clouds, const float* __restrict__ tlo, const float* __restrict__ thi,
     const double4* __restrict__ P4, const int32_t* __restrict__ wave_base, int w_lo, int nwaves,
     int32_t* __restrict__ fb_list, int32_t* __restrict__ fb_count) {
-    // (a query's park overlays its histogram and the tail of its list, both free once the
-    // list is final: <= 128 entries)
+    // (a query's park overlays the tail of its list, free once the list is final: <= 128 entries)
     __shared__ __attribute__((aligned(16))) unsigned s_list[kW][kQ][kStride];
-    __shared__ __attribute__((aligned(1024))) unsigned s_hist[kW][kQ][kHistW];
-    static_assert(kQ * kHistW * 4 == 1024, "one wave's histograms: 1 KB");
     auto park_of = [&](int w, int j) __attribute__((always_inline)) {
-        return Park{reinterpret_cast<double*>(&s_hist[w][j][0]), reinterpret_cast<double*>(&s_list[w][j][kParkAt]),
-                    &s_list[w][j][kParkAt + 2 * (P8_N - kParkA)]};
+        return reinterpret_cast<double*>(&s_list[w][j][kParkAt]);
     };
     __shared__ int s_leaf[kW][kLeaves];  // first tree slot of each scanned leaf
     __shared__ __attribute__((aligned(16))) float s_q[kW][3 * kQ];  // the queries' f32 x[8] y[8] z[8]
@@ -584,7 +551,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
         // select chain over the scalars is turned into a scratch array indexed by g)
         int x = 0;
 #pragma unroll
-        for (int j = 0; j < kQ; ++j) asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(x) : "s"(__builtin_amdgcn_readfirstlane(nbq[j])), "n"(8 * j));
+        for (int j = 0; j < kQ; ++j) asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(x) : "s"(nbq[j]), "n"(8 * j));
         return (unsigned)__shfl(x, lane & ~7, 64);
     };
     int mvv = 0;  // sorted prefix of the group's list
@@ -626,8 +593,6 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
     }
 
     // ---------------------------------------------------------------- bound tightening
-    // (the sorted tightening of rounds 2-5: only for a list that would overflow in the
-    // collect pass, or that holds more than 128 entries at the end -- rare)
     auto tighten = [&]() __attribute__((always_inline)) {
         ++n_sel;
         unsigned nmax = 0;
@@ -654,136 +619,61 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
         }
     };
 
-    // ---------------------------------------------------------------- leaf distances
-    // Each lane holds one point of leaf i: its f32 squared distances to the eight queries
-    // (f32 points, two queries per packed instruction; the bounds carry the error,
-    // widen_bound, the final order uses exact keys).  part: 0 the whole leaf, 1 / 2 its first
-    // / second 32 points.  Lanes past the part carry an infinite distance.
-    auto leaf_dq = [&](int i, int part, float (&dq)[kQ]) __attribute__((always_inline)) -> int {
-        const int a = __builtin_amdgcn_readfirstlane(tree_first(n, T.L, i));
-        const int b = __builtin_amdgcn_readfirstlane(tree_first(n, T.L, i + 1));
-        const bool valid = (bool)((int)(lane < b - a) & (int)(part == 0 || (part == 1) == (lane < 32)));
-        const int slot = cl.off + a + (valid ? lane : 0);
-        typedef float f2 __attribute__((ext_vector_type(2)));
-        const float px = valid ? T.tvec[slot] : INFINITY;
-        const float py = valid ? T.tvec[v.ld + slot] : INFINITY;
-        const float pz = valid ? T.tvec[2 * (size_t)v.ld + slot] : INFINITY;
-        const f2* qf2 = reinterpret_cast<const f2*>(qv);
-        const f2 pxx = f2{px, px}, pyy = f2{py, py}, pzz = f2{pz, pz};
-        // a - b as one v_pk_add_f32 (the compiler splits a broadcast operand into two v_sub_f32)
-        auto pk_sub = [](f2 x, f2 y) __attribute__((always_inline)) {
-            f2 r;
-            asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(x), "v"(y));
-            return r;
-        };
-#pragma unroll
-        for (int jp = 0; jp < kQ / 2; ++jp) {
-            const f2 ex = pk_sub(qf2[jp], pxx), ey = pk_sub(qf2[kQ / 2 + jp], pyy), ez = pk_sub(qf2[kQ + jp], pzz);
-            f2 s2 = ex * ex;
-            s2 = __builtin_elementwise_fma(ey, ey, s2);
-            s2 = __builtin_elementwise_fma(ez, ez, s2);
-            dq[2 * jp] = s2.x;
-            dq[2 * jp + 1] = s2.y;
-        }
-        return a;
-    };
-
-    // ---------------------------------------------------------------- count pass
-    // Query j counts every scanned point whose f32 key is <= Tq[j] into its histogram
-    // bucket min((key -sat Fq[j]) >> kHSh, 63); cb[j] counts those below its crossing
-    // bucket bq[j] (the bucket where the count reaches Kw: the bound Tq[j] is its widened
-    // upper edge).  No list is written: a leaf is recorded in the leaf table for the collect
-    // pass, and the bound only moves down (update).
-    unsigned Fw = 0u;  // the wave's histogram floor (one for the eight tree-adjacent queries)
-    const unsigned hb = (unsigned)(uintptr_t)&s_hist[wid][0][0];  // LDS byte address (1 KB aligned)
-    const unsigned kMask7c = 0x7cu;
-    auto count_leaf = [&](int i) __attribute__((always_inline)) {
-        if (nlist >= kLeaves) { fb_wave = true; PROF8_FB(0); return; }
+    // ---------------------------------------------------------------- leaf scan
+    // Each lane holds one point of leaf i; query j appends it when its entry (cut key |
+    // id) <= Tq[j].  part: 0 the whole leaf, 1 / 2 its first / second 32 points (a leaf that
+    // does not fit a list even after a tightening is appended in two halves).  Lanes past
+    // the part carry an infinite distance: their entries exceed every bound.
+    auto scan_leaf = [&](int i, int part) __attribute__((always_inline)) -> bool {
+        if (nlist >= kLeaves) { fb_wave = true; PROF8_FB(0); return true; }
         const int li = nlist++;
         ++n_leaves;
-        float dq[kQ];
-        const int a = leaf_dq(i, 0, dq);
+        const int a = __builtin_amdgcn_readfirstlane(tree_first(n, T.L, i));
+        const int b = __builtin_amdgcn_readfirstlane(tree_first(n, T.L, i + 1));
         if (lane == 0) leaves[li] = cl.off + a;
-#pragma unroll
-        for (int j = 0; j < kQ; ++j) {
-            const unsigned key = __float_as_uint(dq[j]);
-            if (key <= Tq[j]) {
-                // 16-bit counter bk of query j: word bk >> 1 of its 128 B, half bk & 1
-                const unsigned bk = min(__builtin_elementwise_sub_sat(key, Fw) >> kHSh, 63u);
-                unsigned addr;
-                asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(addr) : "v"(bk << 1), "v"(kMask7c), "s"(hb + 128u * j));
-                asm volatile("ds_add_u32 %0, %1" : : "v"(addr), "v"(1u << ((bk << 4) & 31u)) : "memory");
-            }
-        }
-    };
-    // The bounds after a count, group-parallel (group g: query g).  The group's count
-    // below its crossing bucket vbq is recomputed from the histogram (lane l: buckets
-    // 8l .. 8l+7); where it reached Kw the crossing moves down -- eight buckets per round,
-    // lane l looking at bucket vbq-1-l; the new crossing is the highest bucket below which
-    // fewer than Kw entries remain -- and Tq is its widened upper edge.
-    int vbq = 64;  // the group's crossing bucket
-    auto update = [&]() __attribute__((always_inline)) -> bool {
-        const uint4 hw = reinterpret_cast<const uint4*>(&s_hist[wid][g][0])[l];  // buckets 8l .. 8l+7
-        unsigned below = 0u;
-        {
-            const unsigned w4[4] = {hw.x, hw.y, hw.z, hw.w};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int b0 = 8 * l + 2 * k;
-                below += (b0 < vbq ? (w4[k] & 0xffffu) : 0u) + (b0 + 1 < vbq ? (w4[k] >> 16) : 0u);
-            }
-        }
-        below += gx(below, 1);
-        below += gx(below, 2);
-        below += gx(below, 4);
-        const bool mv = below >= (unsigned)Kw;
-        if (__ballot(mv) == 0ull) return false;
-        ++n_sel;
-        unsigned vcb = below;
-        const unsigned short* h16 = reinterpret_cast<const unsigned short*>(&s_hist[wid][g][0]);
-        bool go = mv;
-        while (__ballot(go) != 0ull) {
-            const int bl = vbq - 1 - l;
-            const unsigned h = bl >= 0 ? (unsigned)h16[bl] : 0u;
-            unsigned tot;
-            const unsigned incl = gscan8(h, l, tot) + h;
-            // (vcb - incl: the entries below bucket bl; never negative)
-            const unsigned gm = (unsigned)(__ballot((int)go & (int)(vcb - incl < (unsigned)Kw)) >> (8 * g)) & 0xffu;
-            if (go) {
-                if (gm != 0u) {
-                    vbq = vbq - 1 - __builtin_ctz(gm);
-                    go = false;
-                } else {
-                    vbq -= 8;
-                    vcb -= tot;
-                }
-            }
-        }
-        unsigned tg = kAll;
-        if (mv) tg = widen_bound(Fw + ((unsigned)(vbq + 1) << kHSh) - 1u, s_norm);
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int j = 0; j < kQ; ++j) Tq[j] = min(Tq[j], (unsigned)__builtin_amdgcn_readlane((int)tg, 8 * j));
-        return true;
-    };
-
-    // ---------------------------------------------------------------- collect pass
-    // Query j appends the points of leaf i (table entry li) whose entry (cut key | id) is
-    // <= Tq[j]; false (nothing written) when a list would overflow.
-    auto append_leaf = [&](int li, int i, int part) __attribute__((always_inline)) -> bool {
-        float dq[kQ];
-        (void)leaf_dq(i, part, dq);
+        const bool valid = (bool)((int)(lane < b - a) & (int)(part == 0 || (part == 1) == (lane < 32)));
+        const int slot = cl.off + a + (valid ? lane : 0);
         const unsigned id = (unsigned)((li << 6) | lane);
         unsigned ent[kQ];
         unsigned long long m[kQ];
         bool over = false;
+        // the list key: the f32 squared distance of the f32 points (two queries per packed
+        // instruction); the bounds carry its error (widen_bound), the final order uses exact keys
+        float dq[kQ];
+        {
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            const float px = valid ? T.tvec[slot] : INFINITY;
+            const float py = valid ? T.tvec[v.ld + slot] : INFINITY;
+            const float pz = valid ? T.tvec[2 * (size_t)v.ld + slot] : INFINITY;
+            const f2* qf2 = reinterpret_cast<const f2*>(qv);
+            const f2 pxx = f2{px, px}, pyy = f2{py, py}, pzz = f2{pz, pz};
+            // a - b as one v_pk_add_f32 (the compiler splits a broadcast operand into two v_sub_f32)
+            auto pk_sub = [](f2 a, f2 b) __attribute__((always_inline)) {
+                f2 r;
+                asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+                return r;
+            };
+#pragma unroll
+            for (int jp = 0; jp < kQ / 2; ++jp) {
+                const f2 ex = pk_sub(qf2[jp], pxx), ey = pk_sub(qf2[kQ / 2 + jp], pyy), ez = pk_sub(qf2[kQ + jp], pzz);
+                f2 s2 = ex * ex;
+                s2 = __builtin_elementwise_fma(ey, ey, s2);
+                s2 = __builtin_elementwise_fma(ez, ez, s2);
+                dq[2 * jp] = s2.x;
+                dq[2 * jp + 1] = s2.y;
+            }
+        }
 #pragma unroll
         for (int j = 0; j < kQ; ++j) {
             ent[j] = (__float_as_uint(dq[j]) & ~kIdBits) | id;
             m[j] = __ballot(ent[j] <= Tq[j]);
             over |= nbq[j] + (unsigned)__popcll(m[j]) > (unsigned)kCap;
         }
-        if (over) return false;
+        if (over) {  // a list would overflow: the caller tightens the bounds and rescans the leaf
+            --nlist;
+            --n_leaves;
+            return false;
+        }
 #pragma unroll
         for (int j = 0; j < kQ; ++j) {
             if (ent[j] <= Tq[j]) {  // (the ballot's own compare: the exec mask, no bit test of m)
@@ -797,51 +687,15 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
     };
 
     if (mode == 1) {
-        reinterpret_cast<uint4*>(&s_hist[wid][0][0])[lane] = make_uint4(0u, 0u, 0u, 0u);  // the wave's 1 KB
-        __builtin_amdgcn_wave_barrier();
+        // The leaves holding the eight queries, then their tree-order neighbours, every
+        // point accepted, until each query has Kw candidates: the first bound.
         const int lf0 = tree_node_of(w0 - cl.off, n, T.L), lf1 = tree_node_of(w0 + kQ - 1 - cl.off, n, T.L);
         const int nleaf = 1 << T.L;
-        // The seed: the leaves holding the eight queries, then their tree-order neighbours
-        // until they hold Kw points (and further while kSeed allows a whole leaf more).
         int s_lo = lf0, s_hi = lf1;
-        {
-            int tot = tree_first(n, T.L, lf1 + 1) - tree_first(n, T.L, lf0);
-            bool up = true;
-            for (;;) {
-                const bool more_hi = s_hi < nleaf - 1, more_lo = s_lo > 0;
-                if (!(more_hi || more_lo)) break;
-                const int cand = (more_hi && (up || !more_lo)) ? s_hi + 1 : s_lo - 1;
-                const int csz = tree_first(n, T.L, cand + 1) - tree_first(n, T.L, cand);
-                if (!(tot < Kw || tot + csz <= kSeed)) break;
-                if (cand > s_hi) s_hi = cand; else s_lo = cand;
-                tot += csz;
-                up = !up;
-            }
-        }
-        // The histogram range of query j: 64 buckets below the bucket of the largest
-        // possible seed key (the farthest corner of a seed leaf's f32 box; lane l of group g:
-        // seed leaves l, l + 8, ...), so that the Kw-th seed key is in range unless the seed
-        // spreads over more than 2^(64 >> (kHSh - 17)) times the squared distance of the Kw-th.
-        {
-            const float qx = qv[g], qy = qv[kQ + g], qz = qv[2 * kQ + g];
-            float tmax = 0.f;
-            for (int i = s_lo + l; i <= s_hi; i += 8) {
-                const float* lo = tlo + ((size_t)c * T.nnodes + first_leaf + i) * 3;
-                const float* hi = thi + ((size_t)c * T.nnodes + first_leaf + i) * 3;
-                const float dx = fmaxf(fabsf(qx - lo[0]), fabsf(hi[0] - qx));
-                const float dy = fmaxf(fabsf(qy - lo[1]), fabsf(hi[1] - qy));
-                const float dz = fmaxf(fabsf(qz - lo[2]), fabsf(hi[2] - qz));
-                tmax = fmaxf(tmax, fmaf(dz, dz, fmaf(dy, dy, dx * dx)));
-            }
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) tmax = fmaxf(tmax, xor_lane(tmax, o));  // (one floor for the wave)
-            const unsigned top = f32_up_bits((double)tmax * (1.0 + 1e-5)) >> kHSh;
-            Fw = __builtin_amdgcn_readfirstlane(top >= 63u ? (top - 63u) << kHSh : 0u);
-        }
         // Then every leaf whose box may hold a point within the largest bound of the
         // eight (squared box-to-box distance from the queries' f32 box, f32 boxes inflated
         // to bound the f64 points): level-A nodes 64 per instruction, then the leaves of
-        // each open one, counted outward from the queries and re-tested as bounds shrink.
+        // each open one, scanned outward from the queries and re-tested as bounds shrink.
         auto thr_f = [&]() __attribute__((always_inline)) {
             unsigned tm = 0u;
 #pragma unroll
@@ -861,46 +715,45 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
         };
         const int sh = T.L > 6 ? 6 : T.L;
         const int nA = 1 << (T.L - sh), firstA = nA - 1;
-        // One loop, one site each for counting a leaf, moving the bounds, appending a leaf and
-        // the sorted tightening (the kernel's code and registers stay small): stage 0 the
-        // seed leaves, 2 level-A nodes, 3 the leaves of the current level-A node, 4 the
-        // collect pass over the leaf table.  In the collect pass a list that would overflow
-        // (a loose bound over massive ties) is tightened and the leaf retried, then appended
-        // in halves; still no room: the exact kernel.
-        int stage = 0, nxt = s_lo, c0 = 0, l0 = 0;
-        bool haveA = false;
+        // one loop, one scan site: stage 0 the queries' own leaves, 1 their tree-order
+        // neighbours until Kw candidates exist (accept-all), 2 level-A nodes, 3 the leaves
+        // of the current level-A node
+        // A leaf that does not fit a list: tighten and retry; then its two halves (each
+        // after a tightening if needed); still no room (massive ties at the bound): the
+        // exact kernel.  One tightening site keeps the kernel's code and registers small.
+        int stage = 0, nxt = lf0, c0 = 0, l0 = 0;
+        bool up = true, haveA = false;
         float lbA = INFINITY, lbL = INFINITY;
         OutwardBits itA(0ull, 0), itL(0ull, 0);
-        float tf = INFINITY;
-        int cur = -1, cur_li = 0, part = 0, lfi = 0;
-        unsigned long long mk = 0ull;
-        bool do_update = false, do_tighten = false, retried = false, end_retried = false;
+        int cur = -1, part = 0;
+        bool do_tighten = false, retried = false;
+        float tf = INFINITY;  // f32 box-test bound of the union of the eight (set with each tightening)
         while (!fb_wave) {
-            if (do_update) {
-                do_update = false;
-                if (update()) tf = thr_f();  // the box-test bound changes only here
-            }
             if (do_tighten) {
                 PROF8_NOW(t_t0);
                 tighten();
                 PROF8_NOW(t_t1);
                 PROF8_ADD(c_tight, t_t0, t_t1);
                 do_tighten = false;
+                tf = thr_f();  // the box-test bound changes only here
+#if defined(SE3ICP_LRF8_CUT) && SE3ICP_LRF8_CUT == 4
+                if (stage == 2) break;  // (measurement build: stop after the first bound)
+#endif
             }
-            if (cur >= 0) {
-                if (stage < 4) {  // counting leaf cur
-                    count_leaf(cur);
-                    cur = -1;
-                    do_update = true;
-                    continue;
-                }
-                if (append_leaf(cur_li, cur, part)) {  // appending leaf cur (part)
+            if (cur >= 0) {  // appending leaf cur (part)
+#if defined(SE3ICP_LRF8_CUT) && SE3ICP_LRF8_CUT == 5
+                if (stage >= 2) { cur = -1; part = 0; ++n_leaves; continue; }  // (measurement build: no scans after the first bound)
+#endif
+                if (scan_leaf(cur, part)) {
                     if (part == 1) part = 2;
                     else { cur = -1; part = 0; }
                     retried = false;
-                } else if (!retried) {
+                } else if (!retried && (int)nbq[0] >= Kw) {
                     do_tighten = true;
                     retried = true;
+#ifdef SE3ICP_PROF
+                    ++n_tover;
+#endif
                 } else if (part == 0) {
                     part = 1;
                     retried = false;
@@ -913,68 +766,59 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
             int leaf = -1;
             if (stage == 0) {
                 leaf = nxt++;
-                if (nxt > s_hi) stage = 2;
-#if defined(SE3ICP_LRF8_CUT) && SE3ICP_LRF8_CUT == 5
-                if (nxt > s_hi) stage = 4;  // (measurement build: no traversal after the seed)
-#endif
+                if (nxt > lf1) stage = 1;
+            } else if (stage == 1) {
+                // (filling the lists beyond Kw while a whole leaf still fits: the first
+                // bound, the Kw-th of more nearby points, is tighter)
+                const bool more_hi = s_hi < nleaf - 1, more_lo = s_lo > 0;
+                const int cand = (more_hi && (up || !more_lo)) ? s_hi + 1 : s_lo - 1;
+                const int csz = (more_hi || more_lo) ? tree_first(n, T.L, cand + 1) - tree_first(n, T.L, cand) : 0;
+                if ((more_hi || more_lo) && ((int)nbq[0] < Kw || (int)nbq[0] + csz <= kFill)) {
+                    leaf = cand;
+                    if (cand > s_hi) s_hi = cand; else s_lo = cand;
+                    up = !up;
+                } else {
+                    do_tighten = true;
+                    stage = 2;
+                    continue;
+                }
             } else if (stage == 2) {
                 if (!haveA) {
-                    if (c0 >= nA) {  // counted: the collect pass
-#if defined(SE3ICP_LRF8_CUT) && SE3ICP_LRF8_CUT == 4
-                        break;  // (measurement build: stop after the count pass)
+                    if (c0 >= nA) {  // done; the final sort takes lists of <= 128: tighten once more
+                        unsigned nmax = 0;
+#pragma unroll
+                        for (int j = 0; j < kQ; ++j) nmax = max(nmax, nbq[j]);
+                        if (nmax > 128 && !retried) {
+#ifdef SE3ICP_PROF
+                            ++n_tend;
 #endif
-                        stage = 4;
-                        tf = thr_f();
-                        lfi = 0;
-                        float lb = INFINITY;
-                        if (lane < nlist) {
-                            lfi = tree_node_of(leaves[lane] - cl.off, n, T.L);
-                            lb = box_lb(first_leaf + lfi);
+                            do_tighten = true;
+                            retried = true;
+                            continue;
                         }
-                        mk = __ballot(lb <= tf);
-                        continue;
+                        if (nmax > 128) { fb_wave = true; PROF8_FB(2); }  // (ties at the bound)
+                        break;
                     }
                     const int ai = c0 + lane;
                     lbA = ai < nA ? box_lb(firstA + ai) : INFINITY;
                     itA = OutwardBits(__ballot(lbA <= tf), (lf0 >> sh) - c0);
                     haveA = true;
                 }
-                const int ja = itA.next();
-                if (ja < 0) { haveA = false; c0 += 64; continue; }
-                if (!(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbA), ja)) <= tf)) continue;
-                l0 = (c0 + ja) << sh;
+                const int j = itA.next();
+                if (j < 0) { haveA = false; c0 += 64; continue; }
+                if (!(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbA), j)) <= tf)) continue;
+                l0 = (c0 + j) << sh;
                 const int li = l0 + lane;
                 lbL = INFINITY;
                 if ((int)(lane < (1 << sh)) & ((int)(li < s_lo) | (int)(li > s_hi))) lbL = box_lb(first_leaf + li);
                 itL = OutwardBits(__ballot(lbL <= tf), lf0 - l0);
                 stage = 3;
                 continue;
-            } else if (stage == 3) {
+            } else {
                 const int t = itL.next();
                 if (t < 0) { stage = 2; continue; }
                 if (!(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbL), t)) <= tf)) continue;
                 leaf = l0 + t;
-            } else {
-                if (mk == 0ull) {  // collected; the final sort takes lists of <= 128: tighten once more
-                    unsigned nmax = 0;
-#pragma unroll
-                    for (int j = 0; j < kQ; ++j) nmax = max(nmax, nbq[j]);
-                    if (nmax > 128 && !end_retried) {
-#ifdef SE3ICP_PROF
-                        ++n_tend;
-#endif
-                        do_tighten = true;
-                        end_retried = true;
-                        continue;
-                    }
-                    if (nmax > 128) { fb_wave = true; PROF8_FB(2); }  // (ties at the bound)
-                    break;
-                }
-                cur_li = __builtin_ctzll(mk);
-                mk &= mk - 1ull;
-                leaf = __builtin_amdgcn_readlane(lfi, cur_li);
-                part = 0;
-                retried = false;
             }
             cur = leaf;
         }
@@ -1041,7 +885,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
     // two kernels' frames agree bit for bit; the TOLDI and the normal sums are two passes
     // (their live registers do not add up).
     const unsigned* rl = lists + g * kStride;
-    const Park pj = park_of(wid, g);
+    double* pj = park_of(wid, g);
     {
         double x[12];
 #pragma unroll
@@ -1105,14 +949,15 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
         __builtin_amdgcn_wave_barrier();
         if (l == 0) {
             const int flags = mine ? ((want_t ? 1 : 0) | (want_n ? 2 : 0)) : 0;
-            pj.i[PI_FLAGS] = (unsigned)flags;
+            pj[P8_FLAGS] = (double)flags;
             if (mine) {
 #pragma unroll
                 for (int i = 0; i < 9; ++i) pj[P8_SUM + 12 + i] = x[i];
-                pj.i[PI_KK] = (unsigned)kk;
-                pj.i[PI_GP] = (unsigned)(cl.off + T.perm[wq]);
-                pj.i[PI_NTOP] = (unsigned)nTop;
-                pj.i[PI_W] = (unsigned)wq;
+                pj[P8_KK] = (double)kk;
+                pj[P8_GP] = (double)(cl.off + T.perm[wq]);
+                pj[P8_K] = (double)K;
+                pj[P8_NTOP] = (double)nTop;
+                pj[P8_W] = (double)wq;
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -1134,9 +979,9 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
     // TOLDI: C about the quirk centroid cl = (S' - q) / rz (ISR.cpp:259-272, see k_knn.hip),
     // its smallest eigenvector by cyclic Jacobi; normals: FastEigen3x3 of the kn-point
     // covariance (Open3D EstimateNormals, ISR.cpp:643) and the GICP covariance from it.
-    auto toldi_eig = [&](const Park& pb) __attribute__((always_inline)) {
-        const p3 q = ld3(P4, (int)pb.i[PI_W]);  // the query's tree slot
-        const double rz = (double)((int)pb.i[PI_KK] / 3);
+    auto toldi_eig = [&](double* pb) __attribute__((always_inline)) {
+        const p3 q = ld3(P4, (int)pb[P8_W]);  // the query's tree slot
+        const double rz = (double)((int)pb[P8_KK] / 3);
         const double q3[3] = {q.x, q.y, q.z};
         double cq[3], S[3];
 #pragma unroll
@@ -1144,20 +989,21 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
             cq[a] = (pb[P8_SUM + a] - q3[a]) / rz;
             S[a] = pb[P8_SUM + 3 + a];
         }
+        const double* M = pb + P8_SUM + 6;
         const int ia[6] = {0, 0, 0, 1, 1, 2}, ib[6] = {0, 1, 2, 1, 2, 2};
         double c6[6];
 #pragma unroll
         for (int k = 0; k < 6; ++k)
-            c6[k] = pb[P8_SUM + 6 + k] - S[ia[k]] * cq[ib[k]] - cq[ia[k]] * S[ib[k]] + rz * cq[ia[k]] * cq[ib[k]];
+            c6[k] = M[k] - S[ia[k]] * cq[ib[k]] - cq[ia[k]] * S[ib[k]] + rz * cq[ia[k]] * cq[ib[k]];
         const d3 zn = jacobi_smallest_evec(c6[0], c6[1], c6[2], c6[3], c6[4], c6[5]);
         pb[P8_ZN] = zn.x;
         pb[P8_ZN + 1] = zn.y;
         pb[P8_ZN + 2] = zn.z;
     };
-    auto normal_eig = [&](const Park& pb) __attribute__((always_inline)) {
-        const int wb = (int)pb.i[PI_W];
+    auto normal_eig = [&](const double* pb) __attribute__((always_inline)) {
+        const int wb = (int)pb[P8_W];
         const int cc = cloud_of[wb];
-        const int knb = min(setup[cc].k_nrm, (int)pb.i[PI_NTOP]);
+        const int knb = min(setup[cc].k_nrm, (int)pb[P8_NTOP]);
         double n6[6] = {1, 0, 0, 1, 0, 1};
         if (knb >= 3) {
             double cu[9];
@@ -1172,7 +1018,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
         }
         d3 nm = fast_eigen3x3(n6[0], n6[1], n6[2], n6[3], n6[4], n6[5]);
         if (sqrt(dot3(nm, nm)) == 0.0) nm = d3{0, 0, 1};
-        const int gp = (int)pb.i[PI_GP];
+        const int gp = (int)pb[P8_GP];
         v.nrm64[gp] = nm.x;
         v.nrm64[v.ld + gp] = nm.y;
         v.nrm64[2 * (size_t)v.ld + gp] = nm.z;
@@ -1181,8 +1027,8 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
     // (cyclic Jacobi), wave 1 the normals at the same time.
     __syncthreads();
     if (wid <= 1) {
-        const Park pb = park_of(lane < kW * kQ ? lane / kQ : 0, lane % kQ);
-        const int b_flags = lane < kW * kQ ? (int)pb.i[PI_FLAGS] : 0;
+        double* pb = park_of(lane < kW * kQ ? lane / kQ : 0, lane % kQ);
+        const int b_flags = lane < kW * kQ ? (int)pb[P8_FLAGS] : 0;
         if ((b_flags & 1) && wid == 0) toldi_eig(pb);
         if ((b_flags & 2) && wid == 1) normal_eig(pb);
     }
@@ -1190,12 +1036,12 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
 
     // ---------------------------------------------------------------- TOLDI axes (ISR.cpp:286-306)
     {
-        const int flags = (int)pj.i[PI_FLAGS];
+        const int flags = (int)pj[P8_FLAGS];
         double x6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         if (flags & 1) {
             const double nx = pj[P8_ZN], ny = pj[P8_ZN + 1], nz = pj[P8_ZN + 2];
             const double R = pj[P8_R];
-            const int kkq = (int)pj.i[PI_KK];
+            const int kkq = (int)pj[P8_KK];
             p3 pn = ld3(P4, (int)rl[max(min(1 + l, kkq - 1), 0)]);
             for (int r = 1 + l; r < kkq; r += 8) {  // ranks 1 .. kk-1
                 const p3 p = pn;
@@ -1223,10 +1069,10 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
     // the frames (ISR.cpp:298-307, 597-607), on wave 0 for the block's 32 queries
     __syncthreads();
     if (wid == 0) {
-        const Park pb = park_of(lane < kW * kQ ? lane / kQ : 0, lane % kQ);
-        const int b_flags = lane < kW * kQ ? (int)pb.i[PI_FLAGS] : 0;
+        const double* pb = park_of(lane < kW * kQ ? lane / kQ : 0, lane % kQ);
+        const int b_flags = lane < kW * kQ ? (int)pb[P8_FLAGS] : 0;
         if (b_flags & 1) {
-            const int w = (int)pb.i[PI_W];
+            const int w = (int)pb[P8_W];
             const CloudSetup sw = setup[cloud_of[w]];
             const p3 q = ld3(P4, w);
             d3 nrm{pb[P8_ZN], pb[P8_ZN + 1], pb[P8_ZN + 2]};
@@ -1240,7 +1086,7 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
             const double al = sw.alpha, be = sw.beta;
             const double f12[12] = {al * xax.x, al * xax.y, al * xax.z, al * yax.x, al * yax.y, al * yax.z,
                                     al * zax.x, al * zax.y, al * zax.z, be * q.x, be * q.y, be * q.z};
-            store_frame_rows(v.fr64, v.fr32, (int)pb.i[PI_GP], f12, sw.cf_target, q.x, q.y, q.z);
+            store_frame_rows(v.fr64, v.fr32, (int)pb[P8_GP], f12, sw.cf_target, q.x, q.y, q.z);
         }
     }
 #ifdef SE3ICP_PROF
