@@ -33,6 +33,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path[:0] = [os.path.join(ROOT, "se3-icp_amd"), ROOT]
 
 FP32_PEAK_TFLOPS = 157.3   # MI355X vector (= f32 MFMA) peak, /opt/skills/guides/MI355X_MICROARCH.md
+FP64_VEC_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak (same guide)
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak, same guide
 N_SIMDS = 1024             # 256 CUs x 4 SIMDs (same guide)
 CLOCK_GHZ = 2.4            # peak engine clock (same guide)
@@ -340,7 +341,9 @@ def main():
                     "exact_kernel_queries_per_step": ktot.get("lrf_fallback", 0.0) / args.steps}
         wl = args.workload if args.c2_cloud == "downsample" else f"{args.workload}u"
         roof_nn = nn_roofline(ktot, kms, wl)
-        roof_lrf = lrf_roofline(ktot, kms, args.steps, W["params"]["number_of_nn_for_LRF"], wl)
+        # (normals, KNN 30, ISR.cpp:643: both clouds for GICP, the targets for pt2pl, none for pt2pt)
+        roof_lrf = lrf_roofline(ktot, kms, args.steps, W["params"]["number_of_nn_for_LRF"], wl,
+                                {"gicp": 30, "pt2pl": 15, "pt2pt": 0}[W["variant"]])
         roof_red = reduce_roofline(last, pairs, W, kms["reduce_ms"] / args.steps, wl)
         # the bench line's roofline is the step's dominant kernel by GPU time; the other
         # named kernel is reported beside it
@@ -406,9 +409,11 @@ def nn_roofline(ktot, kms, wl):
     if dom == "nn_se3_ms":
         D, evals, boxes, nl, kname = 12, ktot["se3_dist_evals"], ktot["se3_box_tests"], ktot["nn_se3_launches"], \
             "k_nn_search<12>"
+        useful = ktot.get("se3_useful_evals", 0.0)
     else:
         D, evals, boxes, nl, kname = 3, ktot["r3_dist_evals"], ktot["r3_box_tests"], ktot["nn_r3_launches"], \
             "k_nn_search<3>"
+        useful = ktot.get("r3_useful_evals", 0.0)
     t_ms = kms[dom]
     flop_dist, flop_box = 3 * D, 4 * D
     flops = evals * flop_dist + boxes * flop_box
@@ -431,7 +436,14 @@ def nn_roofline(ktot, kms, wl):
         "avg_launch_ms": round(t_ms / nl, 4),
         "launches": int(nl),
         "flop_per_unit": {"distance_eval": flop_dist, "box_test": flop_box},
-        "units_per_launch": {"distance_evals": round(evals / nl), "box_tests": round(boxes / nl)},
+        "units_per_launch": {"distance_evals": round(evals / nl), "box_tests": round(boxes / nl),
+                             "useful_distance_evals": round(useful / nl)},
+        # the distance evaluations of occupied (query, target) pairs only -- the lanes a sweep
+        # keeps busy without a query that wants the leaf are not work (round 6)
+        "useful": {"distance_evals_per_launch": round(useful / nl),
+                   "share_of_evaluation_slots": round(useful / evals, 4) if evals else None,
+                   "achieved_tflops": round(useful * flop_dist / (t_ms / 1000.0) / 1e12, 3) if t_ms > 0 else None,
+                   "frac": round(useful * flop_dist / (t_ms / 1000.0) / 1e12 / FP32_PEAK_TFLOPS, 4) if t_ms > 0 else None},
         "traffic": traffic,
         "traffic_source": src,
     }
@@ -447,9 +459,45 @@ def busy_fraction(quad_cycles, t_ms):
     return round(b, 3) if b <= 1.0 else None
 
 
-def lrf_roofline(ktot, kms, steps, k, wl):
+def lrf_fp64_flops_per_point(k: int, k_nrm: int, ncand: float) -> float:
+    """f64 flops the reference's own arithmetic needs per point on the TOLDI / normals path
+    (ISR.cpp:241-331, Open3D EstimateNormals at ISR.cpp:643): the exact squared distances of
+    the final candidates (3 sub, 3 mul, 2 add each), the TOLDI neighbour sums over ranks
+    1..k/3 (21 per rank: the offset, its 3 + 3 running sums and the 6 moments), the radius
+    (8), the normal cumulants over k_nrm ranks (15 per rank), the two 3x3 eigen-problems
+    (covariance assembly + cyclic Jacobi ~400, FastEigen3x3 ~115), the TOLDI axis sums over
+    ranks 1..k-1 (26 per rank: offset, dot, distance, weight, weighted sum) and the frame
+    (~60).  Counted from the kernel's loops, not measured."""
+    rz = k // 3
+    return 8.0 * ncand + 21.0 * rz + 8.0 + 15.0 * k_nrm + 400.0 + 115.0 + 26.0 * (k - 1) + 60.0
+
+
+def lrf_sections():
+    """Per-wave VALU counts of k_lrf8's sections from the newest committed section profile
+    (profiles/*_lrf8_sections.txt, tools/lrf_sections.sh): the share of the kernel's VALU
+    spent in the reference's math (neighbour sums, eigen-solves, axes, frames) against the
+    kNN selection (traversal, bound tightenings, final order)."""
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_lrf8_sections.txt")), reverse=True)
+    for f in files:
+        tot, math = None, 0.0
+        for line in open(f):
+            parts = line.split()
+            if len(parts) > 2 and parts[0] == "lib":
+                tot = float(parts[1])
+            if "neighbour sums:" in line or "eigen-solves, axes, frames:" in line:
+                math += float(line.split(":")[-1].split("VALU")[0].strip().lstrip("+"))
+        if tot:
+            return {"valu_per_wave": tot, "math_valu_per_wave": math, "useful_valu_frac": round(math / tot, 3),
+                    "source": os.path.relpath(f, ROOT)}
+    return None
+
+
+def lrf_roofline(ktot, kms, steps, k, wl, k_nrm=30):
     """k_lrf, the setup's fused kNN-k + TOLDI + normals kernel, one launch per step, priced
-    with SURVEY.md §8(d)'s TOLDI unit: k neighbour gathers of 24 B (f64 xyz) per point."""
+    with SURVEY.md §8(d)'s TOLDI unit: k neighbour gathers of 24 B (f64 xyz) per point.  The
+    kernel is bound by VALU issue (bound "valu"); beside the HBM fraction the line carries
+    the f64 algorithmic flops against the FP64 vector peak and the share of its VALU that is
+    the reference's math (useful_valu_frac)."""
     t_ms = kms["lrf_ms"] / steps
     q = ktot.get("lrf_queries", 0.0) / steps
     bpp = 24.0 * k
@@ -459,16 +507,25 @@ def lrf_roofline(ktot, kms, steps, k, wl):
     # SIMD, summed over the chip's 1,024 SIMDs) over this launch pair's measured time
     av, _ = pmc_counter("k_lrf8", "SQ_ACTIVE_INST_VALU", wl)
     insts, _ = pmc_counter("k_lrf8", "SQ_INSTS_VALU", wl)
+    ncand = 8.0 * ktot.get("lrf_candidates", 0.0) / max(1.0, ktot.get("lrf_queries", 0.0))  # (one group in eight counted)
+    fpp = lrf_fp64_flops_per_point(k, k_nrm, ncand)
+    f64_tf = q * fpp / (t_ms / 1000.0) / 1e12 if t_ms > 0 else 0.0
     return {
         "kernel": "k_lrf8 + k_lrf (hand-overs)",
-        "bound": "hbm",
+        "bound": "valu",
         "note": "fused exact kNN-k (f64) + TOLDI frame + normals/GICP covariance per point: k_lrf8 (eight queries "
                 "per wavefront) and the exact one-query-per-wavefront k_lrf for the points it hands over, one HIP-event "
-                "bracket; algorithmic bytes = k neighbour gathers x 24 B per point (SURVEY.md §8d); the kernels are "
-                "VALU-issue bound, not HBM bound (valu_issue_busy: the fraction of the launch the SIMDs spend issuing "
-                "VALU, from this workload's committed PMC pass; DESIGN.md §5)",
+                "bracket; achieved/frac: algorithmic bytes = k neighbour gathers x 24 B per point (SURVEY.md §8d) "
+                "against HBM; the kernels are VALU-issue bound (valu_issue_busy: the fraction of the launch the SIMDs "
+                "spend issuing VALU, from this workload's committed PMC pass), most of it the kNN selection "
+                "(valu_sections.useful_valu_frac: the reference's math); fp64_algorithmic: the f64 flops of the "
+                "reference's arithmetic against the FP64 vector peak (DESIGN.md §5)",
         "valu_issue_busy": busy_fraction(av, t_ms),
         "valu_insts_per_point": round(insts / q, 1) if (insts and q) else None,
+        "fp64_algorithmic": {"flop_per_point": round(fpp), "candidates_per_point": round(ncand, 1),
+                             "achieved_tflops": round(f64_tf, 3), "peak_tflops": FP64_VEC_PEAK_TFLOPS,
+                             "frac": round(f64_tf / FP64_VEC_PEAK_TFLOPS, 4)},
+        "valu_sections": lrf_sections(),
         "achieved": round(achieved, 2),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SE3ICP_ABI_VERSION 3
+#define SE3ICP_ABI_VERSION 4
 
 typedef enum se3icp_status {
     SE3ICP_OK = 0,
@@ -234,6 +234,12 @@ int64_t se3icp_random_downsample(const double* xyz, int64_t n, double ratio, uin
  *            lrf_fallback}  (setup queries handed to the exact one-per-wave kNN kernel) */
 int se3icp_set_profiling(int device, int on);
 int se3icp_last_kernel_times(int device, double* out);
+/* The same record extended (ABI 4): out[SE3ICP_KERNEL_TIMES_N], n >= SE3ICP_KERNEL_TIMES_N
+ * (else SE3ICP_ERR_INVALID_ARG): the 24 values above, then se3_useful_evals, r3_useful_evals --
+ * the occupied (query, target) distance evaluations of the NN searches (the *_dist_evals
+ * count 64-lane evaluation slots, idle lanes of partly filled sweeps included). */
+#define SE3ICP_KERNEL_TIMES_N 26
+int se3icp_last_kernel_times_n(int device, double* out, int n);
 
 /* Per-iteration correspondence record of ONE pair of the next batch registered on
  * `device` (diagnostic; the parity tests compare it with the reference's loop

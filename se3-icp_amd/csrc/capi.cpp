@@ -308,8 +308,17 @@ int se3icp_set_nn_events(int device, int on) {
 }
 
 int se3icp_last_kernel_times(int device, double* out /* [24] */) {
+    double x[SE3ICP_KERNEL_TIMES_N];
+    const int rc = se3icp_last_kernel_times_n(device, x, SE3ICP_KERNEL_TIMES_N);
+    if (rc == 0)
+        for (int i = 0; i < 24; ++i) out[i] = x[i];
+    return rc;
+}
+
+int se3icp_last_kernel_times_n(int device, double* out, int n) {
     Engine* e = usable_engine(device);
     if (!e || !out) return SE3ICP_ERR_NO_DEVICE;
+    if (n < SE3ICP_KERNEL_TIMES_N) return SE3ICP_ERR_INVALID_ARG;
     const auto& k = e->kernel_times();
     out[0] = k.nn_se3_ms;
     out[1] = k.nn_r3_ms;
@@ -335,6 +344,8 @@ int se3icp_last_kernel_times(int device, double* out /* [24] */) {
     out[21] = k.r3_queries;
     out[22] = k.r3_searched;
     out[23] = k.lrf_fallback;
+    out[24] = k.se3_useful_evals;
+    out[25] = k.r3_useful_evals;
     return 0;
 }
 

@@ -20,7 +20,10 @@ namespace se3icp {
 constexpr int kSmallK = 128;      // neighbourhoods the LDS kNN kernels hold; larger ones: k_knn_big.hip
 constexpr int kBlock = 256;       // threads per block of the streaming/sweep kernels
 constexpr int kRedVals = 28;      // 21 JTJ upper + 6 JTr + 1 mse-sum (pt2pt reuses the slots)
-constexpr int kStatCols = 15;     // columns of the device work-counter table (View::stats); 8..14: SE3ICP_PROF section cycles
+constexpr int kStatCols = 17;     // columns of the device work-counter table (View::stats); 8..14: SE3ICP_PROF section cycles
+// NN work: occupied (query, target) distance evaluations of the SE(3) / R3 searches (the
+// lane-evaluation slots they issue are columns 0 and 2)
+constexpr int kStatUseSe3 = 15, kStatUseR3 = 16;
 constexpr int kHist = 256;        // pose history ring of the loop (View::hist), iterations
 constexpr int kTrimList = 4096;   // k_trim: LDS key list / window capacity per pair
 constexpr int kTrimBlocks = 32;   // k_trim_window: blocks per pair

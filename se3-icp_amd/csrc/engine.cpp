@@ -851,6 +851,8 @@ int Engine::register_batch(int npairs, const double* const* src, const int64_t* 
         ktimes_.se3_searched = sum[5];
         ktimes_.r3_queries = sum[6];
         ktimes_.r3_searched = sum[7];
+        ktimes_.se3_useful_evals = sum[kStatUseSe3];
+        ktimes_.r3_useful_evals = sum[kStatUseR3];
 #ifdef SE3ICP_PROF
         {
             const double nw = std::max(1.0, std::floor(sum[11] / 17592186044416.0));

@@ -32,6 +32,7 @@ struct KernelTimes {
     // work actually done by the NN kernels (device counters): lane-distance evaluations
     // in leaf sweeps and lane-box tests in the traversal
     double se3_dist_evals = 0, se3_box_tests = 0, r3_dist_evals = 0, r3_box_tests = 0;
+    double se3_useful_evals = 0, r3_useful_evals = 0;  // occupied (query, target) evaluations
     // fused kNN/TOLDI/normals kernel of the setup: time, queries, leaves scanned, sorts
     double lrf_ms = 0, lrf_queries = 0, lrf_leaves = 0, lrf_merges = 0, lrf_box_tests = 0, lrf_candidates = 0;
     double lrf_fallback = 0;  // queries k_lrf8 handed to the exact kernel

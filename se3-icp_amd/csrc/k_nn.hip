@@ -692,7 +692,7 @@ __device__ __forceinline__ void nn_finish(const View& v, const PairDev* P, int p
 template <int D>
 __device__ __forceinline__ void single_one(const View& v, const PairDev* P, int pair, const TreeRef& TR,
                                            const CloudDev& ct, int gx, int g, int lane, unsigned* n_eval,
-                                           unsigned* n_box, int tp_pre = -2, float mrg_pre = 0.f);
+                                           unsigned* n_box, unsigned* n_use, int tp_pre = -2, float mrg_pre = 0.f);
 
 template <int D>
 __device__ __forceinline__ void single_list(const View& v, int bw);
@@ -739,16 +739,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
             // a group of a few queries (a chunk's leftovers): each searched by all 64 lanes in
             // turn (single_one's lane-parallel search) -- a lone query with a wide ball would
             // otherwise walk the tree one node per step and set the launch's time
-            unsigned n_eval = 0, n_box = 0;
+            unsigned n_eval = 0, n_box = 0, n_use = 0;
             for (int q = 0; q < cnt_q; ++q) {
                 const int gxq = __builtin_amdgcn_readfirstlane(cs.off + v.qlist[(size_t)gi * 64 + q]);
                 const int gq = __builtin_amdgcn_readfirstlane(cs.off + TR.perm[gxq]);
-                single_one<D>(v, P, pair, TR, ct, gxq, gq, lane, &n_eval, &n_box);
+                single_one<D>(v, P, pair, TR, ct, gxq, gq, lane, &n_eval, &n_box, &n_use);
             }
             if (lane == 0) {
                 unsigned long long* st = v.stats + kStatCols * (gi & 63) + (D == 12 ? 0 : 2);
                 atomicAdd(st, 64ull * n_eval);
                 atomicAdd(st + 1, 64ull * n_box);
+                atomicAdd(v.stats + kStatCols * (gi & 63) + (D == 12 ? kStatUseSe3 : kStatUseR3), (unsigned long long)n_use);
             }
             return;
         }
@@ -826,6 +827,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
         int stk = 0;  // DFS stack in a VGPR: lane i holds entry i (depth <= 2L+1 < 64)
         int sp = 1;
         unsigned n_eval = 0, n_box = 0;  // wave-uniform work counters (roofline accounting)
+        unsigned n_use = 0;  // occupied (query, target) distance evaluations
+        const unsigned long long vmask = __ballot(valid);
     #ifdef SE3ICP_PROF
         unsigned n_want = 0, n_leafv = 0;
         unsigned long long c_leaf = 0, c_lload = 0;  // shader-clock cycles in leaf visits / their target loads
@@ -865,6 +868,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
                     if (W == 0ull) continue;
                     w = __popcll(W);
                 }
+                n_use += (unsigned)__popcll(W & vmask) * (unsigned)cnt;
     #ifdef SE3ICP_PROF
                 n_want += __popcll(W & __ballot(valid));
                 ++n_leafv;
@@ -973,6 +977,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
             unsigned long long* st = v.stats + kStatCols * (gi & 63) + (D == 12 ? 0 : 2);
             atomicAdd(st, 64ull * n_eval);
             atomicAdd(st + 1, 64ull * n_box);
+            atomicAdd(v.stats + kStatCols * (gi & 63) + (D == 12 ? kStatUseSe3 : kStatUseR3), (unsigned long long)n_use);
             // the wave's work (box-test steps + leaf sweeps): the chunk's cost for k_nn_order
     #ifdef SE3ICP_PROF
             if (D == 12) {
@@ -1057,7 +1062,7 @@ template <int D>
 // when the caller fetched them already (single_list); -2: load them here.
 __device__ __forceinline__ void single_one(const View& v, const PairDev* P, int pair, const TreeRef& TR,
                                            const CloudDev& ct, int gx, int g, int lane, unsigned* n_eval,
-                                           unsigned* n_box, int tp_pre, float mrg_pre) {
+                                           unsigned* n_box, unsigned* n_use, int tp_pre, float mrg_pre) {
     float q[D];
     float na;
     {
@@ -1146,6 +1151,7 @@ __device__ __forceinline__ void single_one(const View& v, const PairDev* P, int 
                     }
                 }
                 *n_eval += 1;
+                *n_use += (unsigned)(tb - ta);  // (the one query against every target of the leaf)
                 const bool lt = d < a1;
                 a2 = __builtin_amdgcn_fmed3f(a1, a2, d);
                 b1 = lt ? ta + lane : b1;
@@ -1196,7 +1202,7 @@ __device__ __forceinline__ void single_list(const View& v, int bw) {
     const int seg = (nq + 7) >> 3;
     const int f_end = min(nq, (xcd + 1) * seg);
     const int w0 = __builtin_amdgcn_readfirstlane(xcd * seg + (bw >> 3));
-    unsigned n_eval = 0, n_box = 0;
+    unsigned n_eval = 0, n_box = 0, n_use = 0;
     const TreeRef TR = (D == 12) ? v.t12 : v.t3;
     // The wave's next kSingleBatch list entries are set up together, one per lane (list entry
     // -> point -> pair -> clouds -> previous match -> its tree position, and the margin: a
@@ -1223,7 +1229,7 @@ __device__ __forceinline__ void single_list(const View& v, int bw) {
             const float mrg = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mj), j));
             const PairDev* P = v.pairs + pair;
             const CloudDev ct = v.clouds[P->tgt];
-            single_one<D>(v, P, pair, TR, ct, gx, g, lane, &n_eval, &n_box, kSingleBatch > 1 ? tp : -2, mrg);
+            single_one<D>(v, P, pair, TR, ct, gx, g, lane, &n_eval, &n_box, &n_use, kSingleBatch > 1 ? tp : -2, mrg);
 #ifdef SE3ICP_PROF
             ++n_sq;
 #endif
@@ -1242,6 +1248,7 @@ __device__ __forceinline__ void single_list(const View& v, int bw) {
         unsigned long long* st = v.stats + kStatCols * (w0 & 63) + (D == 12 ? 0 : 2);
         atomicAdd(st, 64ull * n_eval);
         atomicAdd(st + 1, 64ull * n_box);
+        atomicAdd(v.stats + kStatCols * (w0 & 63) + (D == 12 ? kStatUseSe3 : kStatUseR3), (unsigned long long)n_use);
     }
 }
 

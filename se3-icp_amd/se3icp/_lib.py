@@ -36,7 +36,7 @@ EXPORTED_SYMBOLS = [
     "se3icp_toldi_frames", "se3icp_knn_self", "se3icp_estimate_normals", "se3icp_nn",
     "se3icp_synthetic_pairs", "se3icp_synthetic_reference", "se3icp_synthetic_reference_device",
     "se3icp_random_downsample",
-    "se3icp_set_profiling", "se3icp_last_kernel_times", "se3icp_set_trace", "se3icp_set_lrf_exact",
+    "se3icp_set_profiling", "se3icp_last_kernel_times", "se3icp_last_kernel_times_n", "se3icp_set_trace", "se3icp_set_lrf_exact",
     "se3icp_set_nn_events",
     # include/se3icp_cc.h: metrics and pose files of the benchmark drivers (host only)
     "se3icp_cc_rot_3d", "se3icp_cc_angular_error_so3", "se3icp_cc_angular_error_so3_alt",
@@ -155,6 +155,7 @@ def load():
     L.se3icp_random_downsample.argtypes = [dp, C.c_int64, C.c_double, C.c_uint32, dp]
     L.se3icp_set_profiling.argtypes = [C.c_int, C.c_int]
     L.se3icp_last_kernel_times.argtypes = [C.c_int, dp]
+    L.se3icp_last_kernel_times_n.argtypes = [C.c_int, dp, C.c_int]
     L.se3icp_set_trace.argtypes = [C.c_int, C.POINTER(Trace)]
     L.se3icp_set_lrf_exact.argtypes = [C.c_int, C.c_int]
     L.se3icp_set_nn_events.argtypes = [C.c_int, C.c_int]

@@ -243,7 +243,8 @@ class DeviceBatchRunner:
     _KT_KEYS = ["nn_se3_ms", "nn_r3_ms", "recheck_ms", "trim_ms", "reduce_ms", "setup_ms", "nn_se3_launches",
                 "nn_r3_launches", "se3_dist_evals", "se3_box_tests", "r3_dist_evals", "r3_box_tests",
                 "lrf_ms", "lrf_queries", "lrf_leaves", "lrf_merges", "lrf_box_tests", "lrf_candidates",
-                "nn_prep_ms", "se3_queries", "se3_searched", "r3_queries", "r3_searched", "lrf_fallback"]
+                "nn_prep_ms", "se3_queries", "se3_searched", "r3_queries", "r3_searched", "lrf_fallback",
+                "se3_useful_evals", "r3_useful_evals"]
 
     def __init__(self, src_ptr: int, src_off, tgt_ptr: int, tgt_off, method: str,
                  params: _lib.Params | None = None, device: int = 0, slots: int = 1):
@@ -258,14 +259,14 @@ class DeviceBatchRunner:
         self._params = params or _lib.default_params()
         self._pref = C.byref(self._params)
         self._res = [(_lib.Result * self.n)() for _ in range(max(1, slots))]
-        self._kt = [(C.c_double * 24)() for _ in range(max(1, slots))]
+        self._kt = [(C.c_double * len(self._KT_KEYS))() for _ in range(max(1, slots))]
 
     def run(self, slot: int = 0) -> None:
         rc = self._L.se3icp_register_batch_device(self._dev, self.n, self._src, self._so, self._tgt, self._to,
                                                   self._mid, self._pref, self._res[slot], None)
         if rc not in (_lib.OK, _lib.ERR_NONFINITE):
             raise _lib.Se3IcpError(rc, "register_batch_device")
-        self._L.se3icp_last_kernel_times(self._dev, self._kt[slot])
+        self._L.se3icp_last_kernel_times_n(self._dev, self._kt[slot], len(self._KT_KEYS))
 
     def results(self, slot: int = 0) -> list[PairResult]:
         return _results(self._res[slot], self.n)
@@ -361,10 +362,7 @@ def set_profiling(on: bool, device: int = 0) -> None:
 
 
 def last_kernel_times(device: int = 0) -> dict:
-    out = (C.c_double * 24)()
-    _lib.check(_lib.load().se3icp_last_kernel_times(device, out))
-    keys = ["nn_se3_ms", "nn_r3_ms", "recheck_ms", "trim_ms", "reduce_ms", "setup_ms", "nn_se3_launches",
-            "nn_r3_launches", "se3_dist_evals", "se3_box_tests", "r3_dist_evals", "r3_box_tests",
-            "lrf_ms", "lrf_queries", "lrf_leaves", "lrf_merges", "lrf_box_tests", "lrf_candidates",
-            "nn_prep_ms", "se3_queries", "se3_searched", "r3_queries", "r3_searched", "lrf_fallback"]
+    keys = DeviceBatchRunner._KT_KEYS
+    out = (C.c_double * len(keys))()
+    _lib.check(_lib.load().se3icp_last_kernel_times_n(device, out, len(keys)))
     return dict(zip(keys, list(out)))

@@ -36,7 +36,7 @@ def test_library_exports_every_header_symbol(lib):
 
 def test_abi_version_and_status_strings(lib):
     import se3icp
-    assert lib.se3icp_abi_version() == 3
+    assert lib.se3icp_abi_version() == 4
     assert se3icp.status_string(0) == "ok"
     assert "no CPU fallback" in se3icp.status_string(-5)
 
