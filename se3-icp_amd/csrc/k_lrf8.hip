@@ -66,12 +66,6 @@ constexpr int kFill = SE3ICP_LRF8_FILL;
 constexpr int kStride = kCap + 4;
 static_assert(((kStride / 4) & 1) == 1, "an odd number of 16-B slots per list");
 constexpr int kLeaves = 64;              // leaves one wave may scan: candidate id = (list index << 6) | lane
-#ifndef SE3ICP_LRF8_PREFIX_PER
-#define SE3ICP_LRF8_PREFIX_PER 16
-#endif
-// tail entries per lane of the sort-free tightening (tighten_group_prefix): tails up to
-// 8 x this take it, longer ones (and the first tightening) the sorting one
-constexpr int kPrefixPer = SE3ICP_LRF8_PREFIX_PER;
 constexpr unsigned kIdBits = 0xfffu;     // low bits of a list entry: the candidate id
 // bound of the accept-all phase: every finite key (a lane past the leaf's end carries an
 // infinite distance, so its entry is above every bound)
@@ -321,87 +315,6 @@ __device__ __forceinline__ uint3 tighten_group_sorted(unsigned* lists, int g, in
         __builtin_amdgcn_wave_barrier();
     }
     return make_uint3(tg, keep_n, 0u);
-}
-
-// exclusive prefix sum of x over the eight lanes of a group (lane order) and the group's total
-__device__ __forceinline__ unsigned gscan8(unsigned x, int l, unsigned& total) {
-    unsigned p = 0u, s = x;
-#pragma unroll
-    for (int d = 1; d <= 4; d <<= 1) {
-        const unsigned t = gx(s, d);
-        if (l & d) p += t;
-        s += t;
-    }
-    total = s;
-    return p;
-}
-
-// Bound tightening without a sort (round 6), for a list whose first mv >= Kw entries are
-// sorted (A: the kept set of an earlier tightening) and whose tail B (nb <= 8 * PER entries
-// appended since) is not.  The bound only has to be an upper bound of the Kw-th smallest
-// entry (the final order is exact), and with f(i) = i + 1 + #{b in B : b <= A[i]}
-// increasing, A[i*] for the smallest i with f(i) >= Kw is one: at least Kw entries are
-// <= A[i*], and the Kw-th smallest lies in (A[i*-1], A[i*]] -- within one gap of the sorted
-// prefix of the exact value.  i* is found by a few probes (each a broadcast LDS read of A[i]
-// and a count over the tail, eight lanes per query), starting at the interpolation guess
-// Kw - 1 - #{b <= A[Kw-1]}.  The kept entries of A stay a sorted prefix; the kept entries
-// of B are compacted behind them, unsorted (the next tightening's tail).
-// Returns (bound, kept, new sorted prefix) for the group, as tighten_group_sorted.
-template <int PER>
-__device__ __forceinline__ uint3 tighten_group_prefix(unsigned* lists, int g, int l, int nbg, int mv, int Kw, float S) {
-    unsigned* list = lists + g * kStride;
-    const int nb = nbg - mv;
-    const unsigned* B = list + mv;
-    unsigned b[PER];
-#pragma unroll
-    for (int s = 0; s < PER; ++s) {
-        const int e = l + 8 * s;
-        b[s] = e < nb ? B[e] : kPad;
-    }
-    auto count_le = [&](unsigned t) __attribute__((always_inline)) {
-        unsigned cnt = 0u;
-#pragma unroll
-        for (int s = 0; s < PER; ++s) cnt += b[s] <= t ? 1u : 0u;
-        cnt += gx(cnt, 1);
-        cnt += gx(cnt, 2);
-        cnt += gx(cnt, 4);
-        return (int)cnt;
-    };
-    // smallest i in [lo, hi] with f(i) >= Kw; f(Kw - 1) >= Kw, f(i) <= i + 1 + nb
-    int lo = max(0, Kw - 1 - nb), hi = Kw - 1;
-    int i = max(lo, Kw - 1 - count_le(list[Kw - 1]));
-    // (group-uniform loop; groups that finished keep lo == hi)
-    // (the exchanges stay inside the group, whose lanes agree on lo < hi)
-    while (__ballot(lo < hi) != 0ull) {
-        if (lo < hi) {
-            if (i + 1 + count_le(list[i]) >= Kw) hi = i;
-            else lo = i + 1;
-            i = (lo + hi) >> 1;
-        }
-    }
-    const unsigned tg = widen_bound(list[hi] | kIdBits, S);
-    // kept part of A: entries <= tg (>= hi + 1 of them)
-    int ka = hi + 1;
-    {
-        int a = ka, z = mv;
-        while (a < z) {
-            const int m = (a + z) >> 1;
-            if (list[m] <= tg) a = m + 1; else z = m;
-        }
-        ka = a;
-    }
-    unsigned c = 0u;
-#pragma unroll
-    for (int s = 0; s < PER; ++s) c += b[s] <= tg ? 1u : 0u;
-    unsigned kb;
-    unsigned off = (unsigned)ka + gscan8(c, l, kb);
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int s = 0; s < PER; ++s) {
-        if (b[s] <= tg) list[off++] = b[s];
-    }
-    __builtin_amdgcn_wave_barrier();
-    return make_uint3(tg, (unsigned)ka + kb, (unsigned)ka);
 }
 
 // the f64 point of tree slot i from its (x, y, z, 0) record: one 16-B and one 8-B load of
@@ -686,24 +599,17 @@ __global__ __launch_bounds__(64 * kW) __attribute__((amdgpu_waves_per_eu(kCap <=
 #pragma unroll
         for (int j = 0; j < kQ; ++j) nmax = max(nmax, nbq[j]);
         __builtin_amdgcn_wave_barrier();
-        int dmax = 0, mmin = INT_MAX;
+        int dmax = 0;
         bool anyz = false;
 #pragma unroll
         for (int j = 0; j < kQ; ++j) {
             const int mj = __builtin_amdgcn_readlane(mvv, 8 * j);
             dmax = max(dmax, (int)nbq[j] - mj);
             anyz |= mj == 0;
-            mmin = min(mmin, mj);
         }
-        uint3 r3;
-        if ((int)(mmin >= Kw) & (int)(dmax <= 8 * kPrefixPer)) {
-            // every list has a sorted prefix of >= Kw entries and a short tail: no sort
-            r3 = tighten_group_prefix<kPrefixPer>(lists, g, l, (int)group_len(), mvv, Kw, s_norm);
-        } else {
-            const bool presort = anyz || dmax > 128;
-            const int tail_per = presort ? (nmax <= 128 ? 0 : (nmax <= 192 ? 8 : 16)) : (dmax == 0 ? 0 : dmax <= 64 ? 8 : 16);
-            r3 = tighten_group_sorted(lists, g, l, (int)group_len(), mvv, (int)nmax, Kw, presort, tail_per, s_norm);
-        }
+        const bool presort = anyz || dmax > 128;
+        const int tail_per = presort ? (nmax <= 128 ? 0 : (nmax <= 192 ? 8 : 16)) : (dmax == 0 ? 0 : dmax <= 64 ? 8 : 16);
+        const uint3 r3 = tighten_group_sorted(lists, g, l, (int)group_len(), mvv, (int)nmax, Kw, presort, tail_per, s_norm);
         mvv = (int)r3.z;
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
