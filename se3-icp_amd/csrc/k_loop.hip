@@ -666,7 +666,9 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce(View v) {
 #ifdef SE3ICP_PROF
 // k_reduce_final phases summed over launches and pairs (100 MHz ticks): [0] the block
 // partials' sums, [1] the one-lane close / open of the iteration, [2] pair blocks
-__device__ unsigned long long g_fin_prof[4];
+// (one slot per phase: [3] state load, [4] close, [5] open + stores; round 5 packed the
+// three into 21-bit fields of one word, which overflowed over a large batch -- ADVICE r05)
+__device__ unsigned long long g_fin_prof[6];
 #endif
 constexpr int kFinThreads = 512;                    // (the solve's ~220 VGPRs allow two waves per SIMD)
 constexpr int kFinChunks = kFinThreads / kRedVals;  // 18 interleaved chunks of block partials
@@ -747,7 +749,9 @@ __global__ __launch_bounds__(kFinThreads) void k_reduce_final(View v, const int3
         atomicAdd(&g_fin_prof[0], tf1 - tf0);
         atomicAdd(&g_fin_prof[1], tf2 - tf1);
         atomicAdd(&g_fin_prof[2], 1ull);
-        atomicAdd(&g_fin_prof[3], ((tfa - tf1) << 42) | ((tfb - tfa) << 21) | (tf2 - tfb));
+        atomicAdd(&g_fin_prof[3], tfa - tf1);
+        atomicAdd(&g_fin_prof[4], tfb - tfa);
+        atomicAdd(&g_fin_prof[5], tf2 - tfb);
 #endif
     }
 }
@@ -764,13 +768,14 @@ void trim_prof_report() {
                  h[6] ? h[3] / 100.0 / h[6] : 0.0, h[6] ? h[4] / 100.0 / h[6] : 0.0);
     const unsigned long long z[8] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_trim_prof), z, sizeof(z));
-    unsigned long long f[4];
+    unsigned long long f[6];
     if (hipMemcpyFromSymbol(f, HIP_SYMBOL(g_fin_prof), sizeof(f)) == hipSuccess && f[2]) {
         std::fprintf(stderr, "[prof] k_reduce_final per pair block (us): partial sums %.2f, close/open %.2f (state load %.2f, "
                      "close %.2f, open + stores %.2f) (%llu)\n",
-                     f[0] / 100.0 / f[2], f[1] / 100.0 / f[2], (double)(f[3] >> 42) / 100.0 / f[2],
-                     (double)((f[3] >> 21) & 0x1fffff) / 100.0 / f[2], (double)(f[3] & 0x1fffff) / 100.0 / f[2], f[2]);
-        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_fin_prof), z, sizeof(f));
+                     f[0] / 100.0 / f[2], f[1] / 100.0 / f[2], f[3] / 100.0 / f[2], f[4] / 100.0 / f[2],
+                     f[5] / 100.0 / f[2], f[2]);
+        const unsigned long long z6[6] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_fin_prof), z6, sizeof(f));
     }
 #endif
 }

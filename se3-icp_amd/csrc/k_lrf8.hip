@@ -43,7 +43,10 @@ namespace {
 
 using namespace knn;
 
-constexpr int kW = 4;     // waves per block
+#ifndef SE3ICP_LRF8_WAVES
+#define SE3ICP_LRF8_WAVES 4
+#endif
+constexpr int kW = SE3ICP_LRF8_WAVES;  // waves per block
 constexpr int kQ = 8;     // queries per wave (eight lanes each in the group phases)
 #ifndef SE3ICP_LRF8_CAP
 #define SE3ICP_LRF8_CAP 192

@@ -604,7 +604,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
         if ((int)dense & (int)(total > 0) & (int)(lane <= grp) & ((int)(phase == PHASE_SE3) | ((int)order3(v.npairs) & (int)(phase == PHASE_R3)))) {
             const int g = c * NL + lane;
             const int ph = phase == PHASE_SE3 ? 0 : 1;
-            const int row = (ph * 8 + group_xcd(g, v.nchunks * NL)) * 16 + cost_class(v.gcost[g]);
+            const int row = (ph * 8 + group_xcd(g, v.nchunks * NL)) * 16 + cost_class(v.gcost[(size_t)ph * v.nchunks * NL + g]);
             const int at = atomicAdd(&v.cls[row], 1);
             v.cls[kClsHead + (size_t)row * cls_cap(v.nchunks) + at] = g;
         }
@@ -1021,6 +1021,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
     if constexpr (ORD) {
         const int bb = (int)blockIdx.x - kSingleWaves, x = bb & 7, i = bb >> 3;
         const int row0 = ((D == 12 ? 0 : 1) * 8 + x) * 16;
+        // the phase's own group durations (an R3 search is never ordered by the SE(3) waves'
+        // times of unrelated groups)
+        const size_t gcost_row = (size_t)(D == 12 ? 0 : 1) * v.nchunks * 16;
         int acc = 0, k = -1, lo = 0;
         for (int j = 0; j < 16; ++j) {
             const int cj = __builtin_amdgcn_readfirstlane(v.cls[row0 + j]);
@@ -1035,7 +1038,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
             group(gs);
             const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-            if ((int)(lane == 0) & (int)((gs >> 4) < v.nchunks)) v.gcost[gs] = (unsigned)min(t1 - t0, 0xffffffffull) | 1u;
+            if ((int)(lane == 0) & (int)((gs >> 4) < v.nchunks)) v.gcost[gcost_row + gs] = (unsigned)min(t1 - t0, 0xffffffffull) | 1u;
             return;
         }
         if (k < 0) return;
@@ -1043,7 +1046,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         group(gq);
         const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-        if (lane == 0) v.gcost[gq] = (unsigned)min(t1 - t0, 0xffffffffull) | 1u;
+        if (lane == 0) v.gcost[gcost_row + gq] = (unsigned)min(t1 - t0, 0xffffffffull) | 1u;
         return;
     }
     const int gq = __builtin_amdgcn_readfirstlane(

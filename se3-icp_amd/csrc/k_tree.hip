@@ -918,6 +918,25 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
                 }
 #endif
                 for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+#if SE3ICP_TREE_LDS_SAMPLE
+                if (cnt == 0) {
+                    // (wave-uniform) a sub-node holding none of the fixed sample points -- deep
+                    // levels, small nodes: its own points from the columns, every one of them
+                    // (round 5 split such a sub-node on dimension 0 with mean = sd = 0, i.e. by
+                    // index)
+                    for (int e = a0 + lane; e < a1; e += 64) {
+                        const int p = s_val[e];
+                        ++cnt;
+#pragma unroll
+                        for (int d = 0; d < D; ++d) {
+                            const float x = col0[d * m + p];
+                            s1[d] += x;
+                            s2[d] = fmaf(x, x, s2[d]);
+                        }
+                    }
+                    for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+                }
+#endif
                 const float inv = cnt > 0 ? 1.f / (float)cnt : 0.f;
                 int best = 0;
                 float ext = -1.f;
