@@ -509,12 +509,12 @@ int Engine::setup_chunks(int npairs, hipStream_t s) {
     chunk_level_ = std::max(0, tree_L_ - 4);
     nchunks_ = npairs << chunk_level_;
     if (!ensure<int32_t>(d_qlist_, (size_t)nchunks_ * kChunkQ) || !ensure<int32_t>(d_qcount_, (size_t)nchunks_ * (kChunkQ / 64)) ||
-        !ensure<double>(d_hist_, (size_t)kHist * npairs * 12) || !ensure<uint32_t>(d_gcost_, (size_t)2 * nchunks_ * 16) ||
+        !ensure<double>(d_hist_, (size_t)kHist * npairs * 12) || !ensure<uint32_t>(d_gcost_, (size_t)nchunks_ * 16) ||
         !ensure<int32_t>(d_cls_, nn_cls_words(nchunks_)))
         return SE3ICP_ERR_OUT_OF_MEMORY;
     if (pinned(h_hist_, h_hist_cap_, (size_t)npairs * 12)) return SE3ICP_ERR_OUT_OF_MEMORY;
     HIPCHK(hipMemsetAsync(d_cert_.p, 0xff, sizeof(NNCert) * ld_, s));  // iteration -1: no certificate
-    HIPCHK(hipMemsetAsync(d_gcost_.p, 0, sizeof(uint32_t) * 2 * nchunks_ * 16, s));
+    HIPCHK(hipMemsetAsync(d_gcost_.p, 0, sizeof(uint32_t) * nchunks_ * 16, s));
     HIPCHK(hipMemsetAsync(d_cls_.p, 0, sizeof(int32_t) * 2 * 8 * 16, s));
     return 0;
 }

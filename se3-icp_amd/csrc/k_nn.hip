@@ -604,7 +604,12 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
         if ((int)dense & (int)(total > 0) & (int)(lane <= grp) & ((int)(phase == PHASE_SE3) | ((int)order3(v.npairs) & (int)(phase == PHASE_R3)))) {
             const int g = c * NL + lane;
             const int ph = phase == PHASE_SE3 ? 0 : 1;
-            const int row = (ph * 8 + group_xcd(g, v.nchunks * NL)) * 16 + cost_class(v.gcost[(size_t)ph * v.nchunks * NL + g]);
+            // the group's last wave time: one row for both phases, so a pair's first R3
+            // searches are ordered by its groups' SE(3) times (the same source queries against
+            // the same target cloud) until its R3 waves have written their own.  Round 6
+            // measured separate rows per phase: SE(3) NN 18.40 -> 19.02 ms per
+            // step at C4 64 pairs, same box -- the shared row stays, deliberately
+            const int row = (ph * 8 + group_xcd(g, v.nchunks * NL)) * 16 + cost_class(v.gcost[g]);
             const int at = atomicAdd(&v.cls[row], 1);
             v.cls[kClsHead + (size_t)row * cls_cap(v.nchunks) + at] = g;
         }
@@ -1021,16 +1026,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
     if constexpr (ORD) {
         const int bb = (int)blockIdx.x - kSingleWaves, x = bb & 7, i = bb >> 3;
         const int row0 = ((D == 12 ? 0 : 1) * 8 + x) * 16;
-        // the phase's own group durations (an R3 search is never ordered by the SE(3) waves'
-        // times of unrelated groups)
-        const size_t gcost_row = (size_t)(D == 12 ? 0 : 1) * v.nchunks * 16;
         int acc = 0, k = -1, lo = 0;
         for (int j = 0; j < 16; ++j) {
             const int cj = __builtin_amdgcn_readfirstlane(v.cls[row0 + j]);
             if ((int)(k < 0) & (int)(i < acc + cj)) { k = j; lo = acc; }
             acc += cj;
         }
-        // (no group of this XCD timed yet -- a phase's first search: the run order, whose
+        // (no group of this XCD timed yet -- the SE(3) phase's first search; an R3 phase starts
+        // with the SE(3) times, see k_nn_prep: the run order, whose
         // neighbouring chunks share target leaves in the XCD's L2)
         const int known = acc - __builtin_amdgcn_readfirstlane(v.cls[row0]);
         if (known == 0) {
@@ -1038,7 +1041,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
             const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
             group(gs);
             const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-            if ((int)(lane == 0) & (int)((gs >> 4) < v.nchunks)) v.gcost[gcost_row + gs] = (unsigned)min(t1 - t0, 0xffffffffull) | 1u;
+            if ((int)(lane == 0) & (int)((gs >> 4) < v.nchunks)) v.gcost[gs] = (unsigned)min(t1 - t0, 0xffffffffull) | 1u;
             return;
         }
         if (k < 0) return;
@@ -1046,7 +1049,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         group(gq);
         const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-        if (lane == 0) v.gcost[gcost_row + gq] = (unsigned)min(t1 - t0, 0xffffffffull) | 1u;
+        if (lane == 0) v.gcost[gq] = (unsigned)min(t1 - t0, 0xffffffffull) | 1u;
         return;
     }
     const int gq = __builtin_amdgcn_readfirstlane(

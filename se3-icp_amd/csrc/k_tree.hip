@@ -770,6 +770,9 @@ __global__ __launch_bounds__(kLevThreads) void k_tree_level(TreeView t, int leve
 #ifndef SE3ICP_TREE_LDS_SAMPLE
 #define SE3ICP_TREE_LDS_SAMPLE 1
 #endif
+#ifndef SE3ICP_TREE_EMPTY_FALLBACK
+#define SE3ICP_TREE_EMPTY_FALLBACK 1
+#endif
 constexpr int kLocalMax = 4096;  // power of two
 constexpr int kWaveSortPer = 8;  // sub-nodes of <= 512 points: register sort by one wave
 constexpr int kLocalThreads = 512;
@@ -918,7 +921,7 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
                 }
 #endif
                 for (int o = 32; o >= 1; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
-#if SE3ICP_TREE_LDS_SAMPLE
+#if SE3ICP_TREE_LDS_SAMPLE && SE3ICP_TREE_EMPTY_FALLBACK
                 if (cnt == 0) {
                     // (wave-uniform) a sub-node holding none of the fixed sample points -- deep
                     // levels, small nodes: its own points from the columns, every one of them

@@ -106,7 +106,7 @@ struct View {
     // the PHASE's source tree (12-D in the SE(3) phase, 3-D in the R3 phase: a certificate of
     // the other phase is void anyway), so k_nn_prep reads them in tree order, coalesced
     NNCert* cert;
-    uint32_t* gcost;      // [2][nchunks * 16] duration of each group's last search wave per phase (SE(3), R3; 100 MHz ticks; 0: none)
+    uint32_t* gcost;      // [nchunks * 16] duration of each group's last search wave, either phase (100 MHz ticks; 0: none)
     int32_t* cls;         // cost-ordered dispatch: [2 phases][8 XCDs][16 classes] counts, then the lists
 };
 
