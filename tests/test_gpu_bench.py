@@ -44,3 +44,23 @@ def test_two_rank_bench_equals_one_rank(tmp_path):
     a, b = np.load(one), np.load(two)
     assert a.shape == b.shape == (7, 4, 4)
     assert np.array_equal(a, b)
+
+
+@pytest.mark.timeout(900)
+def test_two_rank_balanced_shards_equal_one_rank(tmp_path):
+    """--shard balanced: the 7 pairs assigned by point count (not in contiguous blocks); the
+    gathered poses come back in batch order, bitwise those of one rank."""
+    common = ["--steps", "1", "--warmup", "0", "--workload", "C3", "--cpu-baseline", "off", "--global-batch", "7"]
+    one, two = tmp_path / "one.npy", tmp_path / "two.npy"
+    r1 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dump-poses", str(one)] + common,
+                        capture_output=True, text=True, timeout=300)
+    assert r1.returncode == 0, r1.stderr[-3000:]
+    r2 = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                         "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+                         "--gpus", "2", "--backend", "gloo", "--shard", "balanced", "--dump-poses", str(two)] + common,
+                        capture_output=True, text=True, timeout=300)
+    assert r2.returncode == 0, r2.stderr[-3000:]
+    import json
+    d = json.loads([l for l in r2.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["n_gpus"] == 2 and d["config"]["shard"] == "balanced"
+    assert np.array_equal(np.load(one), np.load(two))
