@@ -64,3 +64,39 @@ def test_two_rank_balanced_shards_equal_one_rank(tmp_path):
     d = json.loads([l for l in r2.stdout.splitlines() if l.startswith("{")][-1])
     assert d["n_gpus"] == 2 and d["config"]["shard"] == "balanced"
     assert np.array_equal(np.load(one), np.load(two))
+
+
+def _rccl_rank(out_path, port):
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, os.path.join(ROOT, "se3-icp_amd"))
+    from se3icp import sharding
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", device_id=dev)
+    assert dist.get_backend() == "nccl"
+    rows = np.zeros((3, sharding.REC))
+    rows[:, :16] = np.eye(4).reshape(16)
+    rows[:, 16] = [5, 6, 7]
+    res = sharding.exchange_results(dist, dev, 1.25, 0.5, 18, rows, pair_ids=[2, 0, 1])
+    dist.destroy_process_group()
+    np.savez(out_path, elapsed=res[0], iters=res[2], it=res[3].num_iterations)
+
+
+@pytest.mark.timeout(600)
+def test_result_exchange_runs_on_rccl(tmp_path):
+    """The bench's end-of-batch exchange (all-reduce of the times and iterations, all-gather
+    of the records) over torch.distributed's "nccl" backend -- RCCL on ROCm -- in a one-rank
+    process group on the box's GPU (the 8-GPU job is the driver's); the records come back in
+    pair order."""
+    import multiprocessing as mp
+    out = tmp_path / "rccl.npz"
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_rccl_rank, args=(str(out), _port()))
+    p.start()
+    p.join(300)
+    assert p.exitcode == 0
+    d = np.load(out)
+    assert float(d["elapsed"]) == 1.25 and int(d["iters"]) == 18
+    assert list(d["it"]) == [6, 7, 5]
