@@ -503,6 +503,11 @@ __device__ unsigned long long g_prep_span[2] = {~0ull, 0ull};
 // the launch span (earliest wave start, latest wave end)
 __device__ unsigned long long g_wave_hist[2][41];
 __device__ unsigned long long g_wave_span[2] = {~0ull, 0ull};
+// SE(3) group waves per hardware XCD (HW_REG_XCC_ID): summed wave time, latest wave end, waves
+__device__ unsigned long long g_xcd_prof[8][3];
+// SE(3) ordered group blocks per hardware XCD: summed lifetime (kernel entry to exit) of the
+// blocks that ran a group, of the empty ones, and the empty ones' count
+__device__ unsigned long long g_xcd_life[8][3];
 // 3-D search waves per launch: [0] group waves, [1] single-query-list waves: count, summed
 // ticks, longest wave (ticks), queries
 __device__ unsigned long long g_r3_prof[2][4];
@@ -999,6 +1004,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
                 atomicAdd(&g_wave_hist[1][hb], dt);
                 atomicMin(&g_wave_span[0], t_w0);
                 atomicMax(&g_wave_span[1], t_w0 + dt);
+                {
+                    const int xcc = (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u);  // HW_REG_XCC_ID
+                    atomicAdd(&g_xcd_prof[xcc][0], dt);
+                    atomicMax(&g_xcd_prof[xcc][1], t_w0 + dt);
+                    atomicAdd(&g_xcd_prof[xcc][2], 1ull);
+                }
                 atomicAdd(v.stats + kStatCols * (gi & 63) + 12, c_leaf);   // shader cycles in leaf visits,
                 atomicAdd(v.stats + kStatCols * (gi & 63) + 14, c_lload);  // in their target loads,
                 atomicAdd(v.stats + kStatCols * (gi & 63) + 13, __builtin_amdgcn_s_memtime() - c_w0);  // in the wave
@@ -1024,6 +1035,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
         }
     };
     if constexpr (ORD) {
+#ifdef SE3ICP_PROF
+        const unsigned long long t_entry = __builtin_amdgcn_s_memrealtime();
+        auto life = [&](int slot) {
+            if ((int)(D == 12) & (int)(lane == 0)) {
+                const int xcc = (int)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u);
+                atomicAdd(&g_xcd_life[xcc][slot], __builtin_amdgcn_s_memrealtime() - t_entry);
+                if (slot == 1) atomicAdd(&g_xcd_life[xcc][2], 1ull);
+            }
+        };
+#else
+        auto life = [](int) {};
+#endif
         const int bb = (int)blockIdx.x - kSingleWaves, x = bb & 7, i = bb >> 3;
         const int row0 = ((D == 12 ? 0 : 1) * 8 + x) * 16;
         int acc = 0, k = -1, lo = 0;
@@ -1042,14 +1065,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(D == 12 ? kW
             group(gs);
             const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
             if ((int)(lane == 0) & (int)((gs >> 4) < v.nchunks)) v.gcost[gs] = (unsigned)min(t1 - t0, 0xffffffffull) | 1u;
+            life(0);
             return;
         }
-        if (k < 0) return;
+        if (k < 0) {
+            life(1);
+            return;
+        }
         const int gq = __builtin_amdgcn_readfirstlane(v.cls[kClsHead + (size_t)(row0 + k) * cls_cap(v.nchunks) + (i - lo)]);
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
         group(gq);
         const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
         if (lane == 0) v.gcost[gq] = (unsigned)min(t1 - t0, 0xffffffffull) | 1u;
+        life(0);
         return;
     }
     const int gq = __builtin_amdgcn_readfirstlane(
@@ -1285,6 +1313,24 @@ void nn_wave_report(int it) {
     for (int b = 0; b < 41; ++b)
         if (h[0][b]) std::fprintf(stderr, " %d:%llu/%.1f%%", 25 * b, h[0][b], 100.0 * (double)h[1][b] / std::max(tot, 1.0));
     std::fprintf(stderr, "\n");
+    unsigned long long xp[8][3];
+    if (hipMemcpyFromSymbol(xp, HIP_SYMBOL(g_xcd_prof), sizeof(xp)) == hipSuccess && sp[1] > sp[0]) {
+        std::fprintf(stderr, "[nn] iter %d: per XCD summed wave time / 512 slots, last wave end after the first start, waves (us):", it);
+        for (int x = 0; x < 8; ++x)
+            std::fprintf(stderr, " %d:%.1f/%.1f/%llu", x, xp[x][0] / 100.0 / 512.0,
+                         xp[x][1] > sp[0] ? (xp[x][1] - sp[0]) / 100.0 : 0.0, xp[x][2]);
+        std::fprintf(stderr, "\n");
+        const unsigned long long zx[8][3] = {};
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_xcd_prof), zx, sizeof(zx));
+        unsigned long long xl[8][3];
+        if (hipMemcpyFromSymbol(xl, HIP_SYMBOL(g_xcd_life), sizeof(xl)) == hipSuccess) {
+            std::fprintf(stderr, "[nn] iter %d: per XCD block lifetimes / 512 slots: working, empty (count) (us):", it);
+            for (int x = 0; x < 8; ++x)
+                std::fprintf(stderr, " %d:%.1f,%.1f(%llu)", x, xl[x][0] / 100.0 / 512.0, xl[x][1] / 100.0 / 512.0, xl[x][2]);
+            std::fprintf(stderr, "\n");
+            (void)hipMemcpyToSymbol(HIP_SYMBOL(g_xcd_life), zx, sizeof(zx));
+        }
+    }
     unsigned long long r3[2][4];
     if (hipMemcpyFromSymbol(r3, HIP_SYMBOL(g_r3_prof), sizeof(r3)) == hipSuccess && (r3[0][0] | r3[1][0])) {
         std::fprintf(stderr, "[nn] iter %d: R3 group waves %llu (%llu queries), mean %.1f us, longest %.1f us; single-list waves "
