@@ -530,6 +530,28 @@ def test_batch_independence_across_schedules(se3icp_mod, case):
             assert (f.num_iterations, f.num_pure_se3_iterations) == (h.num_iterations, h.num_pure_se3_iterations)
 
 
+def test_c4_headline_batch_pairs_match_oracle(se3icp_mod, refcpu, parity_record):
+    """The headline batch itself (BASELINE.json configs[1]: 64 KITTI-like pairs of ~120k
+    points, se3_gicp, one call) checked pair by pair against the oracle, at four pairs spread
+    over the batch (the first, the last and two inside), not only through the sub-batch
+    property above.  The oracle runs on the host's cores (threads: its default)."""
+    from se3icp import datasets
+    pairs, _ = datasets.kitti_like_pairs(64, seed=4)
+    p = se3icp_mod.kitti_params()
+    got = se3icp_mod.register_batch(pairs, "se3_gicp", p)
+    rp = refcpu.default_params(estimated_overlap=0.7, max_num_se3_iterations=10, mse=1e-7, mse_switch_error=5e-7,
+                               number_of_nn_for_LRF=90)
+    worst = 0.0
+    for i in (0, 21, 42, 63):
+        ref = refcpu.register(pairs[i][0], pairs[i][1], refcpu.RUN_SE3_ICP, "gicp", rp)
+        d = float(np.linalg.norm(got[i].T - ref["T"]))
+        worst = max(worst, d)
+        assert d <= 1e-5, (i, d)
+        assert got[i].num_iterations == ref["num_iterations"], i
+        assert got[i].num_pure_se3_iterations == ref["num_pure_se3_iterations"], i
+    parity_record("C4 64-pair headline batch, pairs 0/21/42/63 vs oracle", max_pose_frobenius=worst)
+
+
 def test_profiled_and_event_modes_equal_the_plain_loop(se3icp_mod):
     """Per-stage HIP events (se3icp_set_profiling) and the SE(3) NN bracket
     (se3icp_set_nn_events) change only how the host follows the loop, never its results:
