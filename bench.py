@@ -187,6 +187,8 @@ def main():
     ap.add_argument("--shard", choices=["contiguous", "balanced"], default="contiguous",
                     help="pairs per rank: contiguous blocks of the batch, or a cost-balanced assignment (greedy by "
                          "point count over the whole batch, sharding.shard_balanced)")
+    ap.add_argument("--in-flight", type=int, default=2,
+                    help="calls in flight per GPU (engine slots, one host thread each); 1: one call at a time")
     ap.add_argument("--secondary", choices=["auto", "off"], default="auto",
                     help="C4 at N=1: also time one 8-pair shard on this GPU (the per-GPU work of the 8-GPU job)")
     args = ap.parse_args()
@@ -274,39 +276,63 @@ def main():
                                             params, device=devi)
 
     # the timed steps: one C-ABI call each with prebuilt arguments; every step's results and
-    # kernel times land in their own buffers and are read after the timed region
-    runner = se3icp.DeviceBatchRunner(d_src.data_ptr(), src_off, d_tgt.data_ptr(), tgt_off, W["method"], params,
-                                      device=devi, slots=max(1, args.steps))
+    # kernel times land in their own buffers and are read after the timed region.  With
+    # --in-flight F > 1 the K steps run F at a time on F engine slots of this GPU (own
+    # streams and buffers, one host thread each: PipelinedBatchRunner) -- the value; then the
+    # same K steps one call at a time (single_call), whose isolated kernel and phase times
+    # feed the per-kernel lines and rooflines below.
+    def make_runner(slot):
+        return se3icp.DeviceBatchRunner(d_src.data_ptr(), src_off, d_tgt.data_ptr(), tgt_off, W["method"], params,
+                                        device=devi | (slot << 8), slots=max(1, args.steps))
+    pipe = se3icp.PipelinedBatchRunner(make_runner, in_flight=args.in_flight, steps=args.steps)
     for w in range(args.warmup):
         tw = time.time()
         step()
         log(f"rank {rank}: warmup {w} {time.time() - tw:.2f}s")
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for s in range(args.steps):
-        runner.run(s)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
+    if args.in_flight > 1:
+        pipe.warm()  # (every slot's buffers and code, untimed)
+
+    def timed(run):
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        return time.perf_counter() - t0
+
+    elapsed = timed(pipe.run_steps)
     iters = 0
+    last = None
+    for s in range(args.steps):
+        res = pipe.results(s)
+        iters += sum(r.num_iterations for r in res)
+        last = res
+        log(f"rank {rank}: step {s} done ({sum(r.num_iterations for r in res)} iterations, slot {pipe.owner(s)})")
+    single = None
+    iso = pipe
+    if args.in_flight > 1:
+        iso = se3icp.PipelinedBatchRunner(make_runner, in_flight=1, steps=args.steps)
+        el1 = timed(iso.run_steps)
+        its1 = sum(sum(r.num_iterations for r in iso.results(s)) for s in range(args.steps))
+        el1 = sharding.max_over_ranks(dist, xdev, el1)
+        its1 = sharding.sum_over_ranks(dist, xdev, its1)
+        single = {"value": round(its1 / el1, 3), "ms_per_step": round(1000.0 * el1 / args.steps, 3),
+                  "note": "the same K steps one call at a time (one batch in flight): the per-call rate; the "
+                          "kernel, phase and roofline figures of this line come from these isolated calls"}
     rechecked = 0
     setup_ms = 0.0
     loop_ms = 0.0
     ktot: dict = {}
-    last = None
     for s in range(args.steps):
-        res = runner.results(s)
-        for k, v in runner.kernel_times(s).items():
+        res = iso.results(s)
+        for k, v in iso.kernel_times(s).items():
             ktot[k] = ktot.get(k, 0.0) + v
-        iters += sum(r.num_iterations for r in res)
         rechecked += sum(r.num_rechecked for r in res)
         loop_ms += res[0].time_loop_ms
         setup_ms += res[0].time_setup_ms
-        last = res
-        log(f"rank {rank}: step {s} done ({sum(r.num_iterations for r in res)} iterations)")
     # one untimed step with HIP events around every loop stage: the timed steps carry
     # events only around the SE(3) NN grids (each marker costs the stream a few microseconds)
     se3icp.set_profiling(True, devi)
@@ -373,7 +399,10 @@ def main():
                 "points_per_cloud_mean": int(np.mean(npts)),
                 "parallelism": f"pair-sharded dp{world} ({'RCCL' if args.backend == 'nccl' else 'gloo'} "
                                f"result gather only)",
+                "in_flight": args.in_flight,
             },
+            "in_flight": args.in_flight,
+            "single_call": single,
             "pairs_per_sec": round(total_pairs / elapsed, 4),
             "loop_iterations_per_sec": round(iters_all / loop_s, 3) if loop_s > 0 else None,
             "iterations_per_pair_mean": round(iters_all / total_pairs, 2),
@@ -391,7 +420,7 @@ def main():
             "cpu_baseline": None,
         }
         if args.workload == "C4" and world == 1 and args.secondary == "auto" and len(pairs) > 8:
-            out["secondary_8_pair_shard_one_gpu"] = bench_shard8(pairs, W, params, dev, devi)
+            out["secondary_8_pair_shard_one_gpu"] = bench_shard8(pairs, W, params, dev, devi, in_flight=args.in_flight)
         if args.cpu_baseline == "auto":
             # rank 0's own pairs on the node's host (the same host for every rank), after the
             # timed region; at N > 1 the whole job's value is compared with it
@@ -577,10 +606,11 @@ def reduce_roofline(res, pairs, W, red_ms, wl):
                     "(k_reduce_final); traffic = both kernels' PMC bytes per launch from this workload's pass"}
 
 
-def bench_shard8(pairs, W, params, dev, devi, steps=3):
+def bench_shard8(pairs, W, params, dev, devi, steps=3, in_flight=1):
     """One 8-pair shard of the C4 batch (its first 8 pairs) on this GPU, timed like the
     main steps: the per-GPU work of the 8-GPU strong-scaling job, so the 1-GPU line shows
-    what the per-iteration chain costs at that batch size (a weak-scaling anchor)."""
+    what the per-iteration chain costs at that batch size (a weak-scaling anchor); with
+    in_flight > 1 also as the main steps run, that many calls at a time."""
     import torch
     import se3icp
     sub = pairs[:8]
@@ -601,9 +631,25 @@ def bench_shard8(pairs, W, params, dev, devi, steps=3):
     torch.cuda.synchronize()
     el = time.perf_counter() - t
     its = sum(sum(r.num_iterations for r in runner.results(k)) for k in range(steps))
-    return {"pairs": len(sub), "steps": steps, "ms_per_step": round(1000.0 * el / steps, 3),
-            "value": round(its / el, 3), "unit": "ICP iterations/s", "pairs_per_sec": round(len(sub) * steps / el, 4),
-            "note": "pairs 0-7 of the batch as one call on one GPU: what each GPU registers in the 8-GPU job"}
+    out = {"pairs": len(sub), "steps": steps, "ms_per_step": round(1000.0 * el / steps, 3),
+           "value": round(its / el, 3), "unit": "ICP iterations/s", "pairs_per_sec": round(len(sub) * steps / el, 4),
+           "note": "pairs 0-7 of the batch as one call on one GPU: what each GPU registers in the 8-GPU job"}
+    if in_flight > 1:
+        # the 8-GPU job's per-GPU steps as the main steps run them: in_flight calls at a time
+        ks = 4 * steps
+        pipe = se3icp.PipelinedBatchRunner(
+            lambda slot: se3icp.DeviceBatchRunner(d_src.data_ptr(), so, d_tgt.data_ptr(), to, W["method"], params,
+                                                  device=devi | (slot << 8), slots=ks), in_flight=in_flight, steps=ks)
+        pipe.warm()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        pipe.run_steps()
+        torch.cuda.synchronize()
+        el2 = time.perf_counter() - t
+        its2 = sum(sum(r.num_iterations for r in pipe.results(k)) for k in range(ks))
+        out["in_flight"] = {"calls_in_flight": in_flight, "steps": ks, "ms_per_step": round(1000.0 * el2 / ks, 3),
+                            "value": round(its2 / el2, 3)}
+    return out
 
 
 def host_info():

@@ -275,6 +275,77 @@ class DeviceBatchRunner:
         return dict(zip(self._KT_KEYS, list(self._kt[slot])))
 
 
+class PipelinedBatchRunner:
+    """Consecutive batches with ``in_flight`` of them on the GPU at once: one engine slot per
+    in-flight call (``device | slot << 8``: own stream and buffers) and a
+    host thread per slot taking the next step index until ``steps`` calls are done (ctypes
+    releases the GIL during the C-ABI call).  A call is latency-bound over much of its loop
+    (small per-iteration grids, host-visible phase switches) while its setup is not, so a
+    second call in flight fills what the first leaves idle.  Every call registers the same
+    clouds and returns bitwise the results of a lone call (per-slot engines share nothing).
+
+    runner_factory(slot) -> an object with run(i), results(i), kernel_times(i) over ``steps``
+    result buffers (DeviceBatchRunner; tests pass stand-ins)."""
+
+    def __init__(self, runner_factory, in_flight: int = 2, steps: int = 1):
+        import threading
+
+        self._lock = threading.Lock()
+        self.in_flight = max(1, int(in_flight))
+        self.steps = max(1, int(steps))
+        self._runners = [runner_factory(k) for k in range(self.in_flight)]
+        self._owner = [-1] * self.steps
+
+    def warm(self) -> None:
+        """One untimed call per slot (its buffers and code), into result buffer 0."""
+        for r in self._runners:
+            r.run(0)
+
+    def run_steps(self, steps: int | None = None) -> None:
+        n = self.steps if steps is None else min(int(steps), self.steps)
+        nxt = [0]
+        err: list[BaseException] = []
+
+        def worker(k: int) -> None:
+            while True:
+                with self._lock:
+                    s = nxt[0]
+                    if s >= n or err:
+                        return
+                    nxt[0] = s + 1
+                    self._owner[s] = k
+                try:
+                    self._runners[k].run(s)
+                except BaseException as e:  # noqa: BLE001 (re-raised by the caller's thread)
+                    with self._lock:
+                        err.append(e)
+                    return
+
+        if self.in_flight == 1:
+            for s in range(n):
+                self._owner[s] = 0
+                self._runners[0].run(s)
+            return
+        import threading
+
+        th = [threading.Thread(target=worker, args=(k,)) for k in range(self.in_flight)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if err:
+            raise err[0]
+
+    def owner(self, s: int) -> int:
+        return self._owner[s]
+
+    def results(self, s: int) -> list[PairResult]:
+        return self._runners[self._owner[s]].results(s)
+
+    def kernel_times(self, s: int) -> dict:
+        return self._runners[self._owner[s]].kernel_times(s)
+
+
 def register_batch_traced(pairs, method: str, params: _lib.Params | None = None, pair: int = 0,
                           max_iters: int = 160, device: int = 0):
     """register_batch with the per-iteration record of one pair (se3icp_set_trace): the

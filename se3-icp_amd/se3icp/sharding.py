@@ -137,3 +137,25 @@ def exchange_results(dist, device, elapsed_s: float, loop_s: float, iterations: 
     if pair_ids is not None:
         allr = allr[np.argsort(allr[:, REC], kind="stable"), :REC]
     return float(t_max[0]), float(t_max[1]), int(round(float(tot[0]))), unpack_records(allr)
+
+
+def max_over_ranks(dist, device, x: float) -> float:
+    """The largest of every rank's x (one timed region's seconds); x itself for one rank."""
+    if dist is None:
+        return float(x)
+    import torch
+
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0])
+
+
+def sum_over_ranks(dist, device, x: float) -> float:
+    """The sum of every rank's x (work counts); x itself for one rank."""
+    if dist is None:
+        return float(x)
+    import torch
+
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t[0])

@@ -604,6 +604,37 @@ def test_device_batch_runner_equals_register_batch(se3icp_mod):
         assert kt["lrf_queries"] > 0 and kt["nn_se3_launches"] > 0
 
 
+def test_pipelined_runner_equals_register_batch(se3icp_mod):
+    """bench.py's in-flight steps: two calls at a time on two engine slots of the GPU (own
+    streams and buffers, a host thread each) return, every call, bitwise the poses of the
+    host-buffer batch entry."""
+    torch = pytest.importorskip("torch")
+    from se3icp import datasets
+    pairs, _ = datasets.kitti_like_pairs(4, seed=4)
+    p = se3icp_mod.kitti_params()
+    host = se3icp_mod.register_batch(pairs, "se3_gicp", p)
+    src = np.ascontiguousarray(np.concatenate([a for a, _ in pairs]))
+    tgt = np.ascontiguousarray(np.concatenate([b for _, b in pairs]))
+    so = np.concatenate([[0], np.cumsum([a.shape[0] for a, _ in pairs])])
+    to = np.concatenate([[0], np.cumsum([b.shape[0] for _, b in pairs])])
+    d_src = torch.from_numpy(src).to("cuda:0")
+    d_tgt = torch.from_numpy(tgt).to("cuda:0")
+    torch.cuda.synchronize()
+    steps = 6
+    pipe = se3icp_mod.PipelinedBatchRunner(
+        lambda slot: se3icp_mod.DeviceBatchRunner(d_src.data_ptr(), so, d_tgt.data_ptr(), to, "se3_gicp", p,
+                                                  device=0 | (slot << 8), slots=steps), in_flight=2, steps=steps)
+    pipe.warm()
+    pipe.run_steps()
+    assert {pipe.owner(s) for s in range(steps)} <= {0, 1}
+    for s in range(steps):
+        res = pipe.results(s)
+        assert len(res) == len(host)
+        for i, (a, b) in enumerate(zip(res, host)):
+            assert np.array_equal(a.T, b.T), (s, i, a.T - b.T)
+            assert (a.num_iterations, a.num_pure_se3_iterations) == (b.num_iterations, b.num_pure_se3_iterations)
+
+
 def _lrf_cloud(kind):
     from se3icp import datasets
     if kind == "kitti":

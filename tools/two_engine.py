@@ -5,6 +5,9 @@ pairs, all on one GPU.  Prints one JSON line per configuration (wall ms per batc
 of the repeats) and checks that every configuration returns bitwise the one-call poses.
 
 Usage (GPU box): python3 tools/two_engine.py [--groups 1 2 4] [--reps 3] [--pair-cache DIR]
+                [--stagger-ms 0 10 20]  (G = 2: the second half starts this much later)
+                [--pipeline R]  (also: two slots each registering the WHOLE batch R times from its
+                                 own thread, against one slot registering it 2R times)
 """
 import argparse
 import json
@@ -26,6 +29,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--pairs", type=int, default=64)
     ap.add_argument("--pair-cache", default="/tmp/se3icp_pairs")
+    ap.add_argument("--stagger-ms", type=float, nargs="*", default=[0.0])
+    ap.add_argument("--pipeline", type=int, default=0)
     a = ap.parse_args()
     import torch
     import se3icp
@@ -58,11 +63,18 @@ def main():
         runners = [se3icp.DeviceBatchRunner(ds.data_ptr(), so, dt.data_ptr(), to, "se3_gicp", params, device=g << 8,
                                             slots=1) for g, (ds, dt, so, to) in enumerate(blocks)]
 
+        stagger = 0.0
+
+        def run_late(r, delay):
+            if delay > 0:
+                time.sleep(delay)
+            r.run(0)
+
         def run_all():
             if G == 1:
                 runners[0].run(0)
                 return
-            th = [threading.Thread(target=r.run, args=(0,)) for r in runners]
+            th = [threading.Thread(target=run_late, args=(r, stagger * i / 1e3)) for i, r in enumerate(runners)]
             for t in th:
                 t.start()
             for t in th:
@@ -70,21 +82,56 @@ def main():
 
         run_all()  # warm-up (buffers, code)
         torch.cuda.synchronize()
-        times = []
-        for _ in range(a.reps):
-            t0 = time.perf_counter()
-            run_all()
-            torch.cuda.synchronize()
-            times.append(time.perf_counter() - t0)
-        res = [r for rn in runners for r in rn.results(0)]
-        its = sum(r.num_iterations for r in res)
-        T = np.stack([r.T for r in res])
-        if ref is None:
-            ref = T
-        same = bool(np.array_equal(T, ref))
-        ms = 1000.0 * statistics.median(times)
-        print(json.dumps({"groups": G, "pairs": a.pairs, "ms_per_batch": round(ms, 3), "iter_per_s": round(its / (ms / 1e3), 1),
-                          "times_ms": [round(1000 * t, 3) for t in times], "poses_equal_one_call": same}), flush=True)
+        for stagger in (a.stagger_ms if G == 2 else [0.0]):
+            times = []
+            for _ in range(a.reps):
+                t0 = time.perf_counter()
+                run_all()
+                torch.cuda.synchronize()
+                times.append(time.perf_counter() - t0)
+            res = [r for rn in runners for r in rn.results(0)]
+            its = sum(r.num_iterations for r in res)
+            T = np.stack([r.T for r in res])
+            if ref is None:
+                ref = T
+            same = bool(np.array_equal(T, ref))
+            ms = 1000.0 * statistics.median(times)
+            print(json.dumps({"groups": G, "stagger_ms": stagger, "pairs": a.pairs, "ms_per_batch": round(ms, 3),
+                              "iter_per_s": round(its / (ms / 1e3), 1), "times_ms": [round(1000 * t, 3) for t in times],
+                              "poses_equal_one_call": same}), flush=True)
+    if a.pipeline > 0:
+        # whole batches back to back: one slot 2R calls, against two slots R calls each from
+        # their own threads (calls of the two slots drift out of step)
+        ds, dt, so, to = block(0, a.pairs)
+        torch.cuda.synchronize()
+        rs = [se3icp.DeviceBatchRunner(ds.data_ptr(), so, dt.data_ptr(), to, "se3_gicp", params, device=k << 8, slots=1)
+              for k in range(2)]
+        for r in rs:
+            r.run(0)
+        torch.cuda.synchronize()
+        its = sum(r.num_iterations for r in rs[0].results(0))
+        t0 = time.perf_counter()
+        for _ in range(2 * a.pipeline):
+            rs[0].run(0)
+        torch.cuda.synchronize()
+        one = time.perf_counter() - t0
+
+        def loop(r):
+            for _ in range(a.pipeline):
+                r.run(0)
+
+        th = [threading.Thread(target=loop, args=(r,)) for r in rs]
+        t0 = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        torch.cuda.synchronize()
+        two = time.perf_counter() - t0
+        same = bool(np.array_equal(np.stack([r.T for r in rs[1].results(0)]), np.stack([r.T for r in rs[0].results(0)])))
+        print(json.dumps({"pipeline_calls": 2 * a.pipeline, "pairs": a.pairs,
+                          "one_slot_iter_per_s": round(2 * a.pipeline * its / one, 1),
+                          "two_slots_iter_per_s": round(2 * a.pipeline * its / two, 1), "poses_equal": same}), flush=True)
 
 
 if __name__ == "__main__":
