@@ -12,7 +12,9 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 WA="--workload $W"
 [ "$W" = "C2u" ] && WA="--workload C2 --c2-cloud unique"
-B="python3 bench.py $WA --steps 3 --warmup 1 --cpu-baseline off --secondary off --pair-cache /tmp/se3icp_pairs"
+# (one call at a time: the line's kernel figures come from isolated calls, so the traced
+# kernel averages must too; BENCH_CMD below is the default, calls in flight)
+B="python3 bench.py $WA --steps 3 --warmup 1 --in-flight 1 --cpu-baseline off --secondary off --pair-cache /tmp/se3icp_pairs"
 SQ1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU"
 SQ2="SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_SALU SQ_WAIT_INST_LDS"
 T="${TAG}_${W}"
