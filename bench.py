@@ -187,10 +187,11 @@ def main():
     ap.add_argument("--shard", choices=["contiguous", "balanced"], default="contiguous",
                     help="pairs per rank: contiguous blocks of the batch, or a cost-balanced assignment (greedy by "
                          "point count over the whole batch, sharding.shard_balanced)")
-    ap.add_argument("--in-flight", type=int, default=3,
-                    help="calls in flight per GPU (engine slots, one host thread each); 1: one call at a time. "
-                         "C4, 20 steps (iter/s): 1 / 2 / 3 / 4 in flight = 14,416 / 15,207 / 15,409 / 15,336; "
-                         "its 8-pair shard 11,318 / 12,767 / 13,198 / 13,453")
+    ap.add_argument("--in-flight", type=int, default=0,
+                    help="calls in flight per GPU (engine slots, one host thread each); 1: one call at a time; "
+                         "0 (default): in_flight_for(pairs per call).  C4, 20 steps (iter/s): 1 / 2 / 3 / 4 in "
+                         "flight = 14,416 / 15,207 / 15,409 / 15,336; its 8-pair shard 11,318 / 12,767 / 13,198 / "
+                         "13,453")
     ap.add_argument("--secondary", choices=["auto", "off"], default="auto",
                     help="C4 at N=1: also time one 8-pair shard on this GPU (the per-GPU work of the 8-GPU job)")
     args = ap.parse_args()
@@ -283,6 +284,9 @@ def main():
     # streams and buffers, one host thread each: PipelinedBatchRunner) -- the value; then the
     # same K steps one call at a time (single_call), whose isolated kernel and phase times
     # feed the per-kernel lines and rooflines below.
+    if args.in_flight <= 0:
+        args.in_flight = in_flight_for(count)
+
     def make_runner(slot):
         return se3icp.DeviceBatchRunner(d_src.data_ptr(), src_off, d_tgt.data_ptr(), tgt_off, W["method"], params,
                                         device=devi | (slot << 8), slots=max(1, args.steps))
@@ -422,7 +426,8 @@ def main():
             "cpu_baseline": None,
         }
         if args.workload == "C4" and world == 1 and args.secondary == "auto" and len(pairs) > 8:
-            out["secondary_8_pair_shard_one_gpu"] = bench_shard8(pairs, W, params, dev, devi, in_flight=args.in_flight)
+            out["secondary_8_pair_shard_one_gpu"] = bench_shard8(pairs, W, params, dev, devi,
+                                                                 in_flight=in_flight_for(8) if args.in_flight > 1 else 1)
         if args.cpu_baseline == "auto":
             # rank 0's own pairs on the node's host (the same host for every rank), after the
             # timed region; at N > 1 the whole job's value is compared with it
@@ -606,6 +611,13 @@ def reduce_roofline(res, pairs, W, red_ms, wl):
             "note": "one launch pair per loop iteration for every active pair of the batch (HIP events around the "
                     "two kernels in the profiled step); the 28 sums per pair are then solved on the device "
                     "(k_reduce_final); traffic = both kernels' PMC bytes per launch from this workload's pass"}
+
+
+def in_flight_for(pairs_per_call: int) -> int:
+    """Calls in flight per GPU by default: the smaller the call, the more of its loop is
+    latency-bound and the more a further call in flight fills (measured at C4: 64 pairs
+    best at 3, 8 pairs at 4)."""
+    return 4 if pairs_per_call <= 16 else 3
 
 
 def bench_shard8(pairs, W, params, dev, devi, steps=3, in_flight=1):
