@@ -408,6 +408,9 @@ def main():
                 "in_flight": args.in_flight,
             },
             "in_flight": args.in_flight,
+            # each call's own wall time in the timed region (the calls in flight beside it): the
+            # latency a caller sees, against ms_per_step's amortized time
+            "ms_per_call": round(1000.0 * float(np.mean([pipe.call_seconds(s) for s in range(args.steps)])), 3),
             "single_call": single,
             "pairs_per_sec": round(total_pairs / elapsed, 4),
             "loop_iterations_per_sec": round(iters_all / loop_s, 3) if loop_s > 0 else None,

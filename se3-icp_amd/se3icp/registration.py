@@ -295,6 +295,7 @@ class PipelinedBatchRunner:
         self.steps = max(1, int(steps))
         self._runners = [runner_factory(k) for k in range(self.in_flight)]
         self._owner = [-1] * self.steps
+        self._wall = [0.0] * self.steps  # each call's wall time (s): its latency with the others in flight
 
     def warm(self) -> None:
         """One untimed call per slot (its buffers and code), into result buffer 0."""
@@ -302,6 +303,8 @@ class PipelinedBatchRunner:
             r.run(0)
 
     def run_steps(self, steps: int | None = None) -> None:
+        import time
+
         n = self.steps if steps is None else min(int(steps), self.steps)
         nxt = [0]
         err: list[BaseException] = []
@@ -315,7 +318,9 @@ class PipelinedBatchRunner:
                     nxt[0] = s + 1
                     self._owner[s] = k
                 try:
+                    t0 = time.perf_counter()
                     self._runners[k].run(s)
+                    self._wall[s] = time.perf_counter() - t0
                 except BaseException as e:  # noqa: BLE001 (re-raised by the caller's thread)
                     with self._lock:
                         err.append(e)
@@ -324,7 +329,9 @@ class PipelinedBatchRunner:
         if self.in_flight == 1:
             for s in range(n):
                 self._owner[s] = 0
+                t0 = time.perf_counter()
                 self._runners[0].run(s)
+                self._wall[s] = time.perf_counter() - t0
             return
         import threading
 
@@ -338,6 +345,10 @@ class PipelinedBatchRunner:
 
     def owner(self, s: int) -> int:
         return self._owner[s]
+
+    def call_seconds(self, s: int) -> float:
+        """Wall time of call s (from its start to its return, others in flight beside it)."""
+        return self._wall[s]
 
     def results(self, s: int) -> list[PairResult]:
         return self._runners[self._owner[s]].results(s)
