@@ -635,6 +635,39 @@ def test_pipelined_runner_equals_register_batch(se3icp_mod):
             assert (a.num_iterations, a.num_pure_se3_iterations) == (b.num_iterations, b.num_pure_se3_iterations)
 
 
+def test_in_flight_slots_with_different_batches_are_isolated(se3icp_mod):
+    """Calls in flight on different engine slots with DIFFERENT batches (a KITTI-like gicp
+    batch beside an RGB-D pt2pl batch with confidences off, then swapped) return bitwise the
+    results of each batch registered alone: the slots share no buffer or state."""
+    torch = pytest.importorskip("torch")
+    from se3icp import datasets
+    ka, _ = datasets.kitti_like_pairs(3, seed=4)
+    rb, _ = datasets.rgbd_pairs(6, seed=5, stride=4)
+    jobs = [(ka, "se3_gicp", se3icp_mod.kitti_params()), (rb, "se3_pt2pl", se3icp_mod.lounge_params())]
+    alone = [se3icp_mod.register_batch(pairs, m, p) for pairs, m, p in jobs]
+    dev = []
+    for pairs, m, p in jobs:
+        src = np.ascontiguousarray(np.concatenate([a for a, _ in pairs]))
+        tgt = np.ascontiguousarray(np.concatenate([b for _, b in pairs]))
+        so = np.concatenate([[0], np.cumsum([a.shape[0] for a, _ in pairs])])
+        to = np.concatenate([[0], np.cumsum([b.shape[0] for _, b in pairs])])
+        dev.append((torch.from_numpy(src).to("cuda:0"), so, torch.from_numpy(tgt).to("cuda:0"), to, m, p))
+    torch.cuda.synchronize()
+    for order in ((0, 1), (1, 0)):
+        def factory(slot, order=order):
+            ds, so, dt, to, m, p = dev[order[slot]]
+            return se3icp_mod.DeviceBatchRunner(ds.data_ptr(), so, dt.data_ptr(), to, m, p, device=0 | (slot << 8),
+                                                slots=4)
+        pipe = se3icp_mod.PipelinedBatchRunner(factory, in_flight=2, steps=4)
+        pipe.warm()
+        pipe.run_steps()
+        for s in range(4):
+            job = order[pipe.owner(s)]
+            for i, (a, b) in enumerate(zip(pipe.results(s), alone[job])):
+                assert np.array_equal(a.T, b.T), (order, s, job, i, a.T - b.T)
+                assert a.num_iterations == b.num_iterations, (order, s, job, i)
+
+
 def _lrf_cloud(kind):
     from se3icp import datasets
     if kind == "kitti":
