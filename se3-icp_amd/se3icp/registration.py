@@ -16,6 +16,8 @@ examples/benchmark_kitti.cpp:120-197 and examples/benchmark_lounge.cpp:154-235.
 from __future__ import annotations
 
 import ctypes as C
+import threading
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -288,8 +290,6 @@ class PipelinedBatchRunner:
     result buffers (DeviceBatchRunner; tests pass stand-ins)."""
 
     def __init__(self, runner_factory, in_flight: int = 2, steps: int = 1):
-        import threading
-
         self._lock = threading.Lock()
         self.in_flight = max(1, int(in_flight))
         self.steps = max(1, int(steps))
@@ -303,8 +303,6 @@ class PipelinedBatchRunner:
             r.run(0)
 
     def run_steps(self, steps: int | None = None) -> None:
-        import time
-
         n = self.steps if steps is None else min(int(steps), self.steps)
         nxt = [0]
         err: list[BaseException] = []
@@ -333,8 +331,6 @@ class PipelinedBatchRunner:
                 self._runners[0].run(s)
                 self._wall[s] = time.perf_counter() - t0
             return
-        import threading
-
         th = [threading.Thread(target=worker, args=(k,)) for k in range(self.in_flight)]
         for t in th:
             t.start()
