@@ -773,6 +773,9 @@ __global__ __launch_bounds__(kLevThreads) void k_tree_level(TreeView t, int leve
 #ifndef SE3ICP_TREE_EMPTY_FALLBACK
 #define SE3ICP_TREE_EMPTY_FALLBACK 1
 #endif
+#ifndef SE3ICP_TREE_SRC_ORDER_ONLY
+#define SE3ICP_TREE_SRC_ORDER_ONLY 1
+#endif
 constexpr int kLocalMax = 4096;  // power of two
 constexpr int kWaveSortPer = 8;  // sub-nodes of <= 512 points: register sort by one wave
 constexpr int kLocalThreads = 512;
@@ -1150,6 +1153,10 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
     // inverse, f32 and f64 vectors (the layouts k_tree_finish writes) and the leaf's box
     // (inflated as k_tree_leafbox does)
     const bool want64 = (t.tvec64 != nullptr) & !((t.vec64_sources_only != 0) & ((c & 1) != 0));
+    // a source cloud of the loop's 12-D trees (even ids): the searches walk the TARGET trees
+    // only, so a source tree is its order (perm / pos, the queries' chunks) and its f64
+    // translation rows -- no f32 rows, no boxes, and no gather of its 48-B input rows
+    const bool order_only = SE3ICP_TREE_SRC_ORDER_ONLY && (D == 12) && (t.vec64_sources_only != 0) && ((c & 1) == 0);
     const int R = t.L - G;  // levels of the subtree below its root
     const int lane = tid & 63, wv = tid >> 6;
     const size_t bbase = (size_t)c * t.nnodes * D;
@@ -1177,7 +1184,7 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
             const int src = cl.off + pq[b];
 #pragma unroll
             for (int d = 0; d < D; ++d) v[b][d] = 0.0f;
-            if (inq[b]) {
+            if ((int)inq[b] & (int)!order_only) {
                 if constexpr (D == 12) {
                     const float4* r = reinterpret_cast<const float4*>(t.vec + (size_t)src * 12);
 #pragma unroll
@@ -1213,7 +1220,8 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
             if (in) {
                 t.perm[g] = p;
                 t.pos[src] = A + x;
-                if constexpr (D == 12) {
+                if (order_only) {
+                } else if constexpr (D == 12) {
                     float4* o = reinterpret_cast<float4*>(t.tvec + (size_t)g * 12);
 #pragma unroll
                     for (int k = 0; k < 3; ++k) o[k] = make_float4(v[b][4 * k], v[b][4 * k + 1], v[b][4 * k + 2], v[b][4 * k + 3]);
@@ -1229,6 +1237,7 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
                     }
                 }
             }
+            if (order_only) continue;  // (wave-uniform)
             const size_t hb = bbase + (size_t)tree_heap(t.L, leaf) * D;
 #pragma unroll
             for (int d = 0; d < D; ++d) {
@@ -1253,7 +1262,7 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
     tq[3] = __builtin_amdgcn_s_memrealtime();
 #endif
     __syncthreads();
-    for (int rr = R - 1; rr >= 0; --rr) {
+    for (int rr = order_only ? -1 : R - 1; rr >= 0; --rr) {
         for (int it = tid; it < (D << rr); it += kLocalThreads) {
             const int j = it / D, d = it % D;
             const size_t h = (size_t)tree_heap(G + rr, (i << rr) + j);
@@ -1337,6 +1346,8 @@ __global__ __launch_bounds__(256) void k_tree_leafbox(TreeView t) {
 // block per cloud)
 __global__ __launch_bounds__(1024) void k_tree_up(TreeView t, int top) {
     const int c = blockIdx.x;
+    // (a loop source cloud's 12-D tree has no boxes: see k_tree_local's order_only)
+    if (SE3ICP_TREE_SRC_ORDER_ONLY && (t.D == 12) && (t.vec64_sources_only != 0) && ((c & 1) == 0)) return;
     for (int l = top - 1; l >= 0; --l) {
         const int items = (1 << l) * t.D;
         for (int it = threadIdx.x; it < items; it += blockDim.x) {
