@@ -1154,8 +1154,8 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
     // (inflated as k_tree_leafbox does)
     const bool want64 = (t.tvec64 != nullptr) & !((t.vec64_sources_only != 0) & ((c & 1) != 0));
     // a source cloud of the loop's 12-D trees (even ids): the searches walk the TARGET trees
-    // only, so a source tree is its order (perm / pos, the queries' chunks) and its f64
-    // translation rows -- no f32 rows, no boxes, and no gather of its 48-B input rows
+    // only, so a source tree is its order (perm: the queries' chunks) and its f64 translation
+    // rows -- no inverse, no f32 rows, no boxes, and no gather of its 48-B input rows
     const bool order_only = SE3ICP_TREE_SRC_ORDER_ONLY && (D == 12) && (t.vec64_sources_only != 0) && ((c & 1) == 0);
     const int R = t.L - G;  // levels of the subtree below its root
     const int lane = tid & 63, wv = tid >> 6;
@@ -1219,13 +1219,14 @@ __global__ __launch_bounds__(kLocalThreads) __attribute__((amdgpu_waves_per_eu(4
             const int g = cl.off + A + x, src = cl.off + p;
             if (in) {
                 t.perm[g] = p;
-                t.pos[src] = A + x;
-                if (order_only) {
+                if (order_only) {  // (pos is read for target clouds only: the previous match's slot)
                 } else if constexpr (D == 12) {
+                    t.pos[src] = A + x;
                     float4* o = reinterpret_cast<float4*>(t.tvec + (size_t)g * 12);
 #pragma unroll
                     for (int k = 0; k < 3; ++k) o[k] = make_float4(v[b][4 * k], v[b][4 * k + 1], v[b][4 * k + 2], v[b][4 * k + 3]);
                 } else {
+                    t.pos[src] = A + x;
 #pragma unroll
                     for (int d = 0; d < D; ++d) t.tvec[(size_t)d * ld + g] = v[b][d];
                 }
